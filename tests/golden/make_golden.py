@@ -1,0 +1,111 @@
+"""Generate the golden fixtures in tests/golden/*.npz FROM THE REFERENCE ITSELF.
+
+Run in the survey container only (needs /root/reference, never present on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+It imports the reference's own CorrBlock (model/corr.py:12-60) and coords_grid
+(model/utils.py:24-27), feeds it inputs from tests/golden/prng.py (portable; only seeds are
+stored) and records its outputs.  The fixtures are data (inputs' seeds + reference outputs),
+never reference source.  Backward goldens come from the reference under torch autograd.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import warnings
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import prng  # noqa: E402
+
+REF = "/root/reference"
+sys.dont_write_bytecode = True
+sys.path.insert(0, REF)
+warnings.filterwarnings("ignore")
+from model.corr import CorrBlock  # noqa: E402  (reference)
+
+torch.set_num_threads(8)
+
+
+def fmaps(seed, B, D, H, W):
+    return prng.gauss(seed, (B, D, H, W)), prng.gauss(seed + 1, (B, D, H, W))
+
+
+def ref_build(f1, f2, L, r):
+    return CorrBlock(torch.from_numpy(f1), torch.from_numpy(f2), num_levels=L, radius=r)
+
+
+def save(name, **arrs):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **arrs)
+    print(f"{name}: {os.path.getsize(path) / 1e6:.2f} MB")
+
+
+def case_build_lookup(name, seed, B, D, H, W, L, r, sigmas, store_pyramid=True):
+    f1, f2 = fmaps(seed, B, D, H, W)
+    cb = ref_build(f1, f2, L, r)
+    out = {"meta": np.array([seed, B, D, H, W, L, r], np.int64),
+           "sigmas": np.array(sigmas, np.float32)}
+    if store_pyramid:
+        for l, p in enumerate(cb.corr_pyramid):
+            out[f"pyr{l}"] = p.numpy()
+    corr6 = CorrBlock.corr(torch.from_numpy(f1), torch.from_numpy(f2))
+    out["corr_shape"] = np.array(corr6.shape, np.int64)
+    for k, s in enumerate(sigmas):
+        c = prng.lookup_coords(seed + 100 + k, B, H, W, s)
+        out[f"coords{k}"] = c
+        out[f"look{k}"] = cb(torch.from_numpy(c)).numpy()
+    c = prng.special_coords(B, H, W)
+    out["coords_special"] = c
+    out["look_special"] = cb(torch.from_numpy(c)).numpy()
+    save(name, **out)
+
+
+def case_backward(name, seed, B, D, H, W, L, r, iters):
+    f1, f2 = fmaps(seed, B, D, H, W)
+    t1 = torch.from_numpy(f1).requires_grad_(True)
+    t2 = torch.from_numpy(f2).requires_grad_(True)
+    cb = CorrBlock(t1, t2, num_levels=L, radius=r)
+    K = (2 * r + 1) ** 2
+    loss = 0.0
+    for t in range(iters):
+        c = prng.lookup_coords(seed + 200 + t, B, H, W, 2.0 + t)
+        g = prng.gauss(seed + 300 + t, (B, L * K, H, W))
+        o = cb(torch.from_numpy(c))
+        loss = loss + (o * torch.from_numpy(g)).sum()
+    loss.backward()
+    save(name, meta=np.array([seed, B, D, H, W, L, r, iters], np.int64),
+         df1=t1.grad.numpy(), df2=t2.grad.numpy())
+
+
+def case_dsec_spot(name, seed):
+    """DSEC shape (B=1, 60x80, D=256): slices + fp64 checksums only (full pyramid is 122 MB)."""
+    B, D, H, W, L, r = 1, 256, 60, 80, 4, 4
+    f1, f2 = fmaps(seed, B, D, H, W)
+    cb = ref_build(f1, f2, L, r)
+    q = np.array([0, 1, 79, 80, 2399, 2400, 4719, 4799, 1234, 3000, 4321, 17, 555, 2048, 3333, 4000])
+    out = {"meta": np.array([seed, B, D, H, W, L, r], np.int64), "q": q}
+    for l, p in enumerate(cb.corr_pyramid):
+        p = p.numpy()
+        out[f"pyr{l}_rows"] = p[q]
+        out[f"pyr{l}_sum"] = np.array([p.astype(np.float64).sum(), np.abs(p).astype(np.float64).sum()])
+    c = prng.lookup_coords(seed + 100, B, H, W, 8.0)
+    o = cb(torch.from_numpy(c)).numpy()
+    out["look_q"] = o.reshape(B, -1, H * W)[:, :, q]
+    out["look_sum"] = np.array([o.astype(np.float64).sum(), np.abs(o).astype(np.float64).sum()])
+    save(name, **out)
+
+
+if __name__ == "__main__":
+    case_build_lookup("g_b1_d32_16x16", 11, 1, 32, 16, 16, 4, 4, [0.0, 3.0, 20.0])
+    case_build_lookup("g_b2_d256_17x23", 12, 2, 256, 17, 23, 4, 4, [8.0])
+    case_build_lookup("g_b2_d64_16x20_L2r3", 13, 2, 64, 16, 20, 2, 3, [5.0])
+    case_build_lookup("g_degenerate_b1_d32_12x16", 14, 1, 32, 12, 16, 4, 4, [3.0])
+    case_build_lookup("g_degenerate_b1_d16_15x21", 15, 1, 16, 15, 21, 4, 4, [3.0])
+    case_backward("g_bwd_b2_d16_18x24", 16, 2, 16, 18, 24, 4, 4, 12)
+    case_backward("g_bwd_b1_d32_17x23_L2r3", 17, 1, 32, 17, 23, 2, 3, 3)
+    case_dsec_spot("g_dsec_spot", 18)
