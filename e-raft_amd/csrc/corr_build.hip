@@ -1,0 +1,305 @@
+// corr_build.hip — all-pairs correlation + fused 4-level avg-pool pyramid on gfx950 MFMA.
+//
+// Replaces CorrBlock.corr (model/corr.py:52-60: matmul(F1^T, F2) / sqrt(D)) and the pyramid
+// loop of CorrBlock.__init__ (model/corr.py:21-27: avg_pool2d(2, stride 2) x (L-1)).
+//
+// One workgroup (4 waves) owns a tile of 128 query pixels x one 8x16 patch of target pixels
+// (128 targets).  K = D is staged through LDS in 32-deep chunks (double-buffered, register
+// prefetch of chunk c+1 while chunk c feeds the MFMAs).  Each wave computes 64 queries x an
+// 8x8 target sub-patch with v_mfma_f32_32x32x2_f32 (exact fp32: a k-ordered fmaf chain):
+// A = targets (MFMA rows), B = queries (MFMA columns), so every lane ends up owning ONE query
+// and a 4x8 block of target pixels (lanes l, l+32 hold the two 4-wide halves of the 8x8).
+// The epilogue applies 1/sqrt(D), writes level 0, and pools levels 1..3 in registers
+// (level 3 needs one cross-half shuffle) — every pyramid level leaves the chip exactly once.
+#include <algorithm>
+#include <cmath>
+
+#include "corr_common.h"
+
+namespace corr {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kBQ = 128;  // queries per tile
+constexpr int kPH = 8;    // target patch rows
+constexpr int kPW = 16;   // target patch cols  (kPH * kPW = 128 targets per tile)
+constexpr int kBK = 32;   // k-chunk staged in LDS
+constexpr int kThreads = 256;
+
+struct BuildParams {
+    const float *f1;
+    const float *f2;
+    float *lvl[kFusedLevels];
+    int B, D, H, W, N;
+    int nlev;           // levels written by the epilogue (1..4)
+    int nq, npx, npy;   // query blocks, patch columns, patch rows
+    float inv_s, s;
+    int exact_mul;      // sqrt(D) is a power of two: x * (1/s) == x / s bit-for-bit
+};
+
+__device__ __forceinline__ int xcd_swizzle(int bid, int nwg) {
+    // Blocks are dealt round-robin to the 8 XCDs; give each XCD a contiguous range of
+    // tiles (which share the query slab) — bijective for any nwg (speed only).
+    const int xcd = bid & 7, loc = bid >> 3, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+__device__ __forceinline__ float pool4(float a, float b, float c, float d) {
+    // avg_pool2d(2,2) on CPU ATen: ((a + b) + c) + d, then * 1/4 (bit-identical).
+    float t = a + b;
+    t = t + c;
+    t = t + d;
+    return t * 0.25f;
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kThreads, 2) void corr_build_kernel(BuildParams p) {
+    __shared__ __attribute__((aligned(16))) float sm[2][2][kBK][128];  // [stage][Q,T][k][idx]
+
+    const int tile = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int px = tile % p.npx;
+    const int py = (tile / p.npx) % p.npy;
+    const int qb = (tile / (p.npx * p.npy)) % p.nq;
+    const int b = tile / (p.npx * p.npy * p.nq);
+    const int q0 = qb * kBQ;
+    const int N = p.N, W = p.W, H = p.H, D = p.D;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int wv = tid >> 6, wq = wv >> 1, wt = wv & 1;
+
+    // ---- staging assignment: rows k = kr + 8*i (i = 0..3), 4 consecutive idx at c4 ----
+    const int kr = tid >> 5;
+    const int c4 = (tid & 31) * 4;
+    const int qidx = q0 + c4;  // query of staged element e: qidx + e
+    // target patch layout inside a tile: idx = wt*64 + tt*32 + y4*8 + x8
+    const int sy = ((c4 >> 5) & 1) * 4 + ((c4 >> 3) & 3);
+    const int sx = (c4 >> 6) * 8 + (c4 & 7);
+    const int tY = py * kPH + sy, tX = px * kPW + sx;
+    const size_t tOff = (size_t)tY * W + tX;
+    const float *f1b = p.f1 + (size_t)b * D * N;
+    const float *f2b = p.f2 + (size_t)b * D * N;
+
+    float4 rq[4], rt[4];
+    auto load_chunk = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = k0 + kr + 8 * i;
+            const bool kv = k < D;
+            if (VEC) {
+                rq[i] = (kv && qidx < N) ? *reinterpret_cast<const float4 *>(f1b + (size_t)k * N + qidx)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+                rt[i] = (kv && tY < H && tX < W)
+                            ? *reinterpret_cast<const float4 *>(f2b + (size_t)k * N + tOff)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                float qv[4], tv[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    qv[e] = (kv && qidx + e < N) ? f1b[(size_t)k * N + qidx + e] : 0.f;
+                    tv[e] = (kv && tY < H && tX + e < W) ? f2b[(size_t)k * N + tOff + e] : 0.f;
+                }
+                rq[i] = make_float4(qv[0], qv[1], qv[2], qv[3]);
+                rt[i] = make_float4(tv[0], tv[1], tv[2], tv[3]);
+            }
+        }
+    };
+    auto store_chunk = [&](int st) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            *reinterpret_cast<float4 *>(&sm[st][0][kr + 8 * i][c4]) = rq[i];
+            *reinterpret_cast<float4 *>(&sm[st][1][kr + 8 * i][c4]) = rt[i];
+        }
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nchunks = (D + kBK - 1) / kBK;
+    load_chunk(0);
+    store_chunk(0);
+    __syncthreads();
+
+    for (int c = 0; c < nchunks; ++c) {
+        const int st = c & 1;
+        if (c + 1 < nchunks) load_chunk((c + 1) * kBK);
+        const float *Qs = &sm[st][0][0][0];
+        const float *Ts = &sm[st][1][0][0];
+#pragma unroll
+        for (int s = 0; s < kBK / 2; ++s) {
+            const int k = 2 * s + h;
+            const float b0 = Qs[k * 128 + wq * 64 + l32];
+            const float b1 = Qs[k * 128 + wq * 64 + 32 + l32];
+            const float a0 = Ts[k * 128 + wt * 64 + l32];
+            const float a1 = Ts[k * 128 + wt * 64 + 32 + l32];
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        }
+        if (c + 1 < nchunks) store_chunk(st ^ 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: scale, level 0, in-register pyramid ----
+    // acc[qt][tt][r]: query q0 + wq*64 + qt*32 + l32, target (y, x) of the wave's 8x8
+    // sub-patch with y = tt*4 + (r >> 2), x = 4h + (r & 3)   (32x32 C/D map).
+    const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
+    const int X0 = px * kPW + wt * 8 + 4 * h, Y0 = py * kPH;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+        const int q = q0 + wq * 64 + qt * 32 + l32;
+        const bool qok = q < N;
+        const size_t qrow = (size_t)b * N + q;
+        float v[8][4];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float x = acc[qt][tt][r];
+                v[tt * 4 + (r >> 2)][r & 3] = p.exact_mul ? x * p.inv_s : x / p.s;
+            }
+        // level 0
+        if (qok) {
+            float *o = p.lvl[0] + qrow * N;
+#pragma unroll
+            for (int y = 0; y < 8; ++y) {
+                const int Y = Y0 + y;
+                if (Y < H) {
+                    if (VEC) {
+                        if (X0 < W)
+                            *reinterpret_cast<float4 *>(o + (size_t)Y * W + X0) =
+                                make_float4(v[y][0], v[y][1], v[y][2], v[y][3]);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (X0 + e < W) o[(size_t)Y * W + X0 + e] = v[y][e];
+                    }
+                }
+            }
+        }
+        if (p.nlev < 2) continue;
+        // level 1: 4 rows x 2 cols per lane
+        float l1[4][2];
+#pragma unroll
+        for (int y = 0; y < 4; ++y)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+                l1[y][x] = pool4(v[2 * y][2 * x], v[2 * y][2 * x + 1], v[2 * y + 1][2 * x],
+                                 v[2 * y + 1][2 * x + 1]);
+        if (qok) {
+            float *o = p.lvl[1] + qrow * (size_t)(H1 * W1);
+#pragma unroll
+            for (int y = 0; y < 4; ++y)
+#pragma unroll
+                for (int x = 0; x < 2; ++x) {
+                    const int Y = py * 4 + y, X = (X0 >> 1) + x;
+                    if (Y < H1 && X < W1) o[Y * W1 + X] = l1[y][x];
+                }
+        }
+        if (p.nlev < 3) continue;
+        // level 2: 2 rows x 1 col per lane
+        float l2[2];
+#pragma unroll
+        for (int y = 0; y < 2; ++y) l2[y] = pool4(l1[2 * y][0], l1[2 * y][1], l1[2 * y + 1][0], l1[2 * y + 1][1]);
+        if (qok) {
+            float *o = p.lvl[2] + qrow * (size_t)(H2 * W2);
+            const int X = X0 >> 2;
+#pragma unroll
+            for (int y = 0; y < 2; ++y) {
+                const int Y = py * 2 + y;
+                if (Y < H2 && X < W2) o[Y * W2 + X] = l2[y];
+            }
+        }
+        if (p.nlev < 4) continue;
+        // level 3: the 2x2 level-2 block is split across lane halves h = 0 (x = 0), 1 (x = 1)
+        const float o0 = __shfl_xor(l2[0], 32);
+        const float o1 = __shfl_xor(l2[1], 32);
+        if (h == 0 && qok) {
+            const float l3 = pool4(l2[0], o0, l2[1], o1);
+            const int Y = py, X = X0 >> 3;
+            if (Y < H3 && X < W3) p.lvl[3][qrow * (size_t)(H3 * W3) + Y * W3 + X] = l3;
+        }
+    }
+}
+
+// Levels beyond the fused four: plain 2x2 average pool of level l-1 into level l.
+__global__ __launch_bounds__(256) void pool2x2_kernel(const float *__restrict__ in,
+                                                      float *__restrict__ out, long BN, int H,
+                                                      int W) {
+    const int Ho = H >> 1, Wo = W >> 1;
+    const size_t total = (size_t)BN * Ho * Wo;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * blockDim.x) {
+        const size_t q = i / ((size_t)Ho * Wo);
+        const int rem = (int)(i - q * Ho * Wo);
+        const int y = rem / Wo, x = rem - y * Wo;
+        const float *I = in + q * H * W;
+        out[i] = pool4(I[(2 * y) * W + 2 * x], I[(2 * y) * W + 2 * x + 1], I[(2 * y + 1) * W + 2 * x],
+                       I[(2 * y + 1) * W + 2 * x + 1]);
+    }
+}
+
+bool is_pow2(float s) {
+    int e;
+    return std::frexp(s, &e) == 0.5f;
+}
+
+}  // namespace
+
+hipError_t launch_pool_levels(const LevelPtrs &pyr, int l_from, int levels, long BN, int H, int W,
+                              hipStream_t s) {
+    for (int l = l_from; l < levels; ++l) {
+        const int Hi = H >> (l - 1), Wi = W >> (l - 1);
+        const size_t total = (size_t)BN * (Hi >> 1) * (Wi >> 1);
+        const int grid = (int)std::min<size_t>((total + 255) / 256, 4096);
+        hipLaunchKernelGGL(pool2x2_kernel, dim3(grid), dim3(256), 0, s, pyr.p[l - 1], pyr.p[l], BN,
+                           Hi, Wi);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_build(const float *f1, const float *f2, int B, int D, int H, int W, int levels,
+                        const LevelPtrs &pyr, hipStream_t s) {
+    BuildParams p{};
+    p.f1 = f1;
+    p.f2 = f2;
+    p.B = B;
+    p.D = D;
+    p.H = H;
+    p.W = W;
+    p.N = H * W;
+    p.nlev = levels < kFusedLevels ? levels : kFusedLevels;
+    for (int l = 0; l < kFusedLevels; ++l) p.lvl[l] = l < p.nlev ? pyr.p[l] : nullptr;
+    p.nq = (p.N + kBQ - 1) / kBQ;
+    p.npx = (W + kPW - 1) / kPW;
+    p.npy = (H + kPH - 1) / kPH;
+    p.s = std::sqrt((float)D);
+    p.exact_mul = is_pow2(p.s);
+    p.inv_s = 1.0f / p.s;
+
+    // float4 staging / level-0 stores need 16-B aligned rows and patch columns.
+    const bool vec = (W % 4 == 0) && ((uintptr_t)pyr.p[0] % 16 == 0) &&
+                     ((uintptr_t)f1 % 16 == 0) && ((uintptr_t)f2 % 16 == 0);
+
+    const long tiles = (long)p.nq * p.npx * p.npy * B;
+    if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
+    if (vec)
+        hipLaunchKernelGGL(corr_build_kernel<true>, dim3((unsigned)tiles), dim3(kThreads), 0, s, p);
+    else
+        hipLaunchKernelGGL(corr_build_kernel<false>, dim3((unsigned)tiles), dim3(kThreads), 0, s, p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (levels > kFusedLevels) return launch_pool_levels(pyr, kFusedLevels, levels, (long)B * p.N, H, W, s);
+    return hipSuccess;
+}
+
+}  // namespace corr

@@ -1,0 +1,45 @@
+// Internal definitions shared by the gfx950 correlation kernels (not part of the C-ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/corr_mi355x.h"
+
+namespace corr {
+
+// Host-side launch arguments carrying the per-level pointers by value (no device-side
+// pointer table to allocate).
+struct LevelPtrs {
+    float *p[CORR_MAX_LEVELS];
+};
+struct ConstLevelPtrs {
+    const float *p[CORR_MAX_LEVELS];
+};
+
+// Set the thread-local error and return `code`.
+int fail(int code, const char *fmt, ...);
+// Map a HIP status to CORR_OK / CORR_EHIP (recording the message).
+int hip_status(hipError_t e, const char *what);
+
+// Launch entry points implemented in the .hip translation units (all asynchronous).
+hipError_t launch_build(const float *f1, const float *f2, int B, int D, int H, int W,
+                        int levels, const LevelPtrs &pyr, hipStream_t s);
+hipError_t launch_pool_levels(const LevelPtrs &pyr, int l_from, int levels, long BN, int H,
+                              int W, hipStream_t s);
+hipError_t launch_lookup(const ConstLevelPtrs &pyr, const float *coords, int B, int H, int W,
+                         int levels, int radius, float *out, hipStream_t s);
+hipError_t launch_lookup_bwd(const float *coords, const float *grad_out, int B, int H, int W,
+                             int levels, int radius, const LevelPtrs &gpyr, hipStream_t s);
+hipError_t launch_pool_bwd(const LevelPtrs &gpyr, long BN, int H, int W, int levels,
+                           hipStream_t s);
+size_t build_bwd_workspace(int B, int D, int H, int W);
+hipError_t launch_build_bwd(const float *grad_c, const float *f1, const float *f2, int B, int D,
+                            int H, int W, float *df1, float *df2, float *ws, hipStream_t s);
+
+// Number of levels the build kernel pools in its epilogue (8x8 target patches).
+constexpr int kFusedLevels = 4;
+
+}  // namespace corr

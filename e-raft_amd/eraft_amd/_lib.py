@@ -1,0 +1,137 @@
+"""ctypes binding of libcorr_mi355x.so (C-ABI: include/corr_mi355x.h).
+
+This is the ONLY path to the kernels: there is no CPU or eager-PyTorch fallback.  If the
+library is missing, or a tensor is not on a HIP device, calls raise.
+torch is imported first so that the library binds to the HIP runtime torch already loaded
+(both carry the SONAME libamdhip64.so.7), i.e. one runtime, one set of device pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+from .build import SO_PATH
+
+CORR_OK = 0
+CORR_EINVAL = -1
+CORR_EUNSUPPORTED = -2
+CORR_EHIP = -3
+MAX_LEVELS = 8
+MAX_RADIUS = 7
+
+EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr_lookup_bwd",
+           "corr_pool_bwd", "corr_build_bwd_workspace", "corr_build_bwd")
+
+_lib = None
+
+
+class CorrError(RuntimeError):
+    """A libcorr_mi355x call returned a negative status."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[corr {code}] {msg}")
+        self.code = code
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load (once) and type the library.  Raises if it has not been built."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    so = path or SO_PATH
+    if not os.path.exists(so):
+        raise RuntimeError(
+            f"{so} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(eraft_amd has no CPU fallback)")
+    lib = ctypes.CDLL(so)
+    vp, i, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    lib.corr_version.argtypes, lib.corr_version.restype = [], i
+    lib.corr_last_error.argtypes, lib.corr_last_error.restype = [], ctypes.c_char_p
+    lib.corr_build.argtypes = [vp, vp, i, i, i, i, i, vp, vp]
+    lib.corr_lookup.argtypes = [vp, vp, i, i, i, i, i, vp, vp]
+    lib.corr_lookup_bwd.argtypes = [vp, vp, i, i, i, i, i, vp, vp]
+    lib.corr_pool_bwd.argtypes = [vp, i, i, i, i, vp]
+    lib.corr_build_bwd_workspace.argtypes = [i, i, i, i]
+    lib.corr_build_bwd_workspace.restype = sz
+    lib.corr_build_bwd.argtypes = [vp, vp, vp, i, i, i, i, vp, vp, vp, sz, vp]
+    for f in ("corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd"):
+        getattr(lib, f).restype = i
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(rc: int):
+    if rc != CORR_OK:
+        raise CorrError(rc, load().corr_last_error().decode(errors="replace"))
+
+
+def _dev(t: torch.Tensor, name: str) -> int:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name} is on {t.device}: eraft_amd runs only on an MI355X (HIP) device")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32 (got {t.dtype})")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return t.data_ptr()
+
+
+def _ptrs(ts, name):
+    arr = (ctypes.c_void_p * len(ts))()
+    for k, t in enumerate(ts):
+        arr[k] = _dev(t, f"{name}[{k}]")
+    return arr
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def build(fmap1, fmap2, levels):
+    """corr_build into the caller-allocated level tensors ([B*H*W, 1, H>>l, W>>l])."""
+    B, D, H, W = fmap1.shape
+    a, b, pp = _dev(fmap1, "fmap1"), _dev(fmap2, "fmap2"), _ptrs(levels, "pyr")
+    with torch.cuda.device(fmap1.device):
+        _check(load().corr_build(a, b, B, D, H, W, len(levels), pp, _stream(fmap1)))
+
+
+def lookup(levels, coords, radius, out):
+    B, _, H, W = coords.shape
+    pp, c, o = _ptrs(levels, "pyr"), _dev(coords, "coords"), _dev(out, "out")
+    with torch.cuda.device(coords.device):
+        _check(load().corr_lookup(pp, c, B, H, W, len(levels), radius, o, _stream(coords)))
+
+
+def lookup_bwd(coords, grad_out, radius, grad_levels):
+    B, _, H, W = coords.shape
+    c, g, gp = _dev(coords, "coords"), _dev(grad_out, "grad_out"), _ptrs(grad_levels, "grad_pyr")
+    with torch.cuda.device(coords.device):
+        _check(load().corr_lookup_bwd(c, g, B, H, W, len(grad_levels), radius, gp, _stream(coords)))
+
+
+def pool_bwd(grad_levels, H, W):
+    BN = grad_levels[0].shape[0]
+    gp = _ptrs(grad_levels, "grad_pyr")
+    with torch.cuda.device(grad_levels[0].device):
+        _check(load().corr_pool_bwd(gp, BN, H, W, len(grad_levels), _stream(grad_levels[0])))
+
+
+def build_bwd(grad_c, fmap1, fmap2):
+    """Returns (dfmap1, dfmap2) for grad_c = dLoss/dcorr ([B*N, N] or any view of it)."""
+    B, D, H, W = fmap1.shape
+    for t, nm in ((grad_c, "grad_c"), (fmap1, "fmap1"), (fmap2, "fmap2")):
+        _dev(t, nm)
+    lib = load()
+    ws_bytes = lib.corr_build_bwd_workspace(B, D, H, W)
+    df1 = torch.empty_like(fmap1)
+    df2 = torch.empty_like(fmap2)
+    ws = torch.empty(max(1, ws_bytes // 4), dtype=torch.float32, device=fmap1.device)
+    with torch.cuda.device(fmap1.device):
+        _check(lib.corr_build_bwd(_dev(grad_c, "grad_c"), _dev(fmap1, "fmap1"), _dev(fmap2, "fmap2"),
+                                  B, D, H, W, _dev(df1, "df1"), _dev(df2, "df2"), ws.data_ptr(),
+                                  ws_bytes, _stream(fmap1)))
+    return df1, df2

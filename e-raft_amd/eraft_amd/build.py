@@ -1,0 +1,50 @@
+"""Compile libcorr_mi355x.so (the gfx950 HIP kernels + C-ABI) in-tree with hipcc.
+
+The .so lands in ``e-raft_amd/eraft_amd/_build/`` (git-ignored, but it travels to the GPU
+box with the gpurun snapshot).  No JIT cache, no torch C++ extension: the boundary is the
+plain C-ABI of include/corr_mi355x.h, loaded with ctypes.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(os.path.dirname(PKG), "csrc")
+OUT_DIR = os.path.join(PKG, "_build")
+SO_NAME = "libcorr_mi355x.so"
+SO_PATH = os.path.join(OUT_DIR, SO_NAME)
+SOURCES = ["corr_build.hip", "corr_lookup.hip", "corr_bwd.hip", "corr_api.cpp"]
+HEADERS = ["corr_common.h", os.path.join("..", "..", "include", "corr_mi355x.h")]
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# -ffp-contract=off: the lookup / pool arithmetic is specified op-by-op (each fp32 op rounds
+# once, fmaf only where the reference's ATen kernel fuses); the compiler must not contract.
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+         "-Wall"]
+
+
+def _stale() -> bool:
+    if not os.path.exists(SO_PATH):
+        return True
+    t = os.path.getmtime(SO_PATH)
+    deps = [os.path.join(SRC, s) for s in SOURCES + HEADERS] + [__file__]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_library(force: bool = False, verbose: bool = False) -> str:
+    """Build the shared library if any source is newer than it.  Returns its path."""
+    if not force and not _stale():
+        return SO_PATH
+    os.makedirs(OUT_DIR, exist_ok=True)
+    tmp = SO_PATH + ".tmp"
+    cmd = [HIPCC, *FLAGS, "-o", tmp, *[os.path.join(SRC, s) for s in SOURCES]]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, SO_PATH)
+    return SO_PATH
+
+
+if __name__ == "__main__":
+    print(build_library(force=True, verbose=True))

@@ -1,0 +1,177 @@
+"""Drop-in CorrBlock for E-RAFT on MI355X.
+
+Same constructor, call signature, attributes and output as the reference class
+(AhmedHumais/E-RAFT model/corr.py:12-60):
+
+    corr_fn = CorrBlock(fmap1, fmap2, num_levels=4, radius=4)   # eraft.py:108
+    corr    = corr_fn(coords1)                                  # eraft.py:129
+    vol     = CorrBlock.corr(fmap1, fmap2)                      # [B, H, W, 1, H, W]
+
+Swapping it into the reference model is a one-line import change.
+Every computation goes through libcorr_mi355x.so (gfx950 HIP kernels, C-ABI); there is no
+CPU or eager fallback — CPU tensors raise.
+
+Autograd (training, BASELINE config 4): gradients flow to fmap1 / fmap2 only (coords are
+detached by the caller, eraft.py:128, and the reference never needs d/dcoords).  Instead of
+materialising a dense pyramid gradient per lookup as torch autograd does, every lookup's
+backward accumulates into ONE gradient pyramid owned by this block; the build's backward
+then folds it (avg-pool backward) and runs the two MFMA GEMMs once.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def level_shapes(H: int, W: int, num_levels: int):
+    """avg_pool2d(2, stride 2) floor halving (corr.py:25-27)."""
+    return [(H >> l, W >> l) for l in range(num_levels)]
+
+
+def _alloc_pyramid(B: int, H: int, W: int, num_levels: int, like: torch.Tensor, zero=False):
+    """One allocation holding every level, viewed as the reference's [B*H*W, 1, H_l, W_l]."""
+    BN = B * H * W
+    shapes = level_shapes(H, W, num_levels)
+    sizes = [BN * h * w for h, w in shapes]
+    # keep every level 16-byte aligned (float4 paths)
+    offs, tot = [], 0
+    for s in sizes:
+        offs.append(tot)
+        tot += (s + 3) // 4 * 4
+    fn = torch.zeros if zero else torch.empty
+    buf = fn(tot, dtype=torch.float32, device=like.device)
+    return [buf[o:o + s].view(BN, 1, h, w) for o, s, (h, w) in zip(offs, sizes, shapes)]
+
+
+def _validate_fmaps(fmap1, fmap2, num_levels):
+    for t, nm in ((fmap1, "fmap1"), (fmap2, "fmap2")):
+        if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+            raise RuntimeError(f"{nm} must be a tensor on an MI355X (HIP) device: eraft_amd has no "
+                               "CPU fallback")
+    if fmap1.dim() != 4 or fmap1.shape != fmap2.shape:
+        raise ValueError(f"fmap1 / fmap2 must both be [B, D, H, W] (got {tuple(fmap1.shape)}, "
+                         f"{tuple(fmap2.shape)})")
+    if not (1 <= num_levels <= _lib.MAX_LEVELS):
+        raise ValueError(f"num_levels must be in [1, {_lib.MAX_LEVELS}]")
+    _, _, H, W = fmap1.shape
+    if (H >> (num_levels - 1)) < 1 or (W >> (num_levels - 1)) < 1:
+        # the reference raises inside avg_pool2d (corr.py:26)
+        raise RuntimeError(f"{H}x{W} feature maps are too small for {num_levels} pyramid levels")
+
+
+class _State:
+    """Per-block state shared by the build and lookup autograd nodes."""
+
+    __slots__ = ("levels", "grad_levels", "H", "W")
+
+    def __init__(self, H, W):
+        self.levels = None
+        self.grad_levels = None
+        self.H, self.W = H, W
+
+
+class _BuildFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, fmap1, fmap2, num_levels, state):
+        B, _, H, W = fmap1.shape
+        levels = _alloc_pyramid(B, H, W, num_levels, fmap1)
+        _lib.build(fmap1, fmap2, levels)
+        ctx.save_for_backward(fmap1, fmap2)
+        ctx.state = state
+        token = fmap1.new_zeros(())  # autograd anchor: every lookup depends on it
+        return (*levels, token)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        fmap1, fmap2 = ctx.saved_tensors
+        st = ctx.state
+        gl = st.grad_levels
+        direct = grads[:-1]
+        if any(g is not None for g in direct):
+            # gradients that reached corr_pyramid outside the lookups
+            if gl is None:
+                B, _, H, W = fmap1.shape
+                gl = _alloc_pyramid(B, H, W, len(direct), fmap1, zero=True)
+            for acc, g in zip(gl, direct):
+                if g is not None:
+                    acc.add_(g)
+        st.grad_levels = None
+        if gl is None:
+            return None, None, None, None
+        _lib.pool_bwd(gl, st.H, st.W)
+        df1, df2 = _lib.build_bwd(gl[0], fmap1, fmap2)
+        return df1, df2, None, None
+
+
+class _LookupFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, coords, token, radius, state):
+        levels = state.levels
+        B, _, H, W = coords.shape
+        K = (2 * radius + 1) ** 2
+        out = torch.empty((B, len(levels) * K, H, W), dtype=torch.float32, device=coords.device)
+        _lib.lookup(levels, coords, radius, out)
+        ctx.save_for_backward(coords)
+        ctx.radius = radius
+        ctx.state = state
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        (coords,) = ctx.saved_tensors
+        st = ctx.state
+        if st.grad_levels is None:
+            B, _, H, W = coords.shape
+            st.grad_levels = _alloc_pyramid(B, H, W, len(st.levels), coords, zero=True)
+        _lib.lookup_bwd(coords, grad_out.contiguous(), ctx.radius, st.grad_levels)
+        return None, torch.zeros((), dtype=torch.float32, device=coords.device), None, None
+
+
+class CorrBlock:
+    """MI355X-native replacement for model/corr.py:12 ``CorrBlock``."""
+
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4):
+        self.num_levels = num_levels
+        self.radius = radius
+        if not (0 <= radius <= _lib.MAX_RADIUS):
+            raise ValueError(f"radius must be in [0, {_lib.MAX_RADIUS}]")
+        _validate_fmaps(fmap1, fmap2, num_levels)
+        fmap1 = fmap1.contiguous()
+        fmap2 = fmap2.contiguous()
+        _, _, H, W = fmap1.shape
+        self._state = _State(H, W)
+        self._token = None
+        if torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad):
+            outs = _BuildFn.apply(fmap1, fmap2, num_levels, self._state)
+            self.corr_pyramid = list(outs[:-1])
+            self._token = outs[-1]
+        else:
+            B = fmap1.shape[0]
+            self.corr_pyramid = _alloc_pyramid(B, H, W, num_levels, fmap1)
+            _lib.build(fmap1.detach(), fmap2.detach(), self.corr_pyramid)
+        self._state.levels = [p.detach() for p in self.corr_pyramid]
+
+    def __call__(self, coords):
+        if coords.dim() != 4 or coords.shape[1] != 2:
+            raise ValueError(f"coords must be [B, 2, H, W] (got {tuple(coords.shape)})")
+        B, _, H, W = coords.shape
+        if B * H * W != self.corr_pyramid[0].shape[0] or (H, W) != (self._state.H, self._state.W):
+            raise ValueError("coords do not match the feature maps this block was built from")
+        # the reference accepts any strides (permute at corr.py:31); fp32 as in eraft.py:128
+        coords = coords.detach().contiguous()
+        if self._token is not None and torch.is_grad_enabled():
+            return _LookupFn.apply(coords, self._token, self.radius, self._state)
+        K = (2 * self.radius + 1) ** 2
+        out = torch.empty((B, self.num_levels * K, H, W), dtype=torch.float32, device=coords.device)
+        _lib.lookup(self._state.levels, coords, self.radius, out)
+        return out
+
+    @staticmethod
+    def corr(fmap1, fmap2):
+        """model/corr.py:52-60: all-pairs volume [B, H, W, 1, H, W] scaled by 1/sqrt(D)."""
+        _validate_fmaps(fmap1, fmap2, 1)
+        B, _, H, W = fmap1.shape
+        (lvl,) = _alloc_pyramid(B, H, W, 1, fmap1)
+        _lib.build(fmap1.detach().contiguous(), fmap2.detach().contiguous(), [lvl])
+        return lvl.view(B, H, W, 1, H, W)

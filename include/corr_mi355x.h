@@ -1,0 +1,102 @@
+/*
+ * corr_mi355x.h — C-ABI of libcorr_mi355x.so, the MI355X (gfx950) E-RAFT correlation hot path.
+ *
+ * Drop-in boundary for the reference CorrBlock (AhmedHumais/E-RAFT, model/corr.py:12-60).
+ * Plain pointers and sizes only; no torch types.  Every pointer argument except the host
+ * arrays of level pointers is DEVICE memory on the current HIP device; the caller allocates
+ * everything (pyramid, outputs, gradients, workspace) and the library never allocates,
+ * frees or synchronises.  All work is enqueued asynchronously on `stream` (a hipStream_t;
+ * NULL = the default stream) and calls are graph-capturable.
+ *
+ * Layouts (fp32, C-contiguous), N = H*W, K = (2*radius+1)^2:
+ *   fmap1, fmap2          [B][D][H][W]                       (corr.py:53-56)
+ *   pyramid level l       [B*N][H>>l][W>>l]                  (corr.py:21-27, floor halving)
+ *   coords                [B][2][H][W], ch0 = x, ch1 = y     (utils.py:24-27, corr.py:31)
+ *   lookup output         [B][levels*K][H][W]                (corr.py:46-50)
+ *
+ * Return value: CORR_OK (0) or a negative CORR_E* code; corr_last_error() then returns a
+ * thread-local message.  The reference performs no validation (torch raises inside
+ * avg_pool2d / grid_sample); here bad arguments are rejected up front with CORR_EINVAL.
+ * A level of height or width 1 is accepted and, like the reference (utils.py:11-12 divides
+ * by W_l - 1 = 0), produces NaN for all of that level's channels and no gradient.
+ */
+#ifndef CORR_MI355X_H
+#define CORR_MI355X_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CORR_OK 0
+#define CORR_EINVAL -1       /* bad sizes / null or misaligned pointers            */
+#define CORR_EUNSUPPORTED -2 /* valid for the reference, not supported here (none yet) */
+#define CORR_EHIP -3         /* HIP launch / runtime error                          */
+
+#define CORR_MAX_LEVELS 8
+#define CORR_MAX_RADIUS 7
+
+/* ABI version (major * 100 + minor). */
+int corr_version(void);
+
+/* Thread-local description of the last error on this thread ("" if none). */
+const char *corr_last_error(void);
+
+/*
+ * All-pairs correlation + average-pool pyramid.  Replaces CorrBlock.__init__
+ * (model/corr.py:13-27) together with CorrBlock.corr (model/corr.py:52-60):
+ *   pyr[0][b*N + n][y][x] = sum_d fmap1[b][d][n] * fmap2[b][d][y*W + x] / sqrt(float(D))
+ *   pyr[l][q][y][x]       = avg_pool2d(pyr[l-1], 2, stride 2)[q][y][x]   (floor)
+ * `pyr` is a HOST array of `levels` device pointers.  levels == 1 gives CorrBlock.corr's
+ * [B,H,W,1,H,W] volume.  fp32 in / fp32 MFMA accumulate / fp32 out.
+ */
+int corr_build(const float *fmap1, const float *fmap2, int B, int D, int H, int W, int levels,
+               float *const *pyr, void *stream);
+
+/*
+ * Window lookup.  Replaces CorrBlock.__call__ (model/corr.py:29-50) and bilinear_sampler
+ * (model/utils.py:7-21):
+ *   out[b][l*K + i*(2r+1) + j][h][w] = grid_sample(pyr[l][b*N + h*W + w],
+ *        (x/2^l + i - r, y/2^l + j - r), bilinear, zeros, align_corners=True)
+ * with (x, y) = coords[b][:][h][w].  The slow window index i moves x (corr.py:37-43).
+ * Bit-identical to the reference on identical pyramids.  `pyr` is a host array.
+ */
+int corr_lookup(const float *const *pyr, const float *coords, int B, int H, int W, int levels,
+                int radius, float *out, void *stream);
+
+/*
+ * Input-gradient of corr_lookup (autograd of model/utils.py:15; coords carry no gradient,
+ * model/eraft.py:128).  ACCUMULATES into grad_pyr (host array of device pointers, same
+ * shapes as the pyramid; zero it once before the first lookup of a build).  Deterministic:
+ * a query's contributions stay inside its own map, summed in a fixed order, no atomics.
+ */
+int corr_lookup_bwd(const float *coords, const float *grad_out, int B, int H, int W, int levels,
+                    int radius, float *const *grad_pyr, void *stream);
+
+/*
+ * avg_pool2d backward chain (autograd of model/corr.py:25-27), in place, coarse -> fine:
+ *   grad_pyr[l-1][q][2y+a][2x+c] += grad_pyr[l][q][y][x] * 0.25      (l = levels-1 .. 1)
+ * Afterwards grad_pyr[0] holds dLoss/dcorr.  BN = B*H*W query maps.
+ */
+int corr_pool_bwd(float *const *grad_pyr, int BN, int H, int W, int levels, void *stream);
+
+/* Bytes of device workspace corr_build_bwd needs for these sizes. */
+size_t corr_build_bwd_workspace(int B, int D, int H, int W);
+
+/*
+ * Backward of the all-pairs product and its 1/sqrt(D) scale (autograd of
+ * model/corr.py:58-60).  grad_c: [B*N][N] (= grad_pyr[0] after corr_pool_bwd);
+ *   dfmap1[b][d][n] = sum_m grad_c[b*N+n][m] * fmap2[b][d][m] / sqrt(D)
+ *   dfmap2[b][d][m] = sum_n fmap1[b][d][n] * grad_c[b*N+n][m] / sqrt(D)
+ * Both outputs are OVERWRITTEN.  Deterministic (split-K partial slabs summed in order).
+ */
+int corr_build_bwd(const float *grad_c, const float *fmap1, const float *fmap2, int B, int D,
+                   int H, int W, float *dfmap1, float *dfmap2, void *workspace,
+                   size_t workspace_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CORR_MI355X_H */

@@ -1,0 +1,76 @@
+"""C-ABI checks that need no GPU: the library builds, loads, exports every symbol declared in
+include/corr_mi355x.h, and rejects bad arguments before any HIP call."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "corr_mi355x.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(corr_[a-z_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from eraft_amd.build import build_library
+    from eraft_amd import _lib
+    build_library()
+    return _lib.load()
+
+
+def test_header_declares_the_python_exports():
+    from eraft_amd import _lib
+    assert sorted(_lib.EXPORTS) == _declared()
+
+
+def test_every_declared_symbol_is_exported(lib):
+    for name in _declared():
+        assert hasattr(lib, name), name
+
+
+def test_version_and_workspace(lib):
+    assert lib.corr_version() == 100
+    # DSEC: 256 x 4800 slabs; at least one slab, deterministic plan
+    ws = lib.corr_build_bwd_workspace(1, 256, 60, 80)
+    assert ws >= 256 * 4800 * 4 and ws % (256 * 4800 * 4) == 0
+    assert lib.corr_build_bwd_workspace(0, 256, 60, 80) == 0
+
+
+@pytest.mark.parametrize("args,msg", [
+    ((8, 8, 1, 256, 60, 80, 4, None, None), "pyr is NULL"),
+    ((None, 8, 1, 256, 60, 80, 4, None, None), "fmap1 is NULL"),
+    ((8, 8, 0, 256, 60, 80, 4, None, None), "B, H, W"),
+    ((8, 8, 1, 0, 60, 80, 4, None, None), "D must be"),
+    ((8, 8, 1, 256, 60, 80, 9, None, None), "levels must be"),
+    ((8, 8, 1, 256, 4, 80, 4, None, None), "too small"),
+    ((6, 8, 1, 256, 60, 80, 4, None, None), "aligned"),
+])
+def test_build_rejects_bad_arguments(lib, args, msg):
+    rc = lib.corr_build(*args)
+    assert rc == -1
+    assert msg in lib.corr_last_error().decode()
+
+
+def test_lookup_rejects_bad_radius(lib):
+    pyr = (ctypes.c_void_p * 4)(16, 16, 16, 16)
+    rc = lib.corr_lookup(pyr, 16, 1, 60, 80, 4, 8, 16, None)
+    assert rc == -1 and "radius" in lib.corr_last_error().decode()
+
+
+def test_build_bwd_rejects_small_workspace(lib):
+    rc = lib.corr_build_bwd(16, 16, 16, 1, 256, 60, 80, 16, 16, 16, 4, None)
+    assert rc == -1 and "workspace" in lib.corr_last_error().decode()
+
+
+def test_python_front_end_refuses_cpu_tensors():
+    import torch
+    from eraft_amd import CorrBlock
+    f = torch.zeros(1, 8, 16, 16)
+    with pytest.raises(RuntimeError, match="MI355X"):
+        CorrBlock(f, f)

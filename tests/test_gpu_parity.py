@@ -1,0 +1,240 @@
+"""Parity of the HIP path (eraft_amd -> libcorr_mi355x.so) against the reference's golden
+vectors and the oracle, on an MI355X.  Run on the GPU box: pytest -m gpu.
+
+Bars (north_star): correlation within 1e-4 norm-relative; pooling and lookup BIT-EXACT on
+identical inputs; backward within 1e-4 norm-relative.
+"""
+import numpy as np
+import pytest
+import torch
+
+import prng
+from _util import REL_TOL, bit_equal, golden_names, load, norm_rel
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+BUILD_CASES = [n for n in golden_names() if not n.startswith(("g_bwd", "g_dsec"))]
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    assert torch.cuda.is_available(), "gpu tests need an MI355X"
+    from eraft_amd import _lib
+    _lib.load()  # the HIP library must be the thing under test (no fallback exists)
+
+
+def _cb():
+    from eraft_amd import CorrBlock
+    return CorrBlock
+
+
+def _fmaps(meta, dev=DEV):
+    seed, B, D, H, W = (int(v) for v in meta[:5])
+    f1 = prng.gauss(seed, (B, D, H, W))
+    f2 = prng.gauss(seed + 1, (B, D, H, W))
+    return f1, f2, torch.from_numpy(f1).to(dev), torch.from_numpy(f2).to(dev)
+
+
+@pytest.mark.parametrize("name", BUILD_CASES)
+def test_build_matches_reference(name):
+    g = load(name)
+    L, r = int(g["meta"][5]), int(g["meta"][6])
+    _, _, t1, t2 = _fmaps(g["meta"])
+    cb = _cb()(t1, t2, num_levels=L, radius=r)
+    torch.cuda.synchronize()
+    assert len(cb.corr_pyramid) == L
+    gpu = [p.cpu().numpy() for p in cb.corr_pyramid]
+    for l in range(L):
+        assert gpu[l].shape == g[f"pyr{l}"].shape
+        assert norm_rel(gpu[l], g[f"pyr{l}"]) < REL_TOL, l
+    # fused in-register pyramid is bit-identical to avg_pool2d of the kernel's own level 0
+    for l in range(1, L):
+        assert bit_equal(oracle.avg_pool2x2(gpu[l - 1]), gpu[l]), l
+
+
+@pytest.mark.parametrize("name", BUILD_CASES)
+def test_lookup_bitexact_on_reference_pyramid(name):
+    g = load(name)
+    L, r = int(g["meta"][5]), int(g["meta"][6])
+    _, _, t1, t2 = _fmaps(g["meta"])
+    cb = _cb()(t1, t2, num_levels=L, radius=r)
+    # feed the kernel the reference's own pyramid: output must match bit for bit
+    for l in range(L):
+        cb.corr_pyramid[l].copy_(torch.from_numpy(g[f"pyr{l}"]))
+    keys = [k[len("coords"):] for k in g if k.startswith("coords")]
+    for k in keys:
+        out = cb(torch.from_numpy(g["coords" + k]).to(DEV)).cpu().numpy()
+        assert out.shape == g["look" + k].shape
+        assert bit_equal(out, g["look" + k]), k
+
+
+def test_corr_staticmethod_shape_and_values():
+    g = load("g_b2_d64_16x20_L2r3")
+    _, _, t1, t2 = _fmaps(g["meta"])
+    vol = _cb().corr(t1, t2)
+    assert tuple(vol.shape) == tuple(g["corr_shape"])
+    B, H, W = vol.shape[0], vol.shape[1], vol.shape[2]
+    assert norm_rel(vol.reshape(B * H * W, 1, H, W).cpu().numpy(), g["pyr0"]) < REL_TOL
+
+
+@pytest.mark.parametrize("name", golden_names("g_bwd"))
+def test_backward_matches_reference(name):
+    g = load(name)
+    seed, B, D, H, W, L, r, iters = (int(v) for v in g["meta"])
+    t1 = torch.from_numpy(prng.gauss(seed, (B, D, H, W))).to(DEV).requires_grad_(True)
+    t2 = torch.from_numpy(prng.gauss(seed + 1, (B, D, H, W))).to(DEV).requires_grad_(True)
+    cb = _cb()(t1, t2, num_levels=L, radius=r)
+    K = (2 * r + 1) ** 2
+    loss = 0.0
+    for t in range(iters):
+        c = torch.from_numpy(prng.lookup_coords(seed + 200 + t, B, H, W, 2.0 + t)).to(DEV)
+        gr = torch.from_numpy(prng.gauss(seed + 300 + t, (B, L * K, H, W))).to(DEV)
+        loss = loss + (cb(c) * gr).sum()
+    loss.backward()
+    assert norm_rel(t1.grad.cpu().numpy(), g["df1"]) < REL_TOL
+    assert norm_rel(t2.grad.cpu().numpy(), g["df2"]) < REL_TOL
+
+
+def test_dsec_shape_against_reference_slices():
+    g = load("g_dsec_spot")
+    seed, B, D, H, W, L, r = (int(v) for v in g["meta"])
+    _, _, t1, t2 = _fmaps(g["meta"])
+    cb = _cb()(t1, t2, num_levels=L, radius=r)
+    q = torch.from_numpy(g["q"]).to(DEV)
+    for l in range(L):
+        rows = cb.corr_pyramid[l][q].cpu().numpy()
+        assert norm_rel(rows, g[f"pyr{l}_rows"]) < REL_TOL
+        full = cb.corr_pyramid[l].double()
+        s, a = float(full.sum()), float(full.abs().sum())
+        assert abs(s - g[f"pyr{l}_sum"][0]) <= 1e-4 * g[f"pyr{l}_sum"][1]
+        assert abs(a - g[f"pyr{l}_sum"][1]) <= 1e-4 * g[f"pyr{l}_sum"][1]
+    c = torch.from_numpy(prng.lookup_coords(seed + 100, B, H, W, 8.0)).to(DEV)
+    o = cb(c)
+    oq = o.reshape(B, -1, H * W)[:, :, q].cpu().numpy()
+    assert norm_rel(oq, g["look_q"]) < REL_TOL
+    assert abs(float(o.double().abs().sum()) - g["look_sum"][1]) <= 1e-4 * g["look_sum"][1]
+
+
+@pytest.mark.parametrize("B,D,H,W,L,r", [
+    (1, 256, 60, 80, 4, 4),     # DSEC 480x640
+    (2, 256, 36, 44, 4, 4),     # MVSEC padded (B reduced for oracle time)
+    (1, 20, 17, 23, 3, 2),      # odd sizes, D not a multiple of the k-chunk, scalar paths
+    (3, 7, 9, 13, 2, 1),
+    (1, 33, 8, 8, 4, 4),        # smallest legal 4-level map (level 3 is 1x1 -> NaN lookups)
+])
+def test_gpu_pyramid_and_lookup_vs_oracle(B, D, H, W, L, r):
+    f1 = prng.gauss(B * 1000 + D, (B, D, H, W))
+    f2 = prng.gauss(B * 1000 + D + 1, (B, D, H, W))
+    cb = _cb()(torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV), num_levels=L, radius=r)
+    gpu = [p.cpu().numpy() for p in cb.corr_pyramid]
+    N = H * W
+    sel = np.unique(np.linspace(0, B * N - 1, 24).astype(int))
+    for qi in sel:
+        b, n = divmod(int(qi), N)
+        row = oracle.corr_rows(f1[b:b + 1], f2[b:b + 1], n, n + 1)[0, 0]
+        assert norm_rel(gpu[0][qi, 0].ravel(), row) < REL_TOL
+    for l in range(1, L):
+        assert bit_equal(oracle.avg_pool2x2(gpu[l - 1]), gpu[l])
+    for k, sig in enumerate([0.0, 4.0, 25.0]):
+        c = prng.lookup_coords(7 + k, B, H, W, sig)
+        out = cb(torch.from_numpy(c).to(DEV)).cpu().numpy()
+        assert bit_equal(out, oracle.lookup(gpu, c, r))
+    c = prng.special_coords(B, H, W)
+    assert bit_equal(cb(torch.from_numpy(c).to(DEV)).cpu().numpy(), oracle.lookup(gpu, c, r))
+
+
+def test_lookup_nan_and_inf_coords():
+    B, D, H, W, L, r = 1, 16, 16, 16, 3, 4
+    f1, f2 = prng.gauss(1, (B, D, H, W)), prng.gauss(2, (B, D, H, W))
+    cb = _cb()(torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV), num_levels=L, radius=r)
+    c = prng.lookup_coords(3, B, H, W, 2.0)
+    c[0, 0, 0, :4] = [np.nan, np.inf, -np.inf, 3.0e38]
+    c[0, 1, 1, :3] = [np.nan, -np.inf, 1e30]
+    gpu = [p.cpu().numpy() for p in cb.corr_pyramid]
+    assert bit_equal(cb(torch.from_numpy(c).to(DEV)).cpu().numpy(), oracle.lookup(gpu, c, r))
+
+
+@pytest.mark.parametrize("B,D,H,W,L,r", [(2, 16, 18, 24, 4, 4), (1, 8, 17, 23, 3, 3), (1, 256, 60, 80, 4, 4)])
+def test_lookup_bwd_bitexact_vs_oracle(B, D, H, W, L, r):
+    """One lookup's input-gradient from a zeroed pyramid: same tap / corner order as the
+    oracle -> bit-identical; then the avg-pool backward fold, also bit-identical."""
+    from eraft_amd import _lib
+    from eraft_amd.corr import _alloc_pyramid
+    K = (2 * r + 1) ** 2
+    c = prng.lookup_coords(5, B, H, W, 3.0)
+    c[0, :, 0, :3] = np.float32(np.nan)  # NaN coords contribute nothing
+    go = prng.gauss(6, (B, L * K, H, W))
+    ref = oracle.lookup_bwd(c, go, [np.zeros((B * H * W, 1, h, w), np.float32)
+                                    for h, w in oracle.level_shapes(H, W, L)], r)
+    like = torch.empty(1, device=DEV)
+    gl = _alloc_pyramid(B, H, W, L, like, zero=True)
+    _lib.lookup_bwd(torch.from_numpy(c).to(DEV), torch.from_numpy(go).to(DEV), r, gl)
+    for l in range(L):
+        assert bit_equal(gl[l].cpu().numpy(), ref[l]), l
+    oracle.pool_bwd(ref, H, W)
+    _lib.pool_bwd(gl, H, W)
+    for l in range(L):
+        assert bit_equal(gl[l].cpu().numpy(), ref[l]), l
+
+
+@pytest.mark.parametrize("B,D,H,W", [(1, 256, 60, 80), (2, 32, 18, 24), (1, 20, 17, 23), (8, 16, 12, 16)])
+def test_build_bwd_vs_oracle(B, D, H, W):
+    from eraft_amd import _lib
+    N = H * W
+    f1, f2 = prng.gauss(11, (B, D, H, W)), prng.gauss(12, (B, D, H, W))
+    gc = prng.gauss(13, (B * N, N))
+    if B * N * N * D > 3e9:
+        pytest.skip("oracle too slow")
+    d1, d2 = oracle.corr_bwd(gc.reshape(B * N, 1, H, W), f1, f2)
+    g1, g2 = _lib.build_bwd(torch.from_numpy(gc).to(DEV), torch.from_numpy(f1).to(DEV),
+                            torch.from_numpy(f2).to(DEV))
+    assert norm_rel(g1.cpu().numpy(), d1) < REL_TOL
+    assert norm_rel(g2.cpu().numpy(), d2) < REL_TOL
+
+
+def test_training_shape_backward_vs_oracle():
+    """BASELINE config 4 shape (36x48 fmaps), B and D reduced so the C oracle stays fast."""
+    B, D, H, W, L, r = 2, 32, 36, 48, 4, 4
+    f1, f2 = prng.gauss(21, (B, D, H, W)), prng.gauss(22, (B, D, H, W))
+    K = (2 * r + 1) ** 2
+    cs = [prng.lookup_coords(30 + t, B, H, W, 1.0 + t) for t in range(4)]
+    gs = [prng.gauss(40 + t, (B, L * K, H, W)) for t in range(4)]
+    d1, d2 = oracle.fmap_grads(f1, f2, cs, gs, L, r)
+    t1 = torch.from_numpy(f1).to(DEV).requires_grad_(True)
+    t2 = torch.from_numpy(f2).to(DEV).requires_grad_(True)
+    cb = _cb()(t1, t2, L, r)
+    loss = sum((cb(torch.from_numpy(c).to(DEV)) * torch.from_numpy(g).to(DEV)).sum() for c, g in zip(cs, gs))
+    loss.backward()
+    assert norm_rel(t1.grad.cpu().numpy(), d1) < REL_TOL
+    assert norm_rel(t2.grad.cpu().numpy(), d2) < REL_TOL
+
+
+def test_determinism():
+    B, D, H, W = 1, 64, 24, 32
+    f1 = torch.from_numpy(prng.gauss(1, (B, D, H, W))).to(DEV).requires_grad_(True)
+    f2 = torch.from_numpy(prng.gauss(2, (B, D, H, W))).to(DEV).requires_grad_(True)
+    c = torch.from_numpy(prng.lookup_coords(3, B, H, W, 5.0)).to(DEV)
+    res = []
+    for _ in range(2):
+        f1.grad = f2.grad = None
+        cb = _cb()(f1, f2)
+        o = cb(c)
+        (o * o).sum().backward()
+        res.append((o.detach().cpu().numpy(), f1.grad.cpu().numpy(), f2.grad.cpu().numpy()))
+    for a, b in zip(res[0], res[1]):
+        assert bit_equal(a, b)
+
+
+def test_errors_fail_loudly():
+    CB = _cb()
+    f = torch.zeros(1, 8, 16, 16)
+    with pytest.raises(RuntimeError):
+        CB(f, f)  # CPU tensors: no fallback
+    g = torch.zeros(1, 8, 8, 8, device=DEV)
+    with pytest.raises(RuntimeError):
+        CB(g[:, :, :1, :], g[:, :, :1, :], num_levels=4)  # too small for 4 levels
+    cb = CB(g, g, num_levels=2)
+    with pytest.raises(ValueError):
+        cb(torch.zeros(1, 2, 4, 4, device=DEV))
