@@ -32,6 +32,9 @@ static int check_dims(const char *fn, int B, int H, int W, int levels) {
     // avg_pool2d(2, 2) on a 1-pixel dimension raises in the reference (corr.py:26)
     if ((H >> (levels - 1)) < 1 || (W >> (levels - 1)) < 1)
         return fail(CORR_EINVAL, "%s: %dx%d is too small for %d pyramid levels", fn, H, W, levels);
+    // the lookup's neighbourhood anchors assume |coordinate floors| of in-map taps < 2^20
+    if (H > (1 << 20) || W > (1 << 20))
+        return fail(CORR_EINVAL, "%s: H and W must be <= 2^20", fn);
     const long long N = (long long)H * W;
     if (N > (1LL << 30) || (long long)B * N > (1LL << 31) - 1)
         return fail(CORR_EINVAL, "%s: B*H*W too large", fn);

@@ -6,32 +6,41 @@
 // permute().contiguous() (corr.py:49-50) become ONE launch that writes the NCHW output
 // directly.
 //
-// Layout of the work: a workgroup owns 64 consecutive query pixels of one batch item at one
-// pyramid level.
-//   1. per query and axis: the 2r+1 tap coordinates, exactly as the reference rounds them
-//      (x/2^l + (t - r) -> 2X/(W_l-1) - 1 -> ((x'+1)/2)(W_l-1); fp32, one rounding per op),
-//      their floor and the two 1-D weights -> LDS;
-//   2. the (2r+3)^2 neighbourhood of every query (anchored at its first tap's floor, zero
-//      outside the map) is gathered from HBM with lanes running along the rows -> LDS;
-//   3. lane = query, 4 waves split the taps: 4 corner reads from LDS, fmaf in the order
-//      nw, ne, sw, se (bit-identical to ATen's CPU grid_sampler_2d) and a coalesced store of
-//      out[b][l*K + tap][n] for 64 consecutive n.
-// A corner that lands outside the LDS neighbourhood (only possible under large-magnitude
-// rounding) is read from global memory instead, so semantics never depend on the window.
+// Work layout: a workgroup owns 64 consecutive query pixels of one batch item at one pyramid
+// level, with S = 2r+1 waves — wave i owns window column i (the x-tap; corr.py:37-43: the
+// slow window index moves x).
+//   1. thread (q, i): tap i of query q on both axes, rounded exactly as the reference does
+//      (x/2^l + (i - r) -> 2X/(W_l-1) - 1 -> ((x'+1)/2)(W_l-1); one fp32 rounding per op),
+//      its floor and the two 1-D weights; y-taps -> LDS, the thread keeps its x-tap;
+//   2. every query's (S+2)^2 neighbourhood (anchored at the floor of its tap 0, zero outside
+//      the map) is gathered from HBM into LDS — all of a thread's loads issued before any
+//      LDS store, so the gather costs one memory round trip;
+//   3. thread (q, i) produces the S outputs (i, j = 0..S-1): 4 corner reads from LDS, fmaf in
+//      the order nw, ne, sw, se (bit-identical to ATen's CPU grid_sampler_2d), stores to
+//      out[b][l*K + i*S + j][n] — 64 consecutive n per wave, fully coalesced.
+// Tap floors are monotone in the tap index, so one check of the first and last tap proves
+// that every corner lies inside the neighbourhood.  A workgroup where that fails for some
+// query (only possible for |coordinates| near 2^20) takes a uniform slow path that reads such
+// corners from global memory — keeping global loads out of the common loop (a load there
+// makes every iteration wait on vmcnt, i.e. on the previous iteration's stores).
 //
 // Backward (autograd of utils.py:15 w.r.t. the pyramid; coords are detached at
-// eraft.py:128): one wave per 64 queries x level; each lane scatters its query's taps into a
-// zeroed LDS neighbourhood in a fixed order (taps row-major, corners nw, ne, sw, se), then
-// the neighbourhood is added to the gradient pyramid.  A query's contributions never leave
-// its own map, so no atomics are needed and results are deterministic.
+// eraft.py:128): with regular taps (floor of tap t = anchor + t on both axes — the common
+// case) each neighbourhood cell receives exactly the <= 4 (tap, corner) contributions
+//   se(cx-1, cy-1), ne(cx-1, cy), sw(cx, cy-1), nw(cx, cy)
+// and is computed as a GATHER, summed in the reference's scatter order (taps row-major,
+// corners nw, ne, sw, se), then added once to the gradient pyramid.  A query's cells belong
+// to its own map only, so there are no atomics and results are deterministic.  Irregular
+// workgroups fall back to a sequential per-query scatter in the same order.
 #include <cmath>
+#include <type_traits>
 
 #include "corr_common.h"
 
 namespace corr {
 namespace {
 
-constexpr int kQB = 64;  // queries per workgroup
+constexpr int kQB = 64;  // queries per workgroup (one per lane)
 
 // Sentinel anchor for NaN / huge coordinates: every window cell is outside the map.
 constexpr int kFarAnchor = -(1 << 28);
@@ -66,24 +75,63 @@ __device__ __forceinline__ bool in_map(float xf, float yf, int Wl, int Hl) {
     return xf >= 0.0f && xf < (float)Wl && yf >= 0.0f && yf < (float)Hl;
 }
 
+// True when every in-map corner of the query's taps lies inside its (S+2)^2 neighbourhood.
+template <int S>
+__device__ __forceinline__ bool window_covers(float fx0, float fxl, float fy0, float fyl) {
+    if (anchor_of(fx0) == kFarAnchor || anchor_of(fy0) == kFarAnchor) return true;
+    return (fxl - fx0) <= (float)S && (fyl - fy0) <= (float)S;
+}
+
+// Gather each query's neighbourhood into LDS: cell (ry, rx) of query qq = map (ay+ry, ax+rx),
+// zero outside the map or for queries past N.
+template <int S, int NT>
+__device__ __forceinline__ void gather_window(float *win, const int *ax, const int *ay,
+                                              const float *P, size_t qbase, size_t mapsz, int n0,
+                                              int N, int Wl, int Hl, int tid) {
+    constexpr int WIN = S + 2, WS = WIN * WIN, WSTR = WS | 1;
+    constexpr int PER = (kQB * WS + NT - 1) / NT;
+    float vals[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int g = tid + NT * u;
+        const int qq = g / WS;
+        const int e = g - qq * WS;
+        const int ry = e / WIN, rx = e - ry * WIN;
+        float v = 0.0f;
+        if (g < kQB * WS && n0 + qq < N) {
+            const int Y = ay[qq] + ry, X = ax[qq] + rx;
+            if (X >= 0 && X < Wl && Y >= 0 && Y < Hl) v = P[(qbase + qq) * mapsz + (size_t)Y * Wl + X];
+        }
+        vals[u] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+        const int g = tid + NT * u;
+        if (g < kQB * WS) {
+            const int qq = g / WS;
+            win[qq * WSTR + (g - qq * WS)] = vals[u];
+        }
+    }
+}
+
 template <int S>
 struct LookupSmem {
     static constexpr int WIN = S + 2;
-    static constexpr int WS = WIN * WIN;
-    static constexpr int WSTR = WS | 1;  // odd stride: conflict-free lane = query reads
+    static constexpr int WSTR = (WIN * WIN) | 1;  // odd stride: conflict-free lane = query reads
     float win[kQB * WSTR];
-    float tx[3][S][kQB];
     float ty[3][S][kQB];
+    float fx[2][kQB];  // floor of x-tap 0 and S-1
     int ax[kQB], ay[kQB];
 };
 
 template <int S>
-__global__ __launch_bounds__(256) void lookup_kernel(ConstLevelPtrs pyr, const float *__restrict__ coords,
-                                                     int B, int H, int W, int L,
-                                                     float *__restrict__ out) {
-    constexpr int R = (S - 1) / 2, K = S * S;
+__global__ __launch_bounds__(64 * S) void lookup_kernel(ConstLevelPtrs pyr,
+                                                        const float *__restrict__ coords, int B,
+                                                        int H, int W, int L,
+                                                        float *__restrict__ out) {
+    constexpr int R = (S - 1) / 2, K = S * S, NT = 64 * S;
     using SM = LookupSmem<S>;
-    constexpr int WIN = SM::WIN, WS = SM::WS, WSTR = SM::WSTR;
+    constexpr int WIN = SM::WIN, WSTR = SM::WSTR;
     __shared__ SM sm;
 
     const int N = H * W;
@@ -95,97 +143,100 @@ __global__ __launch_bounds__(256) void lookup_kernel(ConstLevelPtrs pyr, const f
     const float inv_scale = 1.0f / (float)(1 << l);
     const float *P = pyr.p[l];
     const size_t mapsz = (size_t)Hl * Wl;
+    const size_t qbase = (size_t)b * N + n0;
 
     const int tid = threadIdx.x;
     const int q = tid & (kQB - 1);
-    const int role = tid >> 6;  // 0,1: x taps; 2,3: y taps
+    const int i = tid >> 6;  // this wave's x-tap (window column)
     const int n = n0 + q;
     const bool qok = n < N;
 
-    // ---- 1. tap coordinates ----
+    // ---- 1. taps ----
+    const float cxv = qok ? coords[((size_t)b * 2 + 0) * N + n] : 0.0f;
+    const float cyv = qok ? coords[((size_t)b * 2 + 1) * N + n] : 0.0f;
+    const Axis tx = tap_axis(cxv, inv_scale, i, R, Wl);
     {
-        const int axis = role >> 1;
-        const float c = qok ? coords[((size_t)b * 2 + axis) * N + n] : 0.0f;
-        const int size = axis ? Hl : Wl;
-        constexpr int half = (S + 1) / 2;
-        const int t0 = (role & 1) ? half : 0, t1 = (role & 1) ? S : half;
-        for (int t = t0; t < t1; ++t) {
-            const Axis a = tap_axis(c, inv_scale, t, R, size);
-            if (axis == 0) {
-                sm.tx[0][t][q] = a.f;
-                sm.tx[1][t][q] = a.lo;
-                sm.tx[2][t][q] = a.hi;
-                if (t == 0) sm.ax[q] = anchor_of(a.f);
-            } else {
-                sm.ty[0][t][q] = a.f;
-                sm.ty[1][t][q] = a.lo;
-                sm.ty[2][t][q] = a.hi;
-                if (t == 0) sm.ay[q] = anchor_of(a.f);
-            }
+        const Axis a = tap_axis(cyv, inv_scale, i, R, Hl);
+        sm.ty[0][i][q] = a.f;
+        sm.ty[1][i][q] = a.lo;
+        sm.ty[2][i][q] = a.hi;
+        if (i == 0) {
+            sm.ax[q] = anchor_of(tx.f);
+            sm.ay[q] = anchor_of(a.f);
+            sm.fx[0][q] = tx.f;
         }
+        if (i == S - 1) sm.fx[1][q] = tx.f;
     }
     __syncthreads();
 
-    // ---- 2. gather every query's neighbourhood (zero outside the map) ----
-    const size_t qbase = (size_t)b * N + n0;
-    for (int g = tid; g < kQB * WS; g += 256) {
-        const int qq = g / WS;
-        const int e = g - qq * WS;
-        const int ry = e / WIN, rx = e - ry * WIN;
-        float v = 0.0f;
-        if (n0 + qq < N) {
-            const int Y = sm.ay[qq] + ry, X = sm.ax[qq] + rx;
-            if (X >= 0 && X < Wl && Y >= 0 && Y < Hl) v = P[(qbase + qq) * mapsz + (size_t)Y * Wl + X];
-        }
-        sm.win[qq * WSTR + e] = v;
-    }
-    __syncthreads();
+    // ---- 2. neighbourhoods -> LDS ----
+    gather_window<S, NT>(sm.win, sm.ax, sm.ay, P, qbase, mapsz, n0, N, Wl, Hl, tid);
+    const int slow = __syncthreads_or(
+        !window_covers<S>(sm.fx[0][q], sm.fx[1][q], sm.ty[0][0][q], sm.ty[0][S - 1][q]));
 
-    // ---- 3. lane = query; the 4 waves split the K taps ----
+    // ---- 3. outputs (i, 0..S-1) of query q ----
     const int ax = sm.ax[q], ay = sm.ay[q];
     const float *wq = &sm.win[q * WSTR];
-    const float *Pq = P + (qbase + q) * mapsz;
-    auto fetch = [&](float xf, float yf) -> float {
-        if (!in_map(xf, yf, Wl, Hl)) return 0.0f;
-        const int xi = (int)xf, yi = (int)yf;
-        const unsigned cx = (unsigned)(xi - ax), cy = (unsigned)(yi - ay);
-        if (cx < (unsigned)WIN && cy < (unsigned)WIN) return wq[cy * WIN + cx];
-        return Pq[(size_t)yi * Wl + xi];
-    };
-    constexpr int KP = (K + 3) / 4;
-    const int k0 = role * KP, k1 = (k0 + KP < K) ? k0 + KP : K;
-    float *o = out + ((size_t)b * L + l) * K * N + n;
-    for (int k = k0; k < k1; ++k) {
-        const int i = k / S, j = k - (k / S) * S;
-        const float x0 = sm.tx[0][i][q], ex = sm.tx[1][i][q], wx = sm.tx[2][i][q];
-        const float y0 = sm.ty[0][j][q], ey = sm.ty[1][j][q], ny = sm.ty[2][j][q];
-        const float x1 = __fadd_rn(x0, 1.0f), y1 = __fadd_rn(y0, 1.0f);
-        const float vnw = fetch(x0, y0), vne = fetch(x1, y0);
-        const float vsw = fetch(x0, y1), vse = fetch(x1, y1);
-        float acc = __fmul_rn(vnw, __fmul_rn(ey, ex));
-        acc = __builtin_fmaf(vne, __fmul_rn(ey, wx), acc);
-        acc = __builtin_fmaf(vsw, __fmul_rn(ny, ex), acc);
-        acc = __builtin_fmaf(vse, __fmul_rn(ny, wx), acc);
-        if (qok) o[(size_t)k * N] = acc;
+    float *o = out + (((size_t)b * L + l) * K + (size_t)i * S) * N + n;
+    const float x0 = tx.f, ex = tx.lo, wx = tx.hi;
+    if (!slow) {
+        // every corner is inside the neighbourhood (cells outside the map hold 0)
+        const bool far = (ax == kFarAnchor) || (ay == kFarAnchor);
+        const int cx = far ? 0 : (int)x0 - ax;
+        const float *col = wq + cx;
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            const float y0 = sm.ty[0][j][q], ey = sm.ty[1][j][q], ny = sm.ty[2][j][q];
+            const int cy = far ? 0 : (int)y0 - ay;
+            const float *c = col + cy * WIN;
+            float acc = __fmul_rn(c[0], __fmul_rn(ey, ex));
+            acc = __builtin_fmaf(c[1], __fmul_rn(ey, wx), acc);
+            acc = __builtin_fmaf(c[WIN], __fmul_rn(ny, ex), acc);
+            acc = __builtin_fmaf(c[WIN + 1], __fmul_rn(ny, wx), acc);
+            if (qok) o[(size_t)j * N] = acc;
+        }
+    } else {
+        const float *Pq = P + (qbase + q) * mapsz;
+        auto fetch = [&](float xf, float yf) -> float {
+            if (!in_map(xf, yf, Wl, Hl)) return 0.0f;
+            const int xi = (int)xf, yi = (int)yf;
+            const unsigned ux = (unsigned)(xi - ax), uy = (unsigned)(yi - ay);
+            if (ux < (unsigned)WIN && uy < (unsigned)WIN) return wq[uy * WIN + ux];
+            return Pq[(size_t)yi * Wl + xi];
+        };
+        const float x1 = __fadd_rn(x0, 1.0f);
+        for (int j = 0; j < S; ++j) {
+            const float y0 = sm.ty[0][j][q], ey = sm.ty[1][j][q], ny = sm.ty[2][j][q];
+            const float y1 = __fadd_rn(y0, 1.0f);
+            float acc = __fmul_rn(fetch(x0, y0), __fmul_rn(ey, ex));
+            acc = __builtin_fmaf(fetch(x1, y0), __fmul_rn(ey, wx), acc);
+            acc = __builtin_fmaf(fetch(x0, y1), __fmul_rn(ny, ex), acc);
+            acc = __builtin_fmaf(fetch(x1, y1), __fmul_rn(ny, wx), acc);
+            if (qok) o[(size_t)j * N] = acc;
+        }
     }
 }
 
 template <int S>
 struct LookupBwdSmem {
     static constexpr int WIN = S + 2;
-    static constexpr int WS = WIN * WIN;
-    static constexpr int WSTR = WS | 1;
-    float win[kQB * WSTR];
+    static constexpr int WSTR = (WIN * WIN) | 1;
+    float g[S * S][kQB];   // upstream gradient tile
+    float tx[3][S][kQB];   // floor, lo, hi per x-tap
+    float ty[3][S][kQB];
     int ax[kQB], ay[kQB];
+    float win[kQB * WSTR];  // irregular path only
 };
 
 template <int S>
-__global__ __launch_bounds__(64) void lookup_bwd_kernel(const float *__restrict__ coords,
-                                                        const float *__restrict__ grad_out, int B,
-                                                        int H, int W, int L, LevelPtrs gpyr) {
-    constexpr int R = (S - 1) / 2, K = S * S;
+__global__ __launch_bounds__(64 * S) void lookup_bwd_kernel(const float *__restrict__ coords,
+                                                            const float *__restrict__ grad_out,
+                                                            int B, int H, int W, int L,
+                                                            LevelPtrs gpyr) {
+    constexpr int R = (S - 1) / 2, K = S * S, NT = 64 * S;
     using SM = LookupBwdSmem<S>;
-    constexpr int WIN = SM::WIN, WS = SM::WS, WSTR = SM::WSTR;
+    constexpr int WIN = SM::WIN, WS = WIN * WIN, WSTR = SM::WSTR;
+    constexpr int C = S + 1;  // cells per axis reached by regular taps
     __shared__ SM sm;
 
     const int N = H * W;
@@ -199,63 +250,122 @@ __global__ __launch_bounds__(64) void lookup_bwd_kernel(const float *__restrict_
     const size_t mapsz = (size_t)Hl * Wl;
     const size_t qbase = (size_t)b * N + n0;
 
-    const int q = threadIdx.x;
+    const int tid = threadIdx.x;
+    const int q = tid & (kQB - 1);
+    const int t = tid >> 6;
     const int n = n0 + q;
     const bool qok = n < N;
-    const float cx = qok ? coords[((size_t)b * 2 + 0) * N + n] : 0.0f;
-    const float cy = qok ? coords[((size_t)b * 2 + 1) * N + n] : 0.0f;
 
-    Axis tx[S], ty[S];
-#pragma unroll
-    for (int t = 0; t < S; ++t) {
-        tx[t] = tap_axis(cx, inv_scale, t, R, Wl);
-        ty[t] = tap_axis(cy, inv_scale, t, R, Hl);
+    // ---- 1. taps and the upstream gradient tile ----
+    const float cxv = qok ? coords[((size_t)b * 2 + 0) * N + n] : 0.0f;
+    const float cyv = qok ? coords[((size_t)b * 2 + 1) * N + n] : 0.0f;
+    const Axis a = tap_axis(cxv, inv_scale, t, R, Wl);
+    const Axis c = tap_axis(cyv, inv_scale, t, R, Hl);
+    sm.tx[0][t][q] = a.f;
+    sm.tx[1][t][q] = a.lo;
+    sm.tx[2][t][q] = a.hi;
+    sm.ty[0][t][q] = c.f;
+    sm.ty[1][t][q] = c.lo;
+    sm.ty[2][t][q] = c.hi;
+    if (t == 0) {
+        sm.ax[q] = anchor_of(a.f);
+        sm.ay[q] = anchor_of(c.f);
     }
-    const int ax = anchor_of(tx[0].f), ay = anchor_of(ty[0].f);
-    sm.ax[q] = ax;
-    sm.ay[q] = ay;
-    for (int g = q; g < kQB * WSTR; g += 64) sm.win[g] = 0.0f;
+    {
+        const float *g = grad_out + (((size_t)b * L + l) * K + (size_t)t * S) * N + n;
+        float v[S];
+#pragma unroll
+        for (int u = 0; u < S; ++u) v[u] = qok ? g[(size_t)u * N] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < S; ++u) sm.g[t * S + u][q] = v[u];
+    }
     __syncthreads();
+    // regular: floor(tap t) == floor(tap 0) + t on both axes (or the query has no in-map corner)
+    const float fx0 = sm.tx[0][0][q], fy0 = sm.ty[0][0][q];
+    const bool far = anchor_of(fx0) == kFarAnchor || anchor_of(fy0) == kFarAnchor;
+    const bool reg = far || (a.f - fx0 == (float)t && c.f - fy0 == (float)t);
+    const int irregular = __syncthreads_or(!reg);
 
-    float *wq = &sm.win[q * WSTR];
-    float *Gq = G + (qbase + q) * mapsz;
-    auto scatter = [&](float xf, float yf, float v) {
-        if (!in_map(xf, yf, Wl, Hl)) return;
-        const int xi = (int)xf, yi = (int)yf;
-        const unsigned ux = (unsigned)(xi - ax), uy = (unsigned)(yi - ay);
-        if (ux < (unsigned)WIN && uy < (unsigned)WIN)
-            wq[uy * WIN + ux] += v;
-        else
-            Gq[(size_t)yi * Wl + xi] += v;  // outside the neighbourhood: disjoint cells
-    };
-    if (qok) {
-        const float *g = grad_out + ((size_t)b * L + l) * K * N + n;
+    if (!irregular) {
+        // ---- 2a. gather: cell (cx, cy), cx, cy in [0, S] of each query ----
+        constexpr int CELLS = kQB * C * C;
+        constexpr int PER = (CELLS + NT - 1) / NT;
+        float sum[PER], old[PER];
+        size_t dst[PER];
+        bool live[PER];
 #pragma unroll
-        for (int i = 0; i < S; ++i) {
-            const float x0 = tx[i].f, x1 = __fadd_rn(tx[i].f, 1.0f);
+        for (int u = 0; u < PER; ++u) {
+            const int item = tid + NT * u;
+            const int qq = item / (C * C);
+            const int e = item - qq * (C * C);
+            const int cy = e / C, cx = e - cy * C;
+            const int X = sm.ax[qq] + cx, Y = sm.ay[qq] + cy;
+            live[u] = item < CELLS && n0 + qq < N && X >= 0 && X < Wl && Y >= 0 && Y < Hl;
+            float s = 0.0f;
+            if (live[u]) {
+                if (cx >= 1 && cy >= 1)  // se corner of tap (cx-1, cy-1)
+                    s = s + __fmul_rn(sm.g[(cx - 1) * S + cy - 1][qq],
+                                      __fmul_rn(sm.ty[2][cy - 1][qq], sm.tx[2][cx - 1][qq]));
+                if (cx >= 1 && cy < S)  // ne corner of tap (cx-1, cy)
+                    s = s + __fmul_rn(sm.g[(cx - 1) * S + cy][qq],
+                                      __fmul_rn(sm.ty[1][cy][qq], sm.tx[2][cx - 1][qq]));
+                if (cx < S && cy >= 1)  // sw corner of tap (cx, cy-1)
+                    s = s + __fmul_rn(sm.g[cx * S + cy - 1][qq],
+                                      __fmul_rn(sm.ty[2][cy - 1][qq], sm.tx[1][cx][qq]));
+                if (cx < S && cy < S)  // nw corner of tap (cx, cy)
+                    s = s + __fmul_rn(sm.g[cx * S + cy][qq],
+                                      __fmul_rn(sm.ty[1][cy][qq], sm.tx[1][cx][qq]));
+            }
+            sum[u] = s;
+            dst[u] = live[u] ? (qbase + qq) * mapsz + (size_t)Y * Wl + X : 0;
+            old[u] = live[u] ? G[dst[u]] : 0.0f;
+        }
 #pragma unroll
+        for (int u = 0; u < PER; ++u)
+            if (live[u]) G[dst[u]] = old[u] + sum[u];
+        return;
+    }
+
+    // ---- 2b. irregular workgroup: sequential per-query scatter (wave 0, lane = query) ----
+    for (int g = tid; g < kQB * WSTR; g += NT) sm.win[g] = 0.0f;
+    __syncthreads();
+    if (t == 0 && qok) {
+        const int ax = sm.ax[q], ay = sm.ay[q];
+        float *wq = &sm.win[q * WSTR];
+        float *Gq = G + (qbase + q) * mapsz;
+        auto scatter = [&](float xf, float yf, float v) {
+            if (!in_map(xf, yf, Wl, Hl)) return;
+            const int xi = (int)xf, yi = (int)yf;
+            const unsigned ux = (unsigned)(xi - ax), uy = (unsigned)(yi - ay);
+            if (ux < (unsigned)WIN && uy < (unsigned)WIN)
+                wq[uy * WIN + ux] += v;
+            else
+                Gq[(size_t)yi * Wl + xi] += v;  // outside the neighbourhood: disjoint cells
+        };
+        for (int ii = 0; ii < S; ++ii) {
+            const float x0 = sm.tx[0][ii][q], x1 = __fadd_rn(x0, 1.0f);
+            const float ex = sm.tx[1][ii][q], wx = sm.tx[2][ii][q];
             for (int j = 0; j < S; ++j) {
-                const float gv = g[(size_t)(i * S + j) * N];
-                const float y0 = ty[j].f, y1 = __fadd_rn(ty[j].f, 1.0f);
-                scatter(x0, y0, __fmul_rn(gv, __fmul_rn(ty[j].lo, tx[i].lo)));
-                scatter(x1, y0, __fmul_rn(gv, __fmul_rn(ty[j].lo, tx[i].hi)));
-                scatter(x0, y1, __fmul_rn(gv, __fmul_rn(ty[j].hi, tx[i].lo)));
-                scatter(x1, y1, __fmul_rn(gv, __fmul_rn(ty[j].hi, tx[i].hi)));
+                const float gv = sm.g[ii * S + j][q];
+                const float y0 = sm.ty[0][j][q], y1 = __fadd_rn(y0, 1.0f);
+                const float ey = sm.ty[1][j][q], ny = sm.ty[2][j][q];
+                scatter(x0, y0, __fmul_rn(gv, __fmul_rn(ey, ex)));
+                scatter(x1, y0, __fmul_rn(gv, __fmul_rn(ey, wx)));
+                scatter(x0, y1, __fmul_rn(gv, __fmul_rn(ny, ex)));
+                scatter(x1, y1, __fmul_rn(gv, __fmul_rn(ny, wx)));
             }
         }
     }
     __syncthreads();
-
-    // add the neighbourhoods to the gradient pyramid (lanes along window rows)
-    for (int g = q; g < kQB * WS; g += 64) {
+    for (int g = tid; g < kQB * WS; g += NT) {
         const int qq = g / WS;
         const int e = g - qq * WS;
         if (n0 + qq >= N) continue;
         const int ry = e / WIN, rx = e - ry * WIN;
         const int Y = sm.ay[qq] + ry, X = sm.ax[qq] + rx;
         if (X >= 0 && X < Wl && Y >= 0 && Y < Hl) {
-            float *dst = G + (qbase + qq) * mapsz + (size_t)Y * Wl + X;
-            *dst = *dst + sm.win[qq * WSTR + e];
+            float *d = G + (qbase + qq) * mapsz + (size_t)Y * Wl + X;
+            *d = *d + sm.win[qq * WSTR + e];
         }
     }
 }
@@ -283,7 +393,7 @@ template <int S>
 hipError_t launch_lookup_s(const ConstLevelPtrs &pyr, const float *coords, int B, int H, int W,
                            int L, float *out, hipStream_t s) {
     const int nqb = (H * W + kQB - 1) / kQB;
-    hipLaunchKernelGGL(lookup_kernel<S>, dim3(nqb * B, L), dim3(256), 0, s, pyr, coords, B, H, W,
+    hipLaunchKernelGGL(lookup_kernel<S>, dim3(nqb * B, L), dim3(64 * S), 0, s, pyr, coords, B, H, W,
                        L, out);
     return hipGetLastError();
 }
@@ -292,7 +402,7 @@ template <int S>
 hipError_t launch_lookup_bwd_s(const float *coords, const float *grad_out, int B, int H, int W,
                                int L, const LevelPtrs &gpyr, hipStream_t s) {
     const int nqb = (H * W + kQB - 1) / kQB;
-    hipLaunchKernelGGL(lookup_bwd_kernel<S>, dim3(nqb * B, L), dim3(64), 0, s, coords, grad_out,
+    hipLaunchKernelGGL(lookup_bwd_kernel<S>, dim3(nqb * B, L), dim3(64 * S), 0, s, coords, grad_out,
                        B, H, W, L, gpyr);
     return hipGetLastError();
 }
