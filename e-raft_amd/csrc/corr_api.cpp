@@ -1,6 +1,9 @@
 // corr_api.cpp — the extern "C" boundary of libcorr_mi355x.so (declared in
 // include/corr_mi355x.h).  Validates arguments, records thread-local errors and forwards to
 // the gfx950 launchers.  No allocation, no synchronisation, no global mutable state.
+//
+// The reference-shaped entry points (corr_build, corr_lookup, ...) are the row-slab
+// variants (corr_*_rows) with the slab = every query pixel (NQ = H*W).
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -24,9 +27,11 @@ int hip_status(hipError_t e, const char *what) {
     return fail(CORR_EHIP, "%s: %s", what, hipGetErrorString(e));
 }
 
-static int check_dims(const char *fn, int B, int H, int W, int levels) {
+static int check_dims(const char *fn, int B, int NQ, int H, int W, int levels) {
     if (B < 1 || H < 1 || W < 1)
         return fail(CORR_EINVAL, "%s: B, H, W must be >= 1 (got %d, %d, %d)", fn, B, H, W);
+    if (NQ < 1 || NQ > H * (long long)W)
+        return fail(CORR_EINVAL, "%s: NQ must be in [1, H*W] (got %d)", fn, NQ);
     if (levels < 1 || levels > CORR_MAX_LEVELS)
         return fail(CORR_EINVAL, "%s: levels must be in [1, %d] (got %d)", fn, CORR_MAX_LEVELS, levels);
     // avg_pool2d(2, 2) on a 1-pixel dimension raises in the reference (corr.py:26)
@@ -36,7 +41,7 @@ static int check_dims(const char *fn, int B, int H, int W, int levels) {
     if (H > (1 << 20) || W > (1 << 20))
         return fail(CORR_EINVAL, "%s: H and W must be <= 2^20", fn);
     const long long N = (long long)H * W;
-    if (N > (1LL << 30) || (long long)B * N > (1LL << 31) - 1)
+    if (N > (1LL << 30) || (long long)B * NQ > (1LL << 31) - 1)
         return fail(CORR_EINVAL, "%s: B*H*W too large", fn);
     return CORR_OK;
 }
@@ -44,6 +49,23 @@ static int check_dims(const char *fn, int B, int H, int W, int levels) {
 static int check_ptr(const char *fn, const void *p, const char *name) {
     if (!p) return fail(CORR_EINVAL, "%s: %s is NULL", fn, name);
     if ((uintptr_t)p % 4) return fail(CORR_EINVAL, "%s: %s is not 4-byte aligned", fn, name);
+    return CORR_OK;
+}
+
+template <class P>
+static int check_levels(const char *fn, P *const *src, int levels, const char *name, P **dst) {
+    if (!src) return fail(CORR_EINVAL, "%s: %s is NULL", fn, name);
+    for (int l = 0; l < levels; ++l) {
+        int rc = check_ptr(fn, src[l], name);
+        if (rc) return rc;
+        dst[l] = src[l];
+    }
+    return CORR_OK;
+}
+
+static int check_radius(const char *fn, int radius) {
+    if (radius < 0 || radius > CORR_MAX_RADIUS)
+        return fail(CORR_EINVAL, "%s: radius must be in [0, %d] (got %d)", fn, CORR_MAX_RADIUS, radius);
     return CORR_OK;
 }
 
@@ -57,102 +79,107 @@ int corr_version(void) { return 100; }
 
 const char *corr_last_error(void) { return g_err; }
 
+int corr_build_rows(const float *fmap1_rows, int NQ, const float *fmap2, int B, int D, int H,
+                    int W, int levels, float *const *pyr, void *stream) {
+    static const char *fn = "corr_build";
+    g_err[0] = 0;
+    int rc = check_dims(fn, B, NQ, H, W, levels);
+    if (rc) return rc;
+    if (D < 1) return fail(CORR_EINVAL, "%s: D must be >= 1 (got %d)", fn, D);
+    if ((rc = check_ptr(fn, fmap1_rows, "fmap1")) || (rc = check_ptr(fn, fmap2, "fmap2"))) return rc;
+    LevelPtrs lp{};
+    if ((rc = check_levels(fn, pyr, levels, "pyr", lp.p))) return rc;
+    return hip_status(launch_build(fmap1_rows, NQ, fmap2, B, D, H, W, levels, lp, (hipStream_t)stream), fn);
+}
+
 int corr_build(const float *fmap1, const float *fmap2, int B, int D, int H, int W, int levels,
                float *const *pyr, void *stream) {
+    return corr_build_rows(fmap1, H * W, fmap2, B, D, H, W, levels, pyr, stream);
+}
+
+int corr_lookup_rows(const float *const *pyr, const float *coords_rows, int B, int NQ, int H,
+                     int W, int levels, int radius, float *out_rows, void *stream) {
+    static const char *fn = "corr_lookup";
     g_err[0] = 0;
-    int rc = check_dims("corr_build", B, H, W, levels);
-    if (rc) return rc;
-    if (D < 1) return fail(CORR_EINVAL, "corr_build: D must be >= 1 (got %d)", D);
-    if ((rc = check_ptr("corr_build", fmap1, "fmap1")) || (rc = check_ptr("corr_build", fmap2, "fmap2")))
-        return rc;
-    if (!pyr) return fail(CORR_EINVAL, "corr_build: pyr is NULL");
-    LevelPtrs lp{};
-    for (int l = 0; l < levels; ++l) {
-        if ((rc = check_ptr("corr_build", pyr[l], "pyr[l]"))) return rc;
-        lp.p[l] = pyr[l];
-    }
-    return hip_status(launch_build(fmap1, fmap2, B, D, H, W, levels, lp, (hipStream_t)stream),
-                      "corr_build");
+    int rc = check_dims(fn, B, NQ, H, W, levels);
+    if (rc || (rc = check_radius(fn, radius))) return rc;
+    if ((rc = check_ptr(fn, coords_rows, "coords")) || (rc = check_ptr(fn, out_rows, "out"))) return rc;
+    ConstLevelPtrs lp{};
+    if ((rc = check_levels(fn, pyr, levels, "pyr", lp.p))) return rc;
+    return hip_status(launch_lookup(lp, coords_rows, B, NQ, H, W, levels, radius, out_rows, (hipStream_t)stream),
+                      fn);
 }
 
 int corr_lookup(const float *const *pyr, const float *coords, int B, int H, int W, int levels,
                 int radius, float *out, void *stream) {
+    return corr_lookup_rows(pyr, coords, B, H * W, H, W, levels, radius, out, stream);
+}
+
+int corr_lookup_bwd_rows(const float *coords_rows, const float *grad_out_rows, int B, int NQ,
+                         int H, int W, int levels, int radius, float *const *grad_pyr,
+                         void *stream) {
+    static const char *fn = "corr_lookup_bwd";
     g_err[0] = 0;
-    int rc = check_dims("corr_lookup", B, H, W, levels);
-    if (rc) return rc;
-    if (radius < 0 || radius > CORR_MAX_RADIUS)
-        return fail(CORR_EINVAL, "corr_lookup: radius must be in [0, %d] (got %d)", CORR_MAX_RADIUS, radius);
-    if ((rc = check_ptr("corr_lookup", coords, "coords")) || (rc = check_ptr("corr_lookup", out, "out")))
+    int rc = check_dims(fn, B, NQ, H, W, levels);
+    if (rc || (rc = check_radius(fn, radius))) return rc;
+    if ((rc = check_ptr(fn, coords_rows, "coords")) || (rc = check_ptr(fn, grad_out_rows, "grad_out")))
         return rc;
-    if (!pyr) return fail(CORR_EINVAL, "corr_lookup: pyr is NULL");
-    ConstLevelPtrs lp{};
-    for (int l = 0; l < levels; ++l) {
-        if ((rc = check_ptr("corr_lookup", pyr[l], "pyr[l]"))) return rc;
-        lp.p[l] = pyr[l];
-    }
-    return hip_status(launch_lookup(lp, coords, B, H, W, levels, radius, out, (hipStream_t)stream),
-                      "corr_lookup");
+    LevelPtrs lp{};
+    if ((rc = check_levels(fn, grad_pyr, levels, "grad_pyr", lp.p))) return rc;
+    return hip_status(
+        launch_lookup_bwd(coords_rows, grad_out_rows, B, NQ, H, W, levels, radius, lp, (hipStream_t)stream), fn);
 }
 
 int corr_lookup_bwd(const float *coords, const float *grad_out, int B, int H, int W, int levels,
                     int radius, float *const *grad_pyr, void *stream) {
-    g_err[0] = 0;
-    int rc = check_dims("corr_lookup_bwd", B, H, W, levels);
-    if (rc) return rc;
-    if (radius < 0 || radius > CORR_MAX_RADIUS)
-        return fail(CORR_EINVAL, "corr_lookup_bwd: radius must be in [0, %d] (got %d)", CORR_MAX_RADIUS, radius);
-    if ((rc = check_ptr("corr_lookup_bwd", coords, "coords")) ||
-        (rc = check_ptr("corr_lookup_bwd", grad_out, "grad_out")))
-        return rc;
-    if (!grad_pyr) return fail(CORR_EINVAL, "corr_lookup_bwd: grad_pyr is NULL");
-    LevelPtrs lp{};
-    for (int l = 0; l < levels; ++l) {
-        if ((rc = check_ptr("corr_lookup_bwd", grad_pyr[l], "grad_pyr[l]"))) return rc;
-        lp.p[l] = grad_pyr[l];
-    }
-    return hip_status(launch_lookup_bwd(coords, grad_out, B, H, W, levels, radius, lp, (hipStream_t)stream),
-                      "corr_lookup_bwd");
+    return corr_lookup_bwd_rows(coords, grad_out, B, H * W, H, W, levels, radius, grad_pyr, stream);
 }
 
 int corr_pool_bwd(float *const *grad_pyr, int BN, int H, int W, int levels, void *stream) {
+    static const char *fn = "corr_pool_bwd";
     g_err[0] = 0;
-    int rc = check_dims("corr_pool_bwd", 1, H, W, levels);
+    int rc = check_dims(fn, 1, 1, H, W, levels);
     if (rc) return rc;
-    if (BN < 1) return fail(CORR_EINVAL, "corr_pool_bwd: BN must be >= 1");
-    if (!grad_pyr) return fail(CORR_EINVAL, "corr_pool_bwd: grad_pyr is NULL");
+    if (BN < 1) return fail(CORR_EINVAL, "%s: BN must be >= 1", fn);
     LevelPtrs lp{};
-    for (int l = 0; l < levels; ++l) {
-        if ((rc = check_ptr("corr_pool_bwd", grad_pyr[l], "grad_pyr[l]"))) return rc;
-        lp.p[l] = grad_pyr[l];
-    }
-    return hip_status(launch_pool_bwd(lp, BN, H, W, levels, (hipStream_t)stream), "corr_pool_bwd");
+    if ((rc = check_levels(fn, grad_pyr, levels, "grad_pyr", lp.p))) return rc;
+    return hip_status(launch_pool_bwd(lp, BN, H, W, levels, (hipStream_t)stream), fn);
+}
+
+size_t corr_build_bwd_rows_workspace(int B, int D, int NQ, int H, int W) {
+    if (B < 1 || D < 1 || NQ < 1 || H < 1 || W < 1) return 0;
+    return build_bwd_workspace(B, D, NQ, H, W);
 }
 
 size_t corr_build_bwd_workspace(int B, int D, int H, int W) {
-    if (B < 1 || D < 1 || H < 1 || W < 1) return 0;
-    return build_bwd_workspace(B, D, H, W);
+    return corr_build_bwd_rows_workspace(B, D, H * W, H, W);
+}
+
+int corr_build_bwd_rows(const float *grad_c, const float *fmap1_rows, int NQ, const float *fmap2,
+                        int B, int D, int H, int W, float *dfmap1_rows, float *dfmap2,
+                        void *workspace, size_t workspace_bytes, void *stream) {
+    static const char *fn = "corr_build_bwd";
+    g_err[0] = 0;
+    int rc = check_dims(fn, B, NQ, H, W, 1);
+    if (rc) return rc;
+    if (D < 1) return fail(CORR_EINVAL, "%s: D must be >= 1 (got %d)", fn, D);
+    if ((rc = check_ptr(fn, grad_c, "grad_c")) || (rc = check_ptr(fn, fmap1_rows, "fmap1")) ||
+        (rc = check_ptr(fn, fmap2, "fmap2")) || (rc = check_ptr(fn, dfmap1_rows, "dfmap1")) ||
+        (rc = check_ptr(fn, dfmap2, "dfmap2")))
+        return rc;
+    const size_t need = build_bwd_workspace(B, D, NQ, H, W);
+    if (workspace_bytes < need || (need && !workspace))
+        return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
+    return hip_status(launch_build_bwd(grad_c, fmap1_rows, NQ, fmap2, B, D, H, W, dfmap1_rows, dfmap2,
+                                       (float *)workspace, (hipStream_t)stream),
+                      fn);
 }
 
 int corr_build_bwd(const float *grad_c, const float *fmap1, const float *fmap2, int B, int D,
                    int H, int W, float *dfmap1, float *dfmap2, void *workspace,
                    size_t workspace_bytes, void *stream) {
-    g_err[0] = 0;
-    int rc = check_dims("corr_build_bwd", B, H, W, 1);
-    if (rc) return rc;
-    if (D < 1) return fail(CORR_EINVAL, "corr_build_bwd: D must be >= 1 (got %d)", D);
-    if ((rc = check_ptr("corr_build_bwd", grad_c, "grad_c")) ||
-        (rc = check_ptr("corr_build_bwd", fmap1, "fmap1")) ||
-        (rc = check_ptr("corr_build_bwd", fmap2, "fmap2")) ||
-        (rc = check_ptr("corr_build_bwd", dfmap1, "dfmap1")) ||
-        (rc = check_ptr("corr_build_bwd", dfmap2, "dfmap2")))
-        return rc;
-    const size_t need = build_bwd_workspace(B, D, H, W);
-    if (workspace_bytes < need || (need && !workspace))
-        return fail(CORR_EINVAL, "corr_build_bwd: workspace of %zu bytes needed, got %zu", need,
-                    workspace_bytes);
-    return hip_status(launch_build_bwd(grad_c, fmap1, fmap2, B, D, H, W, dfmap1, dfmap2,
-                                       (float *)workspace, (hipStream_t)stream),
-                      "corr_build_bwd");
+    return corr_build_bwd_rows(grad_c, fmap1, H * W, fmap2, B, D, H, W, dfmap1, dfmap2, workspace,
+                               workspace_bytes, stream);
 }
 
 }  // extern "C"

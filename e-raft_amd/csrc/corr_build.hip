@@ -3,35 +3,53 @@
 // Replaces CorrBlock.corr (model/corr.py:52-60: matmul(F1^T, F2) / sqrt(D)) and the pyramid
 // loop of CorrBlock.__init__ (model/corr.py:21-27: avg_pool2d(2, stride 2) x (L-1)).
 //
-// One workgroup (4 waves) owns a tile of 128 query pixels x one 8x16 patch of target pixels
-// (128 targets).  K = D is staged through LDS in 32-deep chunks (double-buffered, register
-// prefetch of chunk c+1 while chunk c feeds the MFMAs).  Each wave computes 64 queries x an
-// 8x8 target sub-patch with v_mfma_f32_32x32x2_f32 (exact fp32: a k-ordered fmaf chain):
-// A = targets (MFMA rows), B = queries (MFMA columns), so every lane ends up owning ONE query
-// and a 4x8 block of target pixels (lanes l, l+32 hold the two 4-wide halves of the 8x8).
-// The epilogue applies 1/sqrt(D), writes level 0, and pools levels 1..3 in registers
-// (level 3 needs one cross-half shuffle) — every pyramid level leaves the chip exactly once.
+// A workgroup of WQ x WT waves owns a tile of BQ = 32*QT*WQ query pixels x one 8 x (8*WT)
+// patch of target pixels.  K = D is staged through LDS in BK-deep chunks (double-buffered;
+// the global loads of chunk c+1 are in flight while chunk c feeds the MFMAs).  Each wave
+// computes (32*QT) queries x an 8x8 target sub-patch with v_mfma_f32_32x32x2_f32 (exact
+// fp32: a k-ordered fmaf chain): A = targets (MFMA rows), B = queries (MFMA columns), so every
+// lane ends up owning ONE query and a 4x8 block of target pixels (lanes l, l+32 hold the two
+// 4-wide halves of the 8x8).  The epilogue applies 1/sqrt(D), writes level 0 and pools levels
+// 1..3 in registers (level 3 needs one cross-half shuffle) — every pyramid level leaves the
+// chip exactly once; no level is re-read to build the next.
+//
+// The k-order of every accumulation (chunks in order, k = 2s + h inside a chunk) does not
+// depend on the tile geometry, so all BuildCfg instantiations give bit-identical results.
 #include <algorithm>
 #include <cmath>
 
 #include "corr_common.h"
 
 namespace corr {
-namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kBQ = 128;  // queries per tile
-constexpr int kPH = 8;    // target patch rows
-constexpr int kPW = 16;   // target patch cols  (kPH * kPW = 128 targets per tile)
-constexpr int kBK = 32;   // k-chunk staged in LDS
-constexpr int kThreads = 256;
+// Tile geometry.  WQ x WT waves; each wave QT query tiles of 32 x one 8x8 target sub-patch.
+// PF: read all of a chunk's MFMA operands from LDS before issuing its MFMAs.
+template <int WQ_, int WT_, int QT_, int BK_, int OCC_, bool PF_ = false>
+struct BuildCfg {
+    static constexpr int WQ = WQ_, WT = WT_, QT = QT_, BK = BK_, OCC = OCC_;
+    static constexpr bool PF = PF_;
+    static constexpr int NT = 64 * WQ * WT;  // threads
+    static constexpr int BQ = 32 * QT * WQ;  // queries per tile
+    static constexpr int PW = 8 * WT;        // target patch columns (8 rows)
+    static constexpr int BT = 64 * WT;       // targets per tile
+    static constexpr int QPT = BK * BQ / 4 / NT;  // float4 staged per thread per chunk (queries)
+    static constexpr int TPT = BK * BT / 4 / NT;  // ... (targets)
+    static constexpr size_t LDS = 2ull * BK * (BQ + BT) * sizeof(float);
+    static_assert(BK * BQ / 4 % NT == 0 && BK * BT / 4 % NT == 0, "staging must tile the chunk");
+    static_assert(NT % (BQ / 4) == 0 && NT % (BT / 4) == 0, "fixed staging column per thread");
+};
+
+// Default geometry (selected by tools/kbench_build.hip measurements).
+using BuildDefault = BuildCfg<2, 2, 2, 32, 2>;
 
 struct BuildParams {
     const float *f1;
     const float *f2;
     float *lvl[kFusedLevels];
-    int B, D, H, W, N;
+    int B, D, H, W, N;  // N = H*W target pixels per batch item
+    int NQ;             // query pixels per batch item (N, or a row slab of it)
     int nlev;           // levels written by the epilogue (1..4)
     int nq, npx, npy;   // query blocks, patch columns, patch rows
     float inv_s, s;
@@ -53,110 +71,145 @@ __device__ __forceinline__ float pool4(float a, float b, float c, float d) {
     return t * 0.25f;
 }
 
-template <bool VEC>
-__global__ __launch_bounds__(kThreads, 2) void corr_build_kernel(BuildParams p) {
-    __shared__ __attribute__((aligned(16))) float sm[2][2][kBK][128];  // [stage][Q,T][k][idx]
+template <class Cfg, bool VEC>
+__global__ __launch_bounds__(Cfg::NT, Cfg::OCC) void corr_build_kernel(BuildParams p) {
+    constexpr int NT = Cfg::NT, BQ = Cfg::BQ, BT = Cfg::BT, BK = Cfg::BK, QT = Cfg::QT;
+    constexpr int PW = Cfg::PW, QPT = Cfg::QPT, TPT = Cfg::TPT;
+    extern __shared__ __attribute__((aligned(16))) float smem[];  // [stage][BK][BQ + BT]
 
     const int tile = xcd_swizzle(blockIdx.x, gridDim.x);
     const int px = tile % p.npx;
     const int py = (tile / p.npx) % p.npy;
     const int qb = (tile / (p.npx * p.npy)) % p.nq;
     const int b = tile / (p.npx * p.npy * p.nq);
-    const int q0 = qb * kBQ;
-    const int N = p.N, W = p.W, H = p.H, D = p.D;
+    const int q0 = qb * BQ;
+    const int N = p.N, NQ = p.NQ, W = p.W, H = p.H, D = p.D;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, h = lane >> 5, l32 = lane & 31;
-    const int wv = tid >> 6, wq = wv >> 1, wt = wv & 1;
+    const int wv = tid >> 6, wq = wv / Cfg::WT, wt = wv % Cfg::WT;
 
-    // ---- staging assignment: rows k = kr + 8*i (i = 0..3), 4 consecutive idx at c4 ----
-    const int kr = tid >> 5;
-    const int c4 = (tid & 31) * 4;
-    const int qidx = q0 + c4;  // query of staged element e: qidx + e
+    // ---- staging: thread -> fixed column (4 consecutive idx), rows k advance by a stride ----
+    constexpr int QCOLS = BQ / 4, TCOLS = BT / 4;
+    constexpr int QKSTEP = NT / QCOLS, TKSTEP = NT / TCOLS;
+    const int qk = tid / QCOLS, qc4 = (tid % QCOLS) * 4;
+    const int tk = tid / TCOLS, tc4 = (tid % TCOLS) * 4;
+    const int qidx = q0 + qc4;
     // target patch layout inside a tile: idx = wt*64 + tt*32 + y4*8 + x8
-    const int sy = ((c4 >> 5) & 1) * 4 + ((c4 >> 3) & 3);
-    const int sx = (c4 >> 6) * 8 + (c4 & 7);
-    const int tY = py * kPH + sy, tX = px * kPW + sx;
+    const int sy = ((tc4 >> 5) & 1) * 4 + ((tc4 >> 3) & 3);
+    const int sx = (tc4 >> 6) * 8 + (tc4 & 7);
+    const int tY = py * 8 + sy, tX = px * PW + sx;
     const size_t tOff = (size_t)tY * W + tX;
-    const float *f1b = p.f1 + (size_t)b * D * N;
+    const bool tvalid = tY < H && tX < W;
+    const float *f1b = p.f1 + (size_t)b * D * NQ;
     const float *f2b = p.f2 + (size_t)b * D * N;
 
-    float4 rq[4], rt[4];
+    float4 rq[QPT], rt[TPT];
     auto load_chunk = [&](int k0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int k = k0 + kr + 8 * i;
-            const bool kv = k < D;
+        for (int i = 0; i < QPT; ++i) {
+            const int k = k0 + qk + QKSTEP * i;
             if (VEC) {
-                rq[i] = (kv && qidx < N) ? *reinterpret_cast<const float4 *>(f1b + (size_t)k * N + qidx)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
-                rt[i] = (kv && tY < H && tX < W)
-                            ? *reinterpret_cast<const float4 *>(f2b + (size_t)k * N + tOff)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
+                rq[i] = (k < D && qidx < NQ) ? *reinterpret_cast<const float4 *>(f1b + (size_t)k * NQ + qidx)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
             } else {
-                float qv[4], tv[4];
+                float v[4];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    qv[e] = (kv && qidx + e < N) ? f1b[(size_t)k * N + qidx + e] : 0.f;
-                    tv[e] = (kv && tY < H && tX + e < W) ? f2b[(size_t)k * N + tOff + e] : 0.f;
-                }
-                rq[i] = make_float4(qv[0], qv[1], qv[2], qv[3]);
-                rt[i] = make_float4(tv[0], tv[1], tv[2], tv[3]);
+                for (int e = 0; e < 4; ++e) v[e] = (k < D && qidx + e < NQ) ? f1b[(size_t)k * NQ + qidx + e] : 0.f;
+                rq[i] = make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TPT; ++i) {
+            const int k = k0 + tk + TKSTEP * i;
+            if (VEC) {
+                rt[i] = (k < D && tvalid) ? *reinterpret_cast<const float4 *>(f2b + (size_t)k * N + tOff)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    v[e] = (k < D && tY < H && tX + e < W) ? f2b[(size_t)k * N + tOff + e] : 0.f;
+                rt[i] = make_float4(v[0], v[1], v[2], v[3]);
             }
         }
     };
     auto store_chunk = [&](int st) {
+        float *Qs = smem + (size_t)st * BK * (BQ + BT);
+        float *Ts = Qs + BK * BQ;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            *reinterpret_cast<float4 *>(&sm[st][0][kr + 8 * i][c4]) = rq[i];
-            *reinterpret_cast<float4 *>(&sm[st][1][kr + 8 * i][c4]) = rt[i];
-        }
+        for (int i = 0; i < QPT; ++i)
+            *reinterpret_cast<float4 *>(&Qs[(qk + QKSTEP * i) * BQ + qc4]) = rq[i];
+#pragma unroll
+        for (int i = 0; i < TPT; ++i)
+            *reinterpret_cast<float4 *>(&Ts[(tk + TKSTEP * i) * BT + tc4]) = rt[i];
     };
 
-    f32x16 acc[2][2];
+    f32x16 acc[QT][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < QT; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    const int nchunks = (D + kBK - 1) / kBK;
+    const int nchunks = (D + BK - 1) / BK;
     load_chunk(0);
     store_chunk(0);
     __syncthreads();
 
     for (int c = 0; c < nchunks; ++c) {
         const int st = c & 1;
-        if (c + 1 < nchunks) load_chunk((c + 1) * kBK);
-        const float *Qs = &sm[st][0][0][0];
-        const float *Ts = &sm[st][1][0][0];
+        if (c + 1 < nchunks) load_chunk((c + 1) * BK);
+        const float *Qs = smem + (size_t)st * BK * (BQ + BT);
+        const float *Ts = Qs + BK * BQ;
+        if constexpr (Cfg::PF) {
+            float bq[BK / 2][QT], a0[BK / 2], a1[BK / 2];
 #pragma unroll
-        for (int s = 0; s < kBK / 2; ++s) {
-            const int k = 2 * s + h;
-            const float b0 = Qs[k * 128 + wq * 64 + l32];
-            const float b1 = Qs[k * 128 + wq * 64 + 32 + l32];
-            const float a0 = Ts[k * 128 + wt * 64 + l32];
-            const float a1 = Ts[k * 128 + wt * 64 + 32 + l32];
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+            for (int s = 0; s < BK / 2; ++s) {
+                const int k = 2 * s + h;
+#pragma unroll
+                for (int i = 0; i < QT; ++i) bq[s][i] = Qs[k * BQ + wq * (32 * QT) + i * 32 + l32];
+                a0[s] = Ts[k * BT + wt * 64 + l32];
+                a1[s] = Ts[k * BT + wt * 64 + 32 + l32];
+            }
+#pragma unroll
+            for (int s = 0; s < BK / 2; ++s)
+#pragma unroll
+                for (int i = 0; i < QT; ++i) {
+                    acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], bq[s][i], acc[i][0], 0, 0, 0);
+                    acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], bq[s][i], acc[i][1], 0, 0, 0);
+                }
+        } else {
+#pragma unroll
+            for (int s = 0; s < BK / 2; ++s) {
+                const int k = 2 * s + h;
+                float bq[QT];
+#pragma unroll
+                for (int i = 0; i < QT; ++i) bq[i] = Qs[k * BQ + wq * (32 * QT) + i * 32 + l32];
+                const float a0 = Ts[k * BT + wt * 64 + l32];
+                const float a1 = Ts[k * BT + wt * 64 + 32 + l32];
+#pragma unroll
+                for (int i = 0; i < QT; ++i) {
+                    acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bq[i], acc[i][0], 0, 0, 0);
+                    acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bq[i], acc[i][1], 0, 0, 0);
+                }
+            }
         }
         if (c + 1 < nchunks) store_chunk(st ^ 1);
         __syncthreads();
     }
 
     // ---- epilogue: scale, level 0, in-register pyramid ----
-    // acc[qt][tt][r]: query q0 + wq*64 + qt*32 + l32, target (y, x) of the wave's 8x8
+    // acc[qt][tt][r]: query q0 + wq*32*QT + qt*32 + l32, target (y, x) of the wave's 8x8
     // sub-patch with y = tt*4 + (r >> 2), x = 4h + (r & 3)   (32x32 C/D map).
     const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
-    const int X0 = px * kPW + wt * 8 + 4 * h, Y0 = py * kPH;
+    const int X0 = px * PW + wt * 8 + 4 * h, Y0 = py * 8;
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-        const int q = q0 + wq * 64 + qt * 32 + l32;
-        const bool qok = q < N;
-        const size_t qrow = (size_t)b * N + q;
+    for (int qt = 0; qt < QT; ++qt) {
+        const int q = q0 + wq * 32 * QT + qt * 32 + l32;
+        const bool qok = q < NQ;
+        const size_t qrow = (size_t)b * NQ + q;
         float v[8][4];
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt)
@@ -229,6 +282,8 @@ __global__ __launch_bounds__(kThreads, 2) void corr_build_kernel(BuildParams p) 
     }
 }
 
+namespace {
+
 // Levels beyond the fused four: plain 2x2 average pool of level l-1 into level l.
 __global__ __launch_bounds__(256) void pool2x2_kernel(const float *__restrict__ in,
                                                       float *__restrict__ out, long BN, int H,
@@ -267,8 +322,10 @@ hipError_t launch_pool_levels(const LevelPtrs &pyr, int l_from, int levels, long
     return hipSuccess;
 }
 
-hipError_t launch_build(const float *f1, const float *f2, int B, int D, int H, int W, int levels,
-                        const LevelPtrs &pyr, hipStream_t s) {
+// Launch one build with tile geometry Cfg (exposed for tools/kbench_build.hip).
+template <class Cfg>
+hipError_t launch_build_cfg(const float *f1, int NQ, const float *f2, int B, int D, int H, int W,
+                            int levels, const LevelPtrs &pyr, hipStream_t s) {
     BuildParams p{};
     p.f1 = f1;
     p.f2 = f2;
@@ -277,29 +334,50 @@ hipError_t launch_build(const float *f1, const float *f2, int B, int D, int H, i
     p.H = H;
     p.W = W;
     p.N = H * W;
+    p.NQ = NQ;
     p.nlev = levels < kFusedLevels ? levels : kFusedLevels;
     for (int l = 0; l < kFusedLevels; ++l) p.lvl[l] = l < p.nlev ? pyr.p[l] : nullptr;
-    p.nq = (p.N + kBQ - 1) / kBQ;
-    p.npx = (W + kPW - 1) / kPW;
-    p.npy = (H + kPH - 1) / kPH;
+    p.nq = (NQ + Cfg::BQ - 1) / Cfg::BQ;
+    p.npx = (W + Cfg::PW - 1) / Cfg::PW;
+    p.npy = (H + 7) / 8;
     p.s = std::sqrt((float)D);
     p.exact_mul = is_pow2(p.s);
     p.inv_s = 1.0f / p.s;
 
     // float4 staging / level-0 stores need 16-B aligned rows and patch columns.
-    const bool vec = (W % 4 == 0) && ((uintptr_t)pyr.p[0] % 16 == 0) &&
+    const bool vec = (W % 4 == 0) && (NQ % 4 == 0) && ((uintptr_t)pyr.p[0] % 16 == 0) &&
                      ((uintptr_t)f1 % 16 == 0) && ((uintptr_t)f2 % 16 == 0);
-
     const long tiles = (long)p.nq * p.npx * p.npy * B;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
-    if (vec)
-        hipLaunchKernelGGL(corr_build_kernel<true>, dim3((unsigned)tiles), dim3(kThreads), 0, s, p);
-    else
-        hipLaunchKernelGGL(corr_build_kernel<false>, dim3((unsigned)tiles), dim3(kThreads), 0, s, p);
+    static bool attr_set[2] = {false, false};
+    if (vec) {
+        if (!attr_set[1]) {
+            hipError_t e = hipFuncSetAttribute((const void *)corr_build_kernel<Cfg, true>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
+            if (e != hipSuccess) return e;
+            attr_set[1] = true;
+        }
+        hipLaunchKernelGGL((corr_build_kernel<Cfg, true>), dim3((unsigned)tiles), dim3(Cfg::NT),
+                           Cfg::LDS, s, p);
+    } else {
+        if (!attr_set[0]) {
+            hipError_t e = hipFuncSetAttribute((const void *)corr_build_kernel<Cfg, false>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
+            if (e != hipSuccess) return e;
+            attr_set[0] = true;
+        }
+        hipLaunchKernelGGL((corr_build_kernel<Cfg, false>), dim3((unsigned)tiles), dim3(Cfg::NT),
+                           Cfg::LDS, s, p);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (levels > kFusedLevels) return launch_pool_levels(pyr, kFusedLevels, levels, (long)B * p.N, H, W, s);
+    if (levels > kFusedLevels) return launch_pool_levels(pyr, kFusedLevels, levels, (long)B * NQ, H, W, s);
     return hipSuccess;
+}
+
+hipError_t launch_build(const float *f1, int NQ, const float *f2, int B, int D, int H, int W,
+                        int levels, const LevelPtrs &pyr, hipStream_t s) {
+    return launch_build_cfg<BuildDefault>(f1, NQ, f2, B, D, H, W, levels, pyr, s);
 }
 
 }  // namespace corr

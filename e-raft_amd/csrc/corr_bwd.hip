@@ -230,24 +230,24 @@ hipError_t run_gemm(bool b_kcontig, const float *A, const float *Bm, float *C, i
 
 }  // namespace
 
-size_t build_bwd_workspace(int B, int D, int H, int W) {
+size_t build_bwd_workspace(int B, int D, int NQ, int H, int W) {
     const int N = H * W;
-    const int splits = plan_splits(D, N, N, B);
     // every GEMM goes through the slab path when sqrt(D) is not a power of two
-    const int need = std::max(splits, 1);
-    return (size_t)need * B * D * N * sizeof(float);
+    const size_t s1 = (size_t)plan_splits(D, NQ, N, B) * B * D * NQ;  // dF1
+    const size_t s2 = (size_t)plan_splits(D, N, NQ, B) * B * D * N;   // dF2
+    return std::max(s1, s2) * sizeof(float);
 }
 
-hipError_t launch_build_bwd(const float *grad_c, const float *f1, const float *f2, int B, int D,
-                            int H, int W, float *df1, float *df2, float *ws, hipStream_t s) {
-    const int N = H * W;
+hipError_t launch_build_bwd(const float *grad_c, const float *f1, int NQ, const float *f2, int B,
+                            int D, int H, int W, float *df1, float *df2, float *ws, hipStream_t s) {
+    const int N = H * W;  // targets; grad_c is [B*NQ][N]
     const float sc = std::sqrt((float)D);
-    const long DN = (long)D * N, NN = (long)N * N;
+    const long DN = (long)D * N, DQ = (long)D * NQ, QN = (long)NQ * N;
     // dF1[d][n] = sum_m F2[d][m] * dC[n][m]      A = F2 (k-contig), B(k=m, n) = dC[n*N + m]
-    hipError_t e = run_gemm(true, f2, grad_c, df1, D, N, N, B, N, N, N, DN, NN, DN, sc, ws, s);
+    hipError_t e = run_gemm(true, f2, grad_c, df1, D, NQ, N, B, N, N, NQ, DN, QN, DQ, sc, ws, s);
     if (e != hipSuccess) return e;
     // dF2[d][m] = sum_n F1[d][n] * dC[n][m]      A = F1 (k-contig), B(k=n, m) = dC[n*N + m]
-    return run_gemm(false, f1, grad_c, df2, D, N, N, B, N, N, N, DN, NN, DN, sc, ws, s);
+    return run_gemm(false, f1, grad_c, df2, D, N, NQ, B, NQ, N, N, DQ, QN, DN, sc, ws, s);
 }
 
 }  // namespace corr

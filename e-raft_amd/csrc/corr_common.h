@@ -25,19 +25,21 @@ int fail(int code, const char *fmt, ...);
 int hip_status(hipError_t e, const char *what);
 
 // Launch entry points implemented in the .hip translation units (all asynchronous).
-hipError_t launch_build(const float *f1, const float *f2, int B, int D, int H, int W,
+// NQ = query pixels per batch item (H*W for the reference shape, rows*W for a row slab);
+// H, W = the target map (fmap2) whose pyramid levels are [B*NQ][H>>l][W>>l].
+hipError_t launch_build(const float *f1, int NQ, const float *f2, int B, int D, int H, int W,
                         int levels, const LevelPtrs &pyr, hipStream_t s);
 hipError_t launch_pool_levels(const LevelPtrs &pyr, int l_from, int levels, long BN, int H,
                               int W, hipStream_t s);
-hipError_t launch_lookup(const ConstLevelPtrs &pyr, const float *coords, int B, int H, int W,
-                         int levels, int radius, float *out, hipStream_t s);
-hipError_t launch_lookup_bwd(const float *coords, const float *grad_out, int B, int H, int W,
-                             int levels, int radius, const LevelPtrs &gpyr, hipStream_t s);
+hipError_t launch_lookup(const ConstLevelPtrs &pyr, const float *coords, int B, int NQ, int H,
+                         int W, int levels, int radius, float *out, hipStream_t s);
+hipError_t launch_lookup_bwd(const float *coords, const float *grad_out, int B, int NQ, int H,
+                             int W, int levels, int radius, const LevelPtrs &gpyr, hipStream_t s);
 hipError_t launch_pool_bwd(const LevelPtrs &gpyr, long BN, int H, int W, int levels,
                            hipStream_t s);
-size_t build_bwd_workspace(int B, int D, int H, int W);
-hipError_t launch_build_bwd(const float *grad_c, const float *f1, const float *f2, int B, int D,
-                            int H, int W, float *df1, float *df2, float *ws, hipStream_t s);
+size_t build_bwd_workspace(int B, int D, int NQ, int H, int W);
+hipError_t launch_build_bwd(const float *grad_c, const float *f1, int NQ, const float *f2, int B,
+                            int D, int H, int W, float *df1, float *df2, float *ws, hipStream_t s);
 
 // Number of levels the build kernel pools in its epilogue (8x8 target patches).
 constexpr int kFusedLevels = 4;

@@ -114,30 +114,73 @@ __device__ __forceinline__ void gather_window(float *win, const int *ax, const i
     }
 }
 
-template <int S>
+// Forward gather: one wave per query at a time, lane -> fixed neighbourhood cells, so the
+// (row, col) of each lane's cells is computed once and every load's address is
+// anchor + constant (no per-element integer division).
+template <int S, int QB, int NT>
+__device__ __forceinline__ void gather_window_wave(float *win, const int *ax, const int *ay,
+                                                   const float *P, size_t qbase, size_t mapsz,
+                                                   int n0, int N, int Wl, int Hl, int tid) {
+    constexpr int WIN = S + 2, WS = WIN * WIN, WSTR = WS | 1;
+    constexpr int NW = NT / 64;
+    constexpr int EPL = (WS + 63) / 64;   // cells per lane per query
+    constexpr int QPW = (QB + NW - 1) / NW;  // queries per wave
+    const int lane = tid & 63, w = tid >> 6;
+    int ry[EPL], rx[EPL];
+#pragma unroll
+    for (int v = 0; v < EPL; ++v) {
+        const int e = lane + 64 * v;
+        ry[v] = e / WIN;
+        rx[v] = e - ry[v] * WIN;
+    }
+    float vals[QPW][EPL];
+#pragma unroll
+    for (int k = 0; k < QPW; ++k) {
+        const int qq = w + NW * k;
+        const bool qv = qq < QB && n0 + qq < N;
+        const int X0 = qv ? ax[qq] : kFarAnchor, Y0 = qv ? ay[qq] : kFarAnchor;
+        const float *Pq = P + (qbase + qq) * mapsz;
+#pragma unroll
+        for (int v = 0; v < EPL; ++v) {
+            const int X = X0 + rx[v], Y = Y0 + ry[v];
+            const bool ok = (lane + 64 * v < WS) && X >= 0 && X < Wl && Y >= 0 && Y < Hl;
+            vals[k][v] = ok ? Pq[(size_t)Y * Wl + X] : 0.0f;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < QPW; ++k) {
+        const int qq = w + NW * k;
+#pragma unroll
+        for (int v = 0; v < EPL; ++v)
+            if (qq < QB && lane + 64 * v < WS) win[qq * WSTR + lane + 64 * v] = vals[k][v];
+    }
+}
+
+template <int S, int QB>
 struct LookupSmem {
     static constexpr int WIN = S + 2;
     static constexpr int WSTR = (WIN * WIN) | 1;  // odd stride: conflict-free lane = query reads
-    float win[kQB * WSTR];
-    float ty[3][S][kQB];
-    float fx[2][kQB];  // floor of x-tap 0 and S-1
-    int ax[kQB], ay[kQB];
+    float win[QB * WSTR];
+    float ty[3][S][QB];
+    float fx[2][QB];  // floor of x-tap 0 and S-1
+    int ax[QB], ay[QB];
 };
 
-template <int S>
-__global__ __launch_bounds__(64 * S) void lookup_kernel(ConstLevelPtrs pyr,
-                                                        const float *__restrict__ coords, int B,
-                                                        int H, int W, int L,
-                                                        float *__restrict__ out) {
-    constexpr int R = (S - 1) / 2, K = S * S, NT = 64 * S;
-    using SM = LookupSmem<S>;
+constexpr int lookup_threads(int S, int QB) { return (QB * S + 63) / 64 * 64; }
+
+template <int S, int QB>
+__global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
+    ConstLevelPtrs pyr, const float *__restrict__ coords, int B, int NQ, int H, int W, int L,
+    float *__restrict__ out) {
+    constexpr int R = (S - 1) / 2, K = S * S, NT = lookup_threads(S, QB);
+    using SM = LookupSmem<S, QB>;
     constexpr int WIN = SM::WIN, WSTR = SM::WSTR;
     __shared__ SM sm;
 
-    const int N = H * W;
-    const int nqb = (N + kQB - 1) / kQB;
+    const int N = NQ;  // query pixels per batch item (H*W, or a row slab of it)
+    const int nqb = (N + QB - 1) / QB;
     const int b = blockIdx.x / nqb;
-    const int n0 = (blockIdx.x - b * nqb) * kQB;
+    const int n0 = (blockIdx.x - b * nqb) * QB;
     const int l = blockIdx.y;
     const int Hl = H >> l, Wl = W >> l;
     const float inv_scale = 1.0f / (float)(1 << l);
@@ -146,16 +189,17 @@ __global__ __launch_bounds__(64 * S) void lookup_kernel(ConstLevelPtrs pyr,
     const size_t qbase = (size_t)b * N + n0;
 
     const int tid = threadIdx.x;
-    const int q = tid & (kQB - 1);
-    const int i = tid >> 6;  // this wave's x-tap (window column)
+    const int q = tid % QB;
+    const int i = tid / QB;  // this thread's x-tap (window column); i >= S: gather only
+    const bool act = i < S;
     const int n = n0 + q;
-    const bool qok = n < N;
+    const bool qok = act && n < N;
 
     // ---- 1. taps ----
     const float cxv = qok ? coords[((size_t)b * 2 + 0) * N + n] : 0.0f;
     const float cyv = qok ? coords[((size_t)b * 2 + 1) * N + n] : 0.0f;
     const Axis tx = tap_axis(cxv, inv_scale, i, R, Wl);
-    {
+    if (act) {
         const Axis a = tap_axis(cyv, inv_scale, i, R, Hl);
         sm.ty[0][i][q] = a.f;
         sm.ty[1][i][q] = a.lo;
@@ -170,9 +214,10 @@ __global__ __launch_bounds__(64 * S) void lookup_kernel(ConstLevelPtrs pyr,
     __syncthreads();
 
     // ---- 2. neighbourhoods -> LDS ----
-    gather_window<S, NT>(sm.win, sm.ax, sm.ay, P, qbase, mapsz, n0, N, Wl, Hl, tid);
+    gather_window_wave<S, QB, NT>(sm.win, sm.ax, sm.ay, P, qbase, mapsz, n0, N, Wl, Hl, tid);
     const int slow = __syncthreads_or(
-        !window_covers<S>(sm.fx[0][q], sm.fx[1][q], sm.ty[0][0][q], sm.ty[0][S - 1][q]));
+        act && !window_covers<S>(sm.fx[0][q], sm.fx[1][q], sm.ty[0][0][q], sm.ty[0][S - 1][q]));
+    if (!act) return;
 
     // ---- 3. outputs (i, 0..S-1) of query q ----
     const int ax = sm.ax[q], ay = sm.ay[q];
@@ -231,7 +276,7 @@ struct LookupBwdSmem {
 template <int S>
 __global__ __launch_bounds__(64 * S) void lookup_bwd_kernel(const float *__restrict__ coords,
                                                             const float *__restrict__ grad_out,
-                                                            int B, int H, int W, int L,
+                                                            int B, int NQ, int H, int W, int L,
                                                             LevelPtrs gpyr) {
     constexpr int R = (S - 1) / 2, K = S * S, NT = 64 * S;
     using SM = LookupBwdSmem<S>;
@@ -239,7 +284,7 @@ __global__ __launch_bounds__(64 * S) void lookup_bwd_kernel(const float *__restr
     constexpr int C = S + 1;  // cells per axis reached by regular taps
     __shared__ SM sm;
 
-    const int N = H * W;
+    const int N = NQ;  // query pixels per batch item (H*W, or a row slab of it)
     const int nqb = (N + kQB - 1) / kQB;
     const int b = blockIdx.x / nqb;
     const int n0 = (blockIdx.x - b * nqb) * kQB;
@@ -390,51 +435,52 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const float *__restrict__
 }
 
 template <int S>
-hipError_t launch_lookup_s(const ConstLevelPtrs &pyr, const float *coords, int B, int H, int W,
-                           int L, float *out, hipStream_t s) {
-    const int nqb = (H * W + kQB - 1) / kQB;
-    hipLaunchKernelGGL(lookup_kernel<S>, dim3(nqb * B, L), dim3(64 * S), 0, s, pyr, coords, B, H, W,
-                       L, out);
+hipError_t launch_lookup_s(const ConstLevelPtrs &pyr, const float *coords, int B, int NQ, int H,
+                           int W, int L, float *out, hipStream_t s) {
+    constexpr int QB = 32;  // queries per workgroup: >= 2 workgroups per CU at DSEC size
+    const int nqb = (NQ + QB - 1) / QB;
+    hipLaunchKernelGGL((lookup_kernel<S, QB>), dim3(nqb * B, L), dim3(lookup_threads(S, QB)), 0, s,
+                       pyr, coords, B, NQ, H, W, L, out);
     return hipGetLastError();
 }
 
 template <int S>
-hipError_t launch_lookup_bwd_s(const float *coords, const float *grad_out, int B, int H, int W,
-                               int L, const LevelPtrs &gpyr, hipStream_t s) {
-    const int nqb = (H * W + kQB - 1) / kQB;
+hipError_t launch_lookup_bwd_s(const float *coords, const float *grad_out, int B, int NQ, int H,
+                               int W, int L, const LevelPtrs &gpyr, hipStream_t s) {
+    const int nqb = (NQ + kQB - 1) / kQB;
     hipLaunchKernelGGL(lookup_bwd_kernel<S>, dim3(nqb * B, L), dim3(64 * S), 0, s, coords, grad_out,
-                       B, H, W, L, gpyr);
+                       B, NQ, H, W, L, gpyr);
     return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t launch_lookup(const ConstLevelPtrs &pyr, const float *coords, int B, int H, int W,
-                         int levels, int radius, float *out, hipStream_t s) {
+hipError_t launch_lookup(const ConstLevelPtrs &pyr, const float *coords, int B, int NQ, int H,
+                         int W, int levels, int radius, float *out, hipStream_t s) {
     switch (radius) {
-        case 0: return launch_lookup_s<1>(pyr, coords, B, H, W, levels, out, s);
-        case 1: return launch_lookup_s<3>(pyr, coords, B, H, W, levels, out, s);
-        case 2: return launch_lookup_s<5>(pyr, coords, B, H, W, levels, out, s);
-        case 3: return launch_lookup_s<7>(pyr, coords, B, H, W, levels, out, s);
-        case 4: return launch_lookup_s<9>(pyr, coords, B, H, W, levels, out, s);
-        case 5: return launch_lookup_s<11>(pyr, coords, B, H, W, levels, out, s);
-        case 6: return launch_lookup_s<13>(pyr, coords, B, H, W, levels, out, s);
-        case 7: return launch_lookup_s<15>(pyr, coords, B, H, W, levels, out, s);
+        case 0: return launch_lookup_s<1>(pyr, coords, B, NQ, H, W, levels, out, s);
+        case 1: return launch_lookup_s<3>(pyr, coords, B, NQ, H, W, levels, out, s);
+        case 2: return launch_lookup_s<5>(pyr, coords, B, NQ, H, W, levels, out, s);
+        case 3: return launch_lookup_s<7>(pyr, coords, B, NQ, H, W, levels, out, s);
+        case 4: return launch_lookup_s<9>(pyr, coords, B, NQ, H, W, levels, out, s);
+        case 5: return launch_lookup_s<11>(pyr, coords, B, NQ, H, W, levels, out, s);
+        case 6: return launch_lookup_s<13>(pyr, coords, B, NQ, H, W, levels, out, s);
+        case 7: return launch_lookup_s<15>(pyr, coords, B, NQ, H, W, levels, out, s);
         default: return hipErrorInvalidValue;
     }
 }
 
-hipError_t launch_lookup_bwd(const float *coords, const float *grad_out, int B, int H, int W,
-                             int levels, int radius, const LevelPtrs &gpyr, hipStream_t s) {
+hipError_t launch_lookup_bwd(const float *coords, const float *grad_out, int B, int NQ, int H,
+                             int W, int levels, int radius, const LevelPtrs &gpyr, hipStream_t s) {
     switch (radius) {
-        case 0: return launch_lookup_bwd_s<1>(coords, grad_out, B, H, W, levels, gpyr, s);
-        case 1: return launch_lookup_bwd_s<3>(coords, grad_out, B, H, W, levels, gpyr, s);
-        case 2: return launch_lookup_bwd_s<5>(coords, grad_out, B, H, W, levels, gpyr, s);
-        case 3: return launch_lookup_bwd_s<7>(coords, grad_out, B, H, W, levels, gpyr, s);
-        case 4: return launch_lookup_bwd_s<9>(coords, grad_out, B, H, W, levels, gpyr, s);
-        case 5: return launch_lookup_bwd_s<11>(coords, grad_out, B, H, W, levels, gpyr, s);
-        case 6: return launch_lookup_bwd_s<13>(coords, grad_out, B, H, W, levels, gpyr, s);
-        case 7: return launch_lookup_bwd_s<15>(coords, grad_out, B, H, W, levels, gpyr, s);
+        case 0: return launch_lookup_bwd_s<1>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
+        case 1: return launch_lookup_bwd_s<3>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
+        case 2: return launch_lookup_bwd_s<5>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
+        case 3: return launch_lookup_bwd_s<7>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
+        case 4: return launch_lookup_bwd_s<9>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
+        case 5: return launch_lookup_bwd_s<11>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
+        case 6: return launch_lookup_bwd_s<13>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
+        case 7: return launch_lookup_bwd_s<15>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -22,7 +22,9 @@ MAX_LEVELS = 8
 MAX_RADIUS = 7
 
 EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr_lookup_bwd",
-           "corr_pool_bwd", "corr_build_bwd_workspace", "corr_build_bwd")
+           "corr_pool_bwd", "corr_build_bwd_workspace", "corr_build_bwd", "corr_build_rows",
+           "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows_workspace",
+           "corr_build_bwd_rows")
 
 _lib = None
 
@@ -56,7 +58,14 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.corr_build_bwd_workspace.argtypes = [i, i, i, i]
     lib.corr_build_bwd_workspace.restype = sz
     lib.corr_build_bwd.argtypes = [vp, vp, vp, i, i, i, i, vp, vp, vp, sz, vp]
-    for f in ("corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd"):
+    lib.corr_build_rows.argtypes = [vp, i, vp, i, i, i, i, i, vp, vp]
+    lib.corr_lookup_rows.argtypes = [vp, vp, i, i, i, i, i, i, vp, vp]
+    lib.corr_lookup_bwd_rows.argtypes = [vp, vp, i, i, i, i, i, i, vp, vp]
+    lib.corr_build_bwd_rows_workspace.argtypes = [i, i, i, i, i]
+    lib.corr_build_bwd_rows_workspace.restype = sz
+    lib.corr_build_bwd_rows.argtypes = [vp, vp, i, vp, i, i, i, i, vp, vp, vp, sz, vp]
+    for f in ("corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd",
+              "corr_build_rows", "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows"):
         getattr(lib, f).restype = i
     if path is None:
         _lib = lib
@@ -91,26 +100,43 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+def _nq(t):
+    """Query pixels per batch item of a [B, C, rows, W] (or [B, C, NQ]) tensor."""
+    n = 1
+    for d in t.shape[2:]:
+        n *= d
+    return n
+
+
 def build(fmap1, fmap2, levels):
-    """corr_build into the caller-allocated level tensors ([B*H*W, 1, H>>l, W>>l])."""
-    B, D, H, W = fmap1.shape
+    """corr_build_rows into caller-allocated levels [B*NQ, 1, H>>l, W>>l].  fmap1 may be a row
+    slab [B, D, rows, W] of the query map; fmap2 is the full target map [B, D, H, W]."""
+    B, D, H, W = fmap2.shape
     a, b, pp = _dev(fmap1, "fmap1"), _dev(fmap2, "fmap2"), _ptrs(levels, "pyr")
     with torch.cuda.device(fmap1.device):
-        _check(load().corr_build(a, b, B, D, H, W, len(levels), pp, _stream(fmap1)))
+        _check(load().corr_build_rows(a, _nq(fmap1), b, B, D, H, W, len(levels), pp, _stream(fmap1)))
 
 
-def lookup(levels, coords, radius, out):
-    B, _, H, W = coords.shape
+def lookup(levels, coords, radius, out, H=None, W=None):
+    """corr_lookup_rows: coords [B, 2, rows, W] -> out [B, L*K, rows, W].  (H, W) = target map
+    (default: the coords' own, i.e. the reference shape)."""
+    B = coords.shape[0]
+    H = coords.shape[2] if H is None else H
+    W = coords.shape[3] if W is None else W
     pp, c, o = _ptrs(levels, "pyr"), _dev(coords, "coords"), _dev(out, "out")
     with torch.cuda.device(coords.device):
-        _check(load().corr_lookup(pp, c, B, H, W, len(levels), radius, o, _stream(coords)))
+        _check(load().corr_lookup_rows(pp, c, B, _nq(coords), H, W, len(levels), radius, o,
+                                       _stream(coords)))
 
 
-def lookup_bwd(coords, grad_out, radius, grad_levels):
-    B, _, H, W = coords.shape
+def lookup_bwd(coords, grad_out, radius, grad_levels, H=None, W=None):
+    B = coords.shape[0]
+    H = coords.shape[2] if H is None else H
+    W = coords.shape[3] if W is None else W
     c, g, gp = _dev(coords, "coords"), _dev(grad_out, "grad_out"), _ptrs(grad_levels, "grad_pyr")
     with torch.cuda.device(coords.device):
-        _check(load().corr_lookup_bwd(c, g, B, H, W, len(grad_levels), radius, gp, _stream(coords)))
+        _check(load().corr_lookup_bwd_rows(c, g, B, _nq(coords), H, W, len(grad_levels), radius, gp,
+                                           _stream(coords)))
 
 
 def pool_bwd(grad_levels, H, W):
@@ -121,17 +147,19 @@ def pool_bwd(grad_levels, H, W):
 
 
 def build_bwd(grad_c, fmap1, fmap2):
-    """Returns (dfmap1, dfmap2) for grad_c = dLoss/dcorr ([B*N, N] or any view of it)."""
-    B, D, H, W = fmap1.shape
+    """Returns (dfmap1, dfmap2) for grad_c = dLoss/dcorr ([B*NQ, H*W] or any view of it).
+    With a row slab fmap1, dfmap1 is the slab's and dfmap2 is this slab's partial sum."""
+    B, D, H, W = fmap2.shape
     for t, nm in ((grad_c, "grad_c"), (fmap1, "fmap1"), (fmap2, "fmap2")):
         _dev(t, nm)
     lib = load()
-    ws_bytes = lib.corr_build_bwd_workspace(B, D, H, W)
+    NQ = _nq(fmap1)
+    ws_bytes = lib.corr_build_bwd_rows_workspace(B, D, NQ, H, W)
     df1 = torch.empty_like(fmap1)
     df2 = torch.empty_like(fmap2)
     ws = torch.empty(max(1, ws_bytes // 4), dtype=torch.float32, device=fmap1.device)
     with torch.cuda.device(fmap1.device):
-        _check(lib.corr_build_bwd(_dev(grad_c, "grad_c"), _dev(fmap1, "fmap1"), _dev(fmap2, "fmap2"),
-                                  B, D, H, W, _dev(df1, "df1"), _dev(df2, "df2"), ws.data_ptr(),
-                                  ws_bytes, _stream(fmap1)))
+        _check(lib.corr_build_bwd_rows(grad_c.data_ptr(), fmap1.data_ptr(), NQ, fmap2.data_ptr(), B, D,
+                                       H, W, df1.data_ptr(), df2.data_ptr(), ws.data_ptr(), ws_bytes,
+                                       _stream(fmap1)))
     return df1, df2

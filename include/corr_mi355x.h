@@ -95,6 +95,30 @@ int corr_build_bwd(const float *grad_c, const float *fmap1, const float *fmap2, 
                    int H, int W, float *dfmap1, float *dfmap2, void *workspace,
                    size_t workspace_bytes, void *stream);
 
+/*
+ * Row-slab variants, for query-row sharding across GPUs (no reference counterpart: the
+ * reference has no multi-GPU CorrBlock).  The queries are NQ consecutive
+ * pixels of fmap1 — a block of whole rows, NQ = rows*W — while the targets are all H*W
+ * pixels of fmap2:
+ *   fmap1_rows [B][D][NQ]; pyramid level l [B*NQ][H>>l][W>>l];
+ *   coords_rows [B][2][NQ]; out_rows [B][levels*K][NQ]; grad_c [B*NQ][H*W].
+ * Every query's arithmetic is identical to the full-size call, so a row partition
+ * reproduces the unsharded results bit for bit.  corr_build_bwd_rows writes this slab's
+ * dfmap1 rows and its PARTIAL dfmap2 (sum it over the slabs, e.g. with an all-reduce).
+ * The reference-shaped functions above are these with NQ = H*W.
+ */
+int corr_build_rows(const float *fmap1_rows, int NQ, const float *fmap2, int B, int D, int H,
+                    int W, int levels, float *const *pyr, void *stream);
+int corr_lookup_rows(const float *const *pyr, const float *coords_rows, int B, int NQ, int H,
+                     int W, int levels, int radius, float *out_rows, void *stream);
+int corr_lookup_bwd_rows(const float *coords_rows, const float *grad_out_rows, int B, int NQ,
+                         int H, int W, int levels, int radius, float *const *grad_pyr,
+                         void *stream);
+size_t corr_build_bwd_rows_workspace(int B, int D, int NQ, int H, int W);
+int corr_build_bwd_rows(const float *grad_c, const float *fmap1_rows, int NQ, const float *fmap2,
+                        int B, int D, int H, int W, float *dfmap1_rows, float *dfmap2,
+                        void *workspace, size_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

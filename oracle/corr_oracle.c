@@ -116,9 +116,10 @@ static float corner(const float *P, int Hl, int Wl, float xf, float yf) {
  * Bilinear weights nw = ey*ex, ne = ey*wx, sw = ny*ex, se = ny*wx, accumulated
  * acc = v_nw*w_nw, then fmaf for ne, sw, se — bit-exact vs ATen grid_sampler_2d (CPU).
  */
-void oracle_lookup(const float *const *pyr, const float *coords, int B, int H, int W, int L,
-                   int r, float *out) {
-    const int N = H * W, S = 2 * r + 1, K = S * S;
+void oracle_lookup_rows(const float *const *pyr, const float *coords, int B, int NQ, int H,
+                        int W, int L, int r, float *out) {
+    /* NQ query pixels per batch item (H*W, or a row slab); (H, W) = the target map */
+    const int N = NQ, S = 2 * r + 1, K = S * S;
     for (int b = 0; b < B; ++b)
         for (int n = 0; n < N; ++n) {
             const float x = coords[((size_t)b * 2 + 0) * N + n];
@@ -158,9 +159,9 @@ static void corner_add(float *G, int Hl, int Wl, float xf, float yf, float v) {
  * ACCUMULATED into (the caller zeroes it once per build).  Contributions of a query stay in
  * its own map.  Order: taps (i, j) row-major, corners nw, ne, sw, se.
  */
-void oracle_lookup_bwd(const float *coords, const float *grad_out, int B, int H, int W, int L,
-                       int r, float *const *grad_pyr) {
-    const int N = H * W, S = 2 * r + 1, K = S * S;
+void oracle_lookup_bwd_rows(const float *coords, const float *grad_out, int B, int NQ, int H,
+                            int W, int L, int r, float *const *grad_pyr) {
+    const int N = NQ, S = 2 * r + 1, K = S * S;
     for (int b = 0; b < B; ++b)
         for (int n = 0; n < N; ++n) {
             const float x = coords[((size_t)b * 2 + 0) * N + n];
@@ -246,4 +247,15 @@ void oracle_corr_bwd(const float *grad_c, const float *f1, const float *f2, int 
     free(a1);
     free(a2);
     free(dc);
+}
+
+/* Reference-shaped forms (every pixel of fmap1 is a query). */
+void oracle_lookup(const float *const *pyr, const float *coords, int B, int H, int W, int L,
+                   int r, float *out) {
+    oracle_lookup_rows(pyr, coords, B, H * W, H, W, L, r, out);
+}
+
+void oracle_lookup_bwd(const float *coords, const float *grad_out, int B, int H, int W, int L,
+                       int r, float *const *grad_pyr) {
+    oracle_lookup_bwd_rows(coords, grad_out, B, H * W, H, W, L, r, grad_pyr);
 }

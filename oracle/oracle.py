@@ -42,6 +42,8 @@ def _load():
         lib.oracle_corr_rows.argtypes = [vp, vp, i, i, i, i, i, vp]
         lib.oracle_avg_pool2x2.argtypes = [vp, l, i, i, vp]
         lib.oracle_lookup.argtypes = [vp, vp, i, i, i, i, i, vp]
+        lib.oracle_lookup_rows.argtypes = [vp, vp, i, i, i, i, i, i, vp]
+        lib.oracle_lookup_rows.restype = None
         lib.oracle_lookup_bwd.argtypes = [vp, vp, i, i, i, i, i, vp]
         lib.oracle_pool_bwd.argtypes = [vp, l, i, i, i]
         lib.oracle_corr_bwd.argtypes = [vp, vp, vp, i, i, i, vp, vp]
@@ -109,6 +111,20 @@ def lookup(pyr, coords, radius=4) -> np.ndarray:
     K = (2 * radius + 1) ** 2
     out = np.empty((B, L * K, H, W), np.float32)
     _load().oracle_lookup(_ptr_array(pyr), _p(coords), B, H, W, L, radius, _p(out))
+    return out
+
+
+def lookup_rows(pyr, coords_rows, H, W, radius=4) -> np.ndarray:
+    """Lookup for a query-row slab: coords [B, 2, rows, Wq] against a pyramid of the
+    (H, W) target map whose levels are [B*rows*Wq, 1, H>>l, W>>l]."""
+    coords_rows = _c(coords_rows)
+    B = coords_rows.shape[0]
+    NQ = int(np.prod(coords_rows.shape[2:]))
+    L = len(pyr)
+    pyr = [_c(p) for p in pyr]
+    K = (2 * radius + 1) ** 2
+    out = np.empty((B, L * K) + coords_rows.shape[2:], np.float32)
+    _load().oracle_lookup_rows(_ptr_array(pyr), _p(coords_rows), B, NQ, H, W, L, radius, _p(out))
     return out
 
 
