@@ -17,6 +17,7 @@
 // depend on the tile geometry, so all BuildCfg instantiations give bit-identical results.
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 
 #include "corr_common.h"
 
@@ -26,10 +27,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // Tile geometry.  WQ x WT waves; each wave QT query tiles of 32 x one 8x8 target sub-patch.
 // PF: read all of a chunk's MFMA operands from LDS before issuing its MFMAs.
-template <int WQ_, int WT_, int QT_, int BK_, int OCC_, bool PF_ = false>
+// SKIP: skip the MFMAs of a 4-row target tile that lies entirely below the map.
+template <int WQ_, int WT_, int QT_, int BK_, int OCC_, bool PF_ = false, bool SKIP_ = true>
 struct BuildCfg {
     static constexpr int WQ = WQ_, WT = WT_, QT = QT_, BK = BK_, OCC = OCC_;
-    static constexpr bool PF = PF_;
+    static constexpr bool PF = PF_, SKIP = SKIP_;
     static constexpr int NT = 64 * WQ * WT;  // threads
     static constexpr int BQ = 32 * QT * WQ;  // queries per tile
     static constexpr int PW = 8 * WT;        // target patch columns (8 rows)
@@ -42,7 +44,7 @@ struct BuildCfg {
 };
 
 // Default geometry (selected by tools/kbench_build.hip measurements).
-using BuildDefault = BuildCfg<2, 2, 2, 32, 2>;
+using BuildDefault = BuildCfg<2, 2, 2, 8, 4, true, false>;
 
 struct BuildParams {
     const float *f1;
@@ -71,13 +73,12 @@ __device__ __forceinline__ float pool4(float a, float b, float c, float d) {
     return t * 0.25f;
 }
 
-template <class Cfg, bool VEC>
-__global__ __launch_bounds__(Cfg::NT, Cfg::OCC) void corr_build_kernel(BuildParams p) {
+// One output tile.  smem: [stage][BK][BQ + BT].
+template <class Cfg, bool VEC, bool TT1>
+__device__ __forceinline__ void build_tile(const BuildParams &p, float *smem, const int tile) {
     constexpr int NT = Cfg::NT, BQ = Cfg::BQ, BT = Cfg::BT, BK = Cfg::BK, QT = Cfg::QT;
     constexpr int PW = Cfg::PW, QPT = Cfg::QPT, TPT = Cfg::TPT;
-    extern __shared__ __attribute__((aligned(16))) float smem[];  // [stage][BK][BQ + BT]
 
-    const int tile = xcd_swizzle(blockIdx.x, gridDim.x);
     const int px = tile % p.npx;
     const int py = (tile / p.npx) % p.npy;
     const int qb = (tile / (p.npx * p.npy)) % p.nq;
@@ -163,6 +164,8 @@ __global__ __launch_bounds__(Cfg::NT, Cfg::OCC) void corr_build_kernel(BuildPara
         if (c + 1 < nchunks) load_chunk((c + 1) * BK);
         const float *Qs = smem + (size_t)st * BK * (BQ + BT);
         const float *Ts = Qs + BK * BQ;
+        // TT1 = false: the lower 4-row target tile lies entirely below the map (H % 8 in
+        // 1..4) — its MFMAs would only produce discarded padding, so they are not issued.
         if constexpr (Cfg::PF) {
             float bq[BK / 2][QT], a0[BK / 2], a1[BK / 2];
 #pragma unroll
@@ -171,14 +174,15 @@ __global__ __launch_bounds__(Cfg::NT, Cfg::OCC) void corr_build_kernel(BuildPara
 #pragma unroll
                 for (int i = 0; i < QT; ++i) bq[s][i] = Qs[k * BQ + wq * (32 * QT) + i * 32 + l32];
                 a0[s] = Ts[k * BT + wt * 64 + l32];
-                a1[s] = Ts[k * BT + wt * 64 + 32 + l32];
+                if (TT1) a1[s] = Ts[k * BT + wt * 64 + 32 + l32];
             }
 #pragma unroll
             for (int s = 0; s < BK / 2; ++s)
 #pragma unroll
                 for (int i = 0; i < QT; ++i) {
                     acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], bq[s][i], acc[i][0], 0, 0, 0);
-                    acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], bq[s][i], acc[i][1], 0, 0, 0);
+                    if (TT1)
+                        acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], bq[s][i], acc[i][1], 0, 0, 0);
                 }
         } else {
 #pragma unroll
@@ -188,11 +192,11 @@ __global__ __launch_bounds__(Cfg::NT, Cfg::OCC) void corr_build_kernel(BuildPara
 #pragma unroll
                 for (int i = 0; i < QT; ++i) bq[i] = Qs[k * BQ + wq * (32 * QT) + i * 32 + l32];
                 const float a0 = Ts[k * BT + wt * 64 + l32];
-                const float a1 = Ts[k * BT + wt * 64 + 32 + l32];
+                const float a1 = TT1 ? Ts[k * BT + wt * 64 + 32 + l32] : 0.0f;
 #pragma unroll
                 for (int i = 0; i < QT; ++i) {
                     acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bq[i], acc[i][0], 0, 0, 0);
-                    acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bq[i], acc[i][1], 0, 0, 0);
+                    if (TT1) acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bq[i], acc[i][1], 0, 0, 0);
                 }
             }
         }
@@ -280,6 +284,19 @@ __global__ __launch_bounds__(Cfg::NT, Cfg::OCC) void corr_build_kernel(BuildPara
             if (Y < H3 && X < W3) p.lvl[3][qrow * (size_t)(H3 * W3) + Y * W3 + X] = l3;
         }
     }
+}
+
+template <class Cfg, bool VEC>
+__global__ __launch_bounds__(Cfg::NT, Cfg::OCC) void corr_build_kernel(BuildParams p) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tile = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int py = (tile / p.npx) % p.npy;
+    // one tile-uniform branch between two complete bodies (register pressure = the max of the
+    // two, not their union)
+    if (!Cfg::SKIP || py * 8 + 4 < p.H)
+        build_tile<Cfg, VEC, true>(p, smem, tile);
+    else
+        build_tile<Cfg, VEC, false>(p, smem, tile);
 }
 
 namespace {
