@@ -75,6 +75,23 @@ def lookup_bytes(B, H, W, L, r):
     return B * N * (L * (2 * r + 2) ** 2 * 4 + L * (2 * r + 1) ** 2 * 4 + 8)
 
 
+def traffic(workload, kernel):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/*_pmc.json,
+    written by tools/pmc_summary.py --json): FETCH_SIZE x 2 (gfx950 reports half the bytes of
+    16-B/lane streaming reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, in bytes.  The PMC
+    passes are separate rocprofv3 runs of this script; null when no profile exists."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_pmc.json")))
+    if not files:
+        return None
+    with open(files[-1]) as fh:
+        d = json.load(fh)
+    k = d.get("kernels", {}).get(kernel)
+    if not k or "FETCH_SIZE" not in k or "WRITE_SIZE" not in k:
+        return None
+    return int(round((2 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024))
+
+
 def cpu_baseline(workload, budget_s):
     """The reference op chain on torch CPU, all host cores, bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
@@ -168,46 +185,67 @@ def main():
         run_build()
         run_lookups()
         torch.cuda.synchronize()
+        def pair():
+            run_build()
+            run_lookups()
+
         if args.eager:
-            g_build = g_look = None
+            step = pair
         else:
-            g_build, g_look = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_build, stream=stream):
-                run_build()
-            with torch.cuda.graph(g_look, stream=stream):
-                run_lookups()
-        step_build = g_build.replay if g_build else run_build
-        step_look = g_look.replay if g_look else run_lookups
+            g_pair = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_pair, stream=stream):
+                pair()
+            step = g_pair.replay
 
         for _ in range(args.warmup):
-            step_build()
-            step_look()
+            step()
         torch.cuda.synchronize()
 
-        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for k in range(args.steps):
-            e0, e1, e2 = ev[k]
-            e0.record(stream)
-            step_build()
-            e1.record(stream)
-            step_look()
-            e2.record(stream)
+            ev[k][0].record(stream)
+            step()
+            ev[k][1].record(stream)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         if world > 1:
             dist.barrier()
+
+        # Per-kernel durations on the launch stream: REP back-to-back launches of each kernel
+        # in one graph, bracketed by HIP events (amortises the graph-launch gap, so the average
+        # is the kernel's own duration and agrees with rocprofv3's kernel trace).
+        REP = 10
+        g_b, g_l = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_b, stream=stream):
+            for _ in range(REP):
+                run_build()
+        with torch.cuda.graph(g_l, stream=stream):
+            for _ in range(REP):
+                run_lookups()
+        kb, kl = [], []
+        for _ in range(5):
+            for g, acc in ((g_b, kb), (g_l, kl)):
+                a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+                g.replay()
+                z.record(stream)
+                z.synchronize()
+                acc.append(a.elapsed_time(z))
+        kb.sort()
+        kl.sort()
 
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    build_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
-    look_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / (args.steps * iters)
+    step_gpu_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+    build_ms = kb[len(kb) // 2] / REP
+    look_ms = kl[len(kl) // 2] / (REP * iters)
 
     pairs = B * args.steps * world
     value = pairs / elapsed
@@ -238,13 +276,17 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "corr_build_kernel",
                          "achieved": round(ach_tf, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(ach_tf / PEAK_FP32_MFMA_TFLOPS, 4),
-                         "traffic": None, "avg_us": round(build_ms * 1e3, 2),
-                         "flops_per_launch": fl},
+                         "traffic": traffic(args.workload, "corr_build_kernel"),
+                         "avg_us": round(build_ms * 1e3, 2), "flops_per_launch": fl,
+                         "bytes_per_launch": build_bytes(B, D, H, W, L)},
             "roofline_lookup": {"bound": "hbm", "kernel": "lookup_kernel",
                                 "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                                "frac": round(look_gbs / PEAK_HBM_GBS, 4), "traffic": None,
-                                "avg_us": round(look_ms * 1e3, 3), "bytes_per_launch": lb,
-                                "note": "includes inter-kernel gap inside the graph"},
+                                "frac": round(look_gbs / PEAK_HBM_GBS, 4),
+                                "traffic": traffic(args.workload, "lookup_kernel"),
+                                "avg_us": round(look_ms * 1e3, 3), "bytes_per_launch": lb},
+            "kernel_timing": f"HIP events around {REP} back-to-back launches per graph on the "
+                             "launch stream, median of 5",
+            "step_gpu_us": round(step_gpu_ms * 1e3, 2),
             "hbm_gbs_algorithmic": round(hbm_gbs, 1),
         }
         if world == 1 and not args.no_cpu_baseline:

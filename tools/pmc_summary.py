@@ -1,39 +1,61 @@
 """Summarise rocprofv3 outputs of tools/profile.sh: per-kernel average duration and PMC
-counters (per dispatch), for the corr kernels.   python tools/pmc_summary.py gpurun_out/prof_<tag>"""
+counters (averaged per dispatch) for the corr kernels.
+
+    python tools/pmc_summary.py gpurun_out/prof_<tag>                 # text
+    python tools/pmc_summary.py gpurun_out/prof_<tag> --json out.json # + machine-readable
+"""
 import csv
 import glob
+import json
 import os
 import sys
 from collections import defaultdict
 
+KERNELS = ("corr_build_kernel", "lookup_bwd_kernel", "lookup_kernel", "gemm_kernel",
+           "splitk_reduce_kernel", "pool_bwd_kernel", "pool2x2_kernel")
+
 
 def short(name):
-    for k in ("corr_build_kernel", "lookup_bwd_kernel", "lookup_kernel", "gemm_kernel",
-              "splitk_reduce_kernel", "pool_bwd_kernel", "pool2x2_kernel"):
+    for k in KERNELS:
         if k in name:
-            return k + ("<" + name.split("<", 1)[1].split(">")[0] + ">" if "<" in name else "")
+            return k
     return None
 
 
-def main(d):
-    stats = glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True)
-    for f in stats:
-        print("== kernel stats", f)
+def collect(d):
+    out = {"kernels": defaultdict(dict)}
+    for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             s = short(row["Name"])
             if s:
-                print(f"  {s:40s} calls {row['Calls']:>6s} avg {float(row['AverageNs'])/1e3:9.2f} us"
-                      f"  min {float(row['MinNs'])/1e3:9.2f}  max {float(row['MaxNs'])/1e3:9.2f}")
+                out["kernels"][s].update(calls=int(row["Calls"]), avg_us=float(row["AverageNs"]) / 1e3,
+                                         min_us=float(row["MinNs"]) / 1e3, max_us=float(row["MaxNs"]) / 1e3)
     for f in sorted(glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), recursive=True)):
         acc = defaultdict(lambda: defaultdict(list))
         for row in csv.DictReader(open(f)):
             s = short(row.get("Kernel_Name", ""))
             if s:
                 acc[s][row["Counter_Name"]].append(float(row["Counter_Value"]))
-        print("== pmc", f)
         for k, cs in acc.items():
-            print("  ", k, "  ".join(f"{c}={sum(v)/len(v):.4g}" for c, v in sorted(cs.items())))
+            for c, v in cs.items():
+                out["kernels"][k][c] = sum(v) / len(v)
+    out["kernels"] = dict(out["kernels"])
+    return out
+
+
+def main(d, js=None):
+    res = collect(d)
+    for k, v in res["kernels"].items():
+        print(f"{k}:")
+        for c, x in sorted(v.items()):
+            print(f"    {c:28s} {x:.6g}")
+    if js:
+        res["source"] = d
+        res["note"] = ("FETCH_SIZE / WRITE_SIZE in kB per dispatch (rocprofv3, separate --pmc passes); "
+                       "gfx950 FETCH_SIZE counts half the bytes of 16-B/lane streaming reads")
+        with open(js, "w") as fh:
+            json.dump(res, fh, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[3] if len(sys.argv) > 3 and sys.argv[2] == "--json" else None)
