@@ -117,7 +117,7 @@ __device__ __forceinline__ void gather_window(float *win, const int *ax, const i
 // Forward gather: one wave per query at a time, lane -> fixed neighbourhood cells, so the
 // (row, col) of each lane's cells is computed once and every load's address is
 // anchor + constant (no per-element integer division).
-template <int S, int QB, int NT>
+template <int S, int QB, int NT, bool NOLOAD = false>
 __device__ __forceinline__ void gather_window_wave(float *win, const int *ax, const int *ay,
                                                    const float *P, size_t qbase, size_t mapsz,
                                                    int n0, int N, int Wl, int Hl, int tid) {
@@ -133,18 +133,31 @@ __device__ __forceinline__ void gather_window_wave(float *win, const int *ax, co
         ry[v] = e / WIN;
         rx[v] = e - ry[v] * WIN;
     }
+    // The query a wave handles at step k is wave-uniform.  All of the wave's anchors are read
+    // from LDS at once (lane k holds query k's) and moved to scalar registers with readlane, so
+    // no step waits on LDS; each load is then base(SGPR) + 32-bit offset.
+    static_assert(QPW <= 64, "one lane per query of the wave");
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    int myX = kFarAnchor, myY = kFarAnchor;
+    {
+        const int qq = wu + NW * lane;
+        if (lane < QPW && qq < QB && n0 + qq < N) {
+            myX = ax[qq];
+            myY = ay[qq];
+        }
+    }
     float vals[QPW][EPL];
 #pragma unroll
     for (int k = 0; k < QPW; ++k) {
-        const int qq = w + NW * k;
-        const bool qv = qq < QB && n0 + qq < N;
-        const int X0 = qv ? ax[qq] : kFarAnchor, Y0 = qv ? ay[qq] : kFarAnchor;
+        const int qq = wu + NW * k;
+        const int X0 = __builtin_amdgcn_readlane(myX, k);
+        const int Y0 = __builtin_amdgcn_readlane(myY, k);
         const float *Pq = P + (qbase + qq) * mapsz;
 #pragma unroll
         for (int v = 0; v < EPL; ++v) {
             const int X = X0 + rx[v], Y = Y0 + ry[v];
-            const bool ok = (lane + 64 * v < WS) && X >= 0 && X < Wl && Y >= 0 && Y < Hl;
-            vals[k][v] = ok ? Pq[(size_t)Y * Wl + X] : 0.0f;
+            const bool ok = (lane + 64 * v < WS) && (unsigned)X < (unsigned)Wl && (unsigned)Y < (unsigned)Hl;
+            vals[k][v] = (ok && !NOLOAD) ? Pq[(unsigned)(Y * Wl + X)] : 0.0f;
         }
     }
 #pragma unroll
@@ -164,11 +177,14 @@ struct LookupSmem {
     float ty[3][S][QB];
     float fx[2][QB];  // floor of x-tap 0 and S-1
     int ax[QB], ay[QB];
+    int flags;
 };
 
 constexpr int lookup_threads(int S, int QB) { return (QB * S + 63) / 64 * 64; }
 
-template <int S, int QB>
+// ABL: diagnostic ablations for tools/kbench_lookup.hip only (0 in the library): bit 0 = no
+// neighbourhood loads, bit 1 = no output stores, bit 2 = no coords load.
+template <int S, int QB, int ABL = 0>
 __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
     ConstLevelPtrs pyr, const float *__restrict__ coords, int B, int NQ, int H, int W, int L,
     float *__restrict__ out) {
@@ -196,27 +212,38 @@ __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
     const bool qok = act && n < N;
 
     // ---- 1. taps ----
-    const float cxv = qok ? coords[((size_t)b * 2 + 0) * N + n] : 0.0f;
-    const float cyv = qok ? coords[((size_t)b * 2 + 1) * N + n] : 0.0f;
+    if (tid == 0) sm.flags = 0;
+    const float cxv = (ABL & 4) ? (float)(n % W) : qok ? coords[((size_t)b * 2 + 0) * N + n] : 0.0f;
+    const float cyv = (ABL & 4) ? (float)(n / W) : qok ? coords[((size_t)b * 2 + 1) * N + n] : 0.0f;
     const Axis tx = tap_axis(cxv, inv_scale, i, R, Wl);
+    const Axis ty = tap_axis(cyv, inv_scale, i, R, Hl);
     if (act) {
-        const Axis a = tap_axis(cyv, inv_scale, i, R, Hl);
-        sm.ty[0][i][q] = a.f;
-        sm.ty[1][i][q] = a.lo;
-        sm.ty[2][i][q] = a.hi;
+        sm.ty[0][i][q] = ty.f;
+        sm.ty[1][i][q] = ty.lo;
+        sm.ty[2][i][q] = ty.hi;
         if (i == 0) {
             sm.ax[q] = anchor_of(tx.f);
-            sm.ay[q] = anchor_of(a.f);
+            sm.ay[q] = anchor_of(ty.f);
             sm.fx[0][q] = tx.f;
         }
         if (i == S - 1) sm.fx[1][q] = tx.f;
     }
     __syncthreads();
+    // Workgroup-uniform mode: bit 0 = some corner lies outside its neighbourhood (slow path),
+    // bit 1 = some query's taps are not regular (floor(tap t) != floor(tap 0) + t).
+    if (act) {
+        const int ax0 = sm.ax[q], ay0 = sm.ay[q];
+        const bool far = ax0 == kFarAnchor || ay0 == kFarAnchor;
+        const bool covers = window_covers<S>(sm.fx[0][q], sm.fx[1][q], sm.ty[0][0][q], sm.ty[0][S - 1][q]);
+        const bool reg = far || (tx.f == (float)(ax0 + i) && ty.f == (float)(ay0 + i));
+        const int f = (covers ? 0 : 1) | (reg ? 0 : 2);
+        if (f) atomicOr(&sm.flags, f);
+    }
 
     // ---- 2. neighbourhoods -> LDS ----
-    gather_window_wave<S, QB, NT>(sm.win, sm.ax, sm.ay, P, qbase, mapsz, n0, N, Wl, Hl, tid);
-    const int slow = __syncthreads_or(
-        act && !window_covers<S>(sm.fx[0][q], sm.fx[1][q], sm.ty[0][0][q], sm.ty[0][S - 1][q]));
+    gather_window_wave<S, QB, NT, (ABL & 1) != 0>(sm.win, sm.ax, sm.ay, P, qbase, mapsz, n0, N, Wl, Hl, tid);
+    __syncthreads();
+    const int mode = sm.flags;
     if (!act) return;
 
     // ---- 3. outputs (i, 0..S-1) of query q ----
@@ -224,7 +251,27 @@ __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
     const float *wq = &sm.win[q * WSTR];
     float *o = out + (((size_t)b * L + l) * K + (size_t)i * S) * N + n;
     const float x0 = tx.f, ex = tx.lo, wx = tx.hi;
-    if (!slow) {
+    if (mode == 0) {
+        // regular taps: tap (i, j) has corners at neighbourhood column i, i+1 and rows j, j+1,
+        // so the S+1 rows of the column pair are read once and shared by consecutive taps
+        // (far queries read an all-zero neighbourhood: their taps have no in-map corner).
+        const float *col = wq + i;
+        float c0[S + 1], c1[S + 1];
+#pragma unroll
+        for (int j = 0; j <= S; ++j) {
+            c0[j] = col[j * WIN];
+            c1[j] = col[j * WIN + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            const float ey = sm.ty[1][j][q], ny = sm.ty[2][j][q];
+            float acc = __fmul_rn(c0[j], __fmul_rn(ey, ex));
+            acc = __builtin_fmaf(c1[j], __fmul_rn(ey, wx), acc);
+            acc = __builtin_fmaf(c0[j + 1], __fmul_rn(ny, ex), acc);
+            acc = __builtin_fmaf(c1[j + 1], __fmul_rn(ny, wx), acc);
+            if (qok && (!(ABL & 2) || acc == 1234.5f)) o[(size_t)j * N] = acc;
+        }
+    } else if (!(mode & 1)) {
         // every corner is inside the neighbourhood (cells outside the map hold 0)
         const bool far = (ax == kFarAnchor) || (ay == kFarAnchor);
         const int cx = far ? 0 : (int)x0 - ax;
