@@ -100,7 +100,42 @@ def case_dsec_spot(name, seed):
     save(name, **out)
 
 
+def init_model(model):
+    sd = model.state_dict()
+    with torch.no_grad():
+        for name, t in sd.items():
+            v = prng.param_init(name, tuple(t.shape))
+            if v is not None:
+                t.copy_(torch.from_numpy(v))
+
+
+def case_e2e(name, seed, H=480, W=640, bins=15, iters=12):
+    """Full reference E-RAFT forward (model/eraft.py:89-146), random weights from
+    prng.param_init, cold call then warm-start call with the reference's own forward splat
+    (utils/image_utils.py:52-83, test.py:209).  flow_up is stored every 4th pixel."""
+    from model.eraft import ERAFT
+    from utils.image_utils import forward_interpolate_pytorch
+    model = ERAFT({"subtype": "warm_start"}, n_first_channels=bins).eval()
+    init_model(model)
+    im1 = torch.from_numpy(prng.voxel_grid(seed, (1, bins, H, W)))
+    im2 = torch.from_numpy(prng.voxel_grid(seed + 2, (1, bins, H, W)))
+    with torch.no_grad():
+        low, ups = model(im1, im2, iters=iters)
+        finit = forward_interpolate_pytorch(low)
+        model2 = ERAFT({"subtype": "warm_start"}, n_first_channels=bins).eval()
+        init_model(model2)
+        low_w, ups_w = model2(im1, im2, iters=iters, flow_init=finit)
+    keys = [f"{k}:{tuple(v.shape)}" for k, v in model.state_dict().items()]
+    save(name, meta=np.array([seed, H, W, bins, iters], np.int64), state_keys=np.array(keys),
+         low=low.numpy(), up_sub=ups[-1][..., ::4, ::4].numpy(),
+         up_mean_abs=np.array([ups[-1].abs().mean().item()]),
+         flow_init=finit.numpy(), low_warm=low_w.numpy(), up_warm_sub=ups_w[-1][..., ::4, ::4].numpy())
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "e2e":
+        case_e2e("g_e2e_dsec", 21)
+        sys.exit(0)
     case_build_lookup("g_b1_d32_16x16", 11, 1, 32, 16, 16, 4, 4, [0.0, 3.0, 20.0])
     case_build_lookup("g_b2_d256_17x23", 12, 2, 256, 17, 23, 4, 4, [8.0])
     case_build_lookup("g_b2_d64_16x20_L2r3", 13, 2, 64, 16, 20, 2, 3, [5.0])

@@ -43,6 +43,35 @@ def gauss(seed: int, shape, sigma: float = 1.0) -> np.ndarray:
     return (g * sigma).astype(np.float32).reshape(shape)
 
 
+def param_init(name: str, shape) -> np.ndarray | None:
+    """Deterministic random-init value of a model parameter / buffer, keyed by its
+    state_dict name (so two independent implementations with the reference's parameter
+    names get identical weights).  None for integer bookkeeping buffers."""
+    import zlib
+    if name.endswith("num_batches_tracked"):
+        return None
+    seed = zlib.crc32(name.encode()) & 0x3FFFFFFF
+    g = gauss(seed, shape).astype(np.float64)
+    if name.endswith("running_var"):
+        v = 1.0 + 0.1 * np.abs(g)
+    elif name.endswith("running_mean"):
+        v = 0.1 * g
+    elif name.endswith("weight") and len(shape) == 4:
+        fan_in = shape[1] * shape[2] * shape[3]
+        v = g * np.sqrt(2.0 / fan_in)
+    elif name.endswith("weight"):
+        v = 1.0 + 0.1 * g
+    else:  # bias
+        v = 0.05 * g
+    return v.astype(np.float32)
+
+
+def voxel_grid(seed: int, shape, density: float = 0.15) -> np.ndarray:
+    """Sparse event-voxel-like input: N(0,1) on ~`density` of the cells, 0 elsewhere."""
+    mask = uniform(seed, shape, stream=7) < density
+    return np.where(mask, gauss(seed + 1, shape), 0.0).astype(np.float32)
+
+
 def coords_grid(B: int, H: int, W: int) -> np.ndarray:
     """Pixel grid [B, 2, H, W], ch0 = x (column), ch1 = y (row) — model/utils.py:24-27."""
     y, x = np.meshgrid(np.arange(H, dtype=np.float32), np.arange(W, dtype=np.float32), indexing="ij")
