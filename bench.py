@@ -37,6 +37,15 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "CorrBlock build+lookup frame-pairs/sec & HBM GB/s at DSEC 480×640, 1–8 GPUs"
 PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec
+PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense BF16/F16 MFMA
+BUILD_ALGO = {0: "fp32", 1: "f16x3"}
+BUILD_KERNELS = {0: "corr_build_kernel", 1: "split_pack_kernel+corr_build_split_kernel"}
+BUILD_NOTE = {
+    0: "fp32 operands on v_mfma_f32_32x32x2_f32",
+    1: "fp32 product emulated on the f16 MFMA (per-pixel 2^e*(hi+lo) split, 3 MFMAs, fp32 "
+       "accumulate); achieved = algorithmic fp32 flops / (pack + MFMA kernel time) against the "
+       "fp32 MFMA peak, the executed f16 rate is in roofline_f16_pipe",
+}
 
 WORKLOADS = {
     # name: (B, D, H, W, levels, radius, iters)
@@ -90,6 +99,12 @@ def traffic(workload, kernel):
     if not k or "FETCH_SIZE" not in k or "WRITE_SIZE" not in k:
         return None
     return int(round((2 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024))
+
+
+def build_traffic(workload, algo):
+    ks = BUILD_KERNELS[algo].split("+")
+    t = [traffic(workload, k) for k in ks]
+    return None if any(x is None for x in t) else sum(t)
 
 
 def cpu_baseline(workload, budget_s):
@@ -170,8 +185,11 @@ def main():
     pyr = _alloc_pyramid(B, H, W, L, f1)
     outs = [torch.empty(B, L * K, H, W, device=dev) for _ in range(iters)]
 
+    algo = _lib.default_algo()
+    ws = _lib.build_workspace(f1, f2, algo)  # packed f16 operands (F16X3), reused every step
+
     def run_build():
-        _lib.build(f1, f2, pyr)
+        _lib.build(f1, f2, pyr, algo, ws)
 
     def run_lookups():
         for c, o in zip(coords, outs):
@@ -273,17 +291,24 @@ def main():
                                    f"fmaps [{B},{D},{H},{W}], {L} levels, radius {r}",
                        "global_batch": B * world, "launch": "eager" if args.eager else "hipgraph",
                        "parallelism": f"replicas x{world} (independent frame pairs per GPU)"},
-            "roofline": {"bound": "mfma", "kernel": "corr_build_kernel",
+            "build_algo": BUILD_ALGO[algo],
+            "roofline": {"bound": "mfma", "kernel": BUILD_KERNELS[algo],
                          "achieved": round(ach_tf, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(ach_tf / PEAK_FP32_MFMA_TFLOPS, 4),
-                         "traffic": traffic(args.workload, "corr_build_kernel"),
+                         "traffic": build_traffic(args.workload, algo),
                          "avg_us": round(build_ms * 1e3, 2), "flops_per_launch": fl,
-                         "bytes_per_launch": build_bytes(B, D, H, W, L)},
+                         "bytes_per_launch": build_bytes(B, D, H, W, L),
+                         "note": BUILD_NOTE[algo]},
             "roofline_lookup": {"bound": "hbm", "kernel": "lookup_kernel",
                                 "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                 "frac": round(look_gbs / PEAK_HBM_GBS, 4),
                                 "traffic": traffic(args.workload, "lookup_kernel"),
                                 "avg_us": round(look_ms * 1e3, 3), "bytes_per_launch": lb},
+            **({"roofline_f16_pipe": {
+                "bound": "mfma", "executed_tflops": round(3 * ach_tf, 1), "peak": PEAK_F16_MFMA_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(3 * ach_tf / PEAK_F16_MFMA_TFLOPS, 4),
+                "note": "3 f16 MFMA products per fp32 product (hi*hi + hi*lo + lo*hi)"}}
+               if algo == _lib.BUILD_F16X3 else {}),
             "kernel_timing": f"HIP events around {REP} back-to-back launches per graph on the "
                              "launch stream, median of 5",
             "step_gpu_us": round(step_gpu_ms * 1e3, 2),

@@ -75,7 +75,7 @@ using namespace corr;
 
 extern "C" {
 
-int corr_version(void) { return 100; }
+int corr_version(void) { return 101; }
 
 const char *corr_last_error(void) { return g_err; }
 
@@ -90,6 +90,36 @@ int corr_build_rows(const float *fmap1_rows, int NQ, const float *fmap2, int B, 
     LevelPtrs lp{};
     if ((rc = check_levels(fn, pyr, levels, "pyr", lp.p))) return rc;
     return hip_status(launch_build(fmap1_rows, NQ, fmap2, B, D, H, W, levels, lp, (hipStream_t)stream), fn);
+}
+
+size_t corr_build_workspace(int algo, int B, int D, int NQ, int H, int W) {
+    if (B < 1 || D < 1 || NQ < 1 || H < 1 || W < 1) return 0;
+    if (algo == CORR_BUILD_F16X3)
+        return build_split_supported(D) ? build_split_workspace(B, D, NQ, H, W) : (size_t)-1;
+    return 0;
+}
+
+int corr_build_ex(int algo, const float *fmap1_rows, int NQ, const float *fmap2, int B, int D,
+                  int H, int W, int levels, float *const *pyr, void *workspace,
+                  size_t workspace_bytes, void *stream) {
+    static const char *fn = "corr_build_ex";
+    if (algo == CORR_BUILD_FP32) return corr_build_rows(fmap1_rows, NQ, fmap2, B, D, H, W, levels, pyr, stream);
+    g_err[0] = 0;
+    if (algo != CORR_BUILD_F16X3) return fail(CORR_EINVAL, "%s: unknown algorithm %d", fn, algo);
+    int rc = check_dims(fn, B, NQ, H, W, levels);
+    if (rc) return rc;
+    if (D < 1) return fail(CORR_EINVAL, "%s: D must be >= 1 (got %d)", fn, D);
+    if (!build_split_supported(D))
+        return fail(CORR_EUNSUPPORTED, "%s: D = %d is too large for CORR_BUILD_F16X3", fn, D);
+    if ((rc = check_ptr(fn, fmap1_rows, "fmap1")) || (rc = check_ptr(fn, fmap2, "fmap2"))) return rc;
+    if ((uintptr_t)workspace % 256) return fail(CORR_EINVAL, "%s: workspace is not 256-byte aligned", fn);
+    const size_t need = build_split_workspace(B, D, NQ, H, W);
+    if (workspace_bytes < need || !workspace)
+        return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
+    LevelPtrs lp{};
+    if ((rc = check_levels(fn, pyr, levels, "pyr", lp.p))) return rc;
+    return hip_status(launch_build_split(fmap1_rows, NQ, fmap2, B, D, H, W, levels, lp, workspace, (hipStream_t)stream),
+                      fn);
 }
 
 int corr_build(const float *fmap1, const float *fmap2, int B, int D, int H, int W, int levels,

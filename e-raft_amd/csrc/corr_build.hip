@@ -19,11 +19,10 @@
 #include <cmath>
 #include <type_traits>
 
-#include "corr_common.h"
+#include "corr_build_common.h"
 
 namespace corr {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // Tile geometry.  WQ x WT waves; each wave QT query tiles of 32 x one 8x8 target sub-patch.
 // PF: read all of a chunk's MFMA operands from LDS before issuing its MFMAs.
@@ -58,19 +57,93 @@ struct BuildParams {
     int exact_mul;      // sqrt(D) is a power of two: x * (1/s) == x / s bit-for-bit
 };
 
-__device__ __forceinline__ int xcd_swizzle(int bid, int nwg) {
-    // Blocks are dealt round-robin to the 8 XCDs; give each XCD a contiguous range of
-    // tiles (which share the query slab) — bijective for any nwg (speed only).
-    const int xcd = bid & 7, loc = bid >> 3, q = nwg >> 3, r = nwg & 7;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
-}
 
-__device__ __forceinline__ float pool4(float a, float b, float c, float d) {
-    // avg_pool2d(2,2) on CPU ATen: ((a + b) + c) + d, then * 1/4 (bit-identical).
-    float t = a + b;
-    t = t + c;
-    t = t + d;
-    return t * 0.25f;
+
+// Epilogue: scale, level 0, in-register pyramid.
+// acc[qt][tt][r]: query qw + qt*32 + l32, target (y, x) of the wave's 8x8 sub-patch at
+// (py*8, xw) with y = tt*4 + (r >> 2), x = 4h + (r & 3)   (32x32 C/D map).
+template <int QT, bool VEC>
+__device__ __forceinline__ void store_pyramid(const BuildParams &p, f32x16 (&acc)[QT][2], const int b,
+                                              const int qw, const int xw, const int py, const int h,
+                                              const int l32) {
+    const int N = p.N, NQ = p.NQ, W = p.W, H = p.H;
+    const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
+    const int X0 = xw + 4 * h, Y0 = py * 8;
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const int q = qw + qt * 32 + l32;
+        const bool qok = q < NQ;
+        const size_t qrow = (size_t)b * NQ + q;
+        float v[8][4];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float x = acc[qt][tt][r];
+                v[tt * 4 + (r >> 2)][r & 3] = p.exact_mul ? x * p.inv_s : x / p.s;
+            }
+        // level 0
+        if (qok) {
+            float *o = p.lvl[0] + qrow * N;
+#pragma unroll
+            for (int y = 0; y < 8; ++y) {
+                const int Y = Y0 + y;
+                if (Y < H) {
+                    if (VEC) {
+                        if (X0 < W)
+                            *reinterpret_cast<float4 *>(o + (size_t)Y * W + X0) =
+                                make_float4(v[y][0], v[y][1], v[y][2], v[y][3]);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (X0 + e < W) o[(size_t)Y * W + X0 + e] = v[y][e];
+                    }
+                }
+            }
+        }
+        if (p.nlev < 2) continue;
+        // level 1: 4 rows x 2 cols per lane
+        float l1[4][2];
+#pragma unroll
+        for (int y = 0; y < 4; ++y)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+                l1[y][x] = pool4(v[2 * y][2 * x], v[2 * y][2 * x + 1], v[2 * y + 1][2 * x],
+                                 v[2 * y + 1][2 * x + 1]);
+        if (qok) {
+            float *o = p.lvl[1] + qrow * (size_t)(H1 * W1);
+#pragma unroll
+            for (int y = 0; y < 4; ++y)
+#pragma unroll
+                for (int x = 0; x < 2; ++x) {
+                    const int Y = py * 4 + y, X = (X0 >> 1) + x;
+                    if (Y < H1 && X < W1) o[Y * W1 + X] = l1[y][x];
+                }
+        }
+        if (p.nlev < 3) continue;
+        // level 2: 2 rows x 1 col per lane
+        float l2[2];
+#pragma unroll
+        for (int y = 0; y < 2; ++y) l2[y] = pool4(l1[2 * y][0], l1[2 * y][1], l1[2 * y + 1][0], l1[2 * y + 1][1]);
+        if (qok) {
+            float *o = p.lvl[2] + qrow * (size_t)(H2 * W2);
+            const int X = X0 >> 2;
+#pragma unroll
+            for (int y = 0; y < 2; ++y) {
+                const int Y = py * 2 + y;
+                if (Y < H2 && X < W2) o[Y * W2 + X] = l2[y];
+            }
+        }
+        if (p.nlev < 4) continue;
+        // level 3: the 2x2 level-2 block is split across lane halves h = 0 (x = 0), 1 (x = 1)
+        const float o0 = __shfl_xor(l2[0], 32);
+        const float o1 = __shfl_xor(l2[1], 32);
+        if (h == 0 && qok) {
+            const float l3 = pool4(l2[0], o0, l2[1], o1);
+            const int Y = py, X = X0 >> 3;
+            if (Y < H3 && X < W3) p.lvl[3][qrow * (size_t)(H3 * W3) + Y * W3 + X] = l3;
+        }
+    }
 }
 
 // One output tile.  smem: [stage][BK][BQ + BT].
@@ -204,86 +277,7 @@ __device__ __forceinline__ void build_tile(const BuildParams &p, float *smem, co
         __syncthreads();
     }
 
-    // ---- epilogue: scale, level 0, in-register pyramid ----
-    // acc[qt][tt][r]: query q0 + wq*32*QT + qt*32 + l32, target (y, x) of the wave's 8x8
-    // sub-patch with y = tt*4 + (r >> 2), x = 4h + (r & 3)   (32x32 C/D map).
-    const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
-    const int X0 = px * PW + wt * 8 + 4 * h, Y0 = py * 8;
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt) {
-        const int q = q0 + wq * 32 * QT + qt * 32 + l32;
-        const bool qok = q < NQ;
-        const size_t qrow = (size_t)b * NQ + q;
-        float v[8][4];
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float x = acc[qt][tt][r];
-                v[tt * 4 + (r >> 2)][r & 3] = p.exact_mul ? x * p.inv_s : x / p.s;
-            }
-        // level 0
-        if (qok) {
-            float *o = p.lvl[0] + qrow * N;
-#pragma unroll
-            for (int y = 0; y < 8; ++y) {
-                const int Y = Y0 + y;
-                if (Y < H) {
-                    if (VEC) {
-                        if (X0 < W)
-                            *reinterpret_cast<float4 *>(o + (size_t)Y * W + X0) =
-                                make_float4(v[y][0], v[y][1], v[y][2], v[y][3]);
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if (X0 + e < W) o[(size_t)Y * W + X0 + e] = v[y][e];
-                    }
-                }
-            }
-        }
-        if (p.nlev < 2) continue;
-        // level 1: 4 rows x 2 cols per lane
-        float l1[4][2];
-#pragma unroll
-        for (int y = 0; y < 4; ++y)
-#pragma unroll
-            for (int x = 0; x < 2; ++x)
-                l1[y][x] = pool4(v[2 * y][2 * x], v[2 * y][2 * x + 1], v[2 * y + 1][2 * x],
-                                 v[2 * y + 1][2 * x + 1]);
-        if (qok) {
-            float *o = p.lvl[1] + qrow * (size_t)(H1 * W1);
-#pragma unroll
-            for (int y = 0; y < 4; ++y)
-#pragma unroll
-                for (int x = 0; x < 2; ++x) {
-                    const int Y = py * 4 + y, X = (X0 >> 1) + x;
-                    if (Y < H1 && X < W1) o[Y * W1 + X] = l1[y][x];
-                }
-        }
-        if (p.nlev < 3) continue;
-        // level 2: 2 rows x 1 col per lane
-        float l2[2];
-#pragma unroll
-        for (int y = 0; y < 2; ++y) l2[y] = pool4(l1[2 * y][0], l1[2 * y][1], l1[2 * y + 1][0], l1[2 * y + 1][1]);
-        if (qok) {
-            float *o = p.lvl[2] + qrow * (size_t)(H2 * W2);
-            const int X = X0 >> 2;
-#pragma unroll
-            for (int y = 0; y < 2; ++y) {
-                const int Y = py * 2 + y;
-                if (Y < H2 && X < W2) o[Y * W2 + X] = l2[y];
-            }
-        }
-        if (p.nlev < 4) continue;
-        // level 3: the 2x2 level-2 block is split across lane halves h = 0 (x = 0), 1 (x = 1)
-        const float o0 = __shfl_xor(l2[0], 32);
-        const float o1 = __shfl_xor(l2[1], 32);
-        if (h == 0 && qok) {
-            const float l3 = pool4(l2[0], o0, l2[1], o1);
-            const int Y = py, X = X0 >> 3;
-            if (Y < H3 && X < W3) p.lvl[3][qrow * (size_t)(H3 * W3) + Y * W3 + X] = l3;
-        }
-    }
+    store_pyramid<QT, VEC>(p, acc, b, q0 + wq * 32 * QT, px * PW + wt * 8, py, h, l32);
 }
 
 template <class Cfg, bool VEC>
@@ -318,10 +312,6 @@ __global__ __launch_bounds__(256) void pool2x2_kernel(const float *__restrict__ 
     }
 }
 
-bool is_pow2(float s) {
-    int e;
-    return std::frexp(s, &e) == 0.5f;
-}
 
 }  // namespace
 

@@ -37,6 +37,11 @@ hipError_t launch_lookup_bwd(const float *coords, const float *grad_out, int B, 
                              int W, int levels, int radius, const LevelPtrs &gpyr, hipStream_t s);
 hipError_t launch_pool_bwd(const LevelPtrs &gpyr, long BN, int H, int W, int levels,
                            hipStream_t s);
+// The f16-split build (corr_build_split.hip): pack kernel + f16 MFMA kernel, operands in `ws`.
+size_t build_split_workspace(int B, int D, int NQ, int H, int W);
+bool build_split_supported(int D);
+hipError_t launch_build_split(const float *f1, int NQ, const float *f2, int B, int D, int H, int W,
+                              int levels, const LevelPtrs &pyr, void *ws, hipStream_t s);
 size_t build_bwd_workspace(int B, int D, int NQ, int H, int W);
 hipError_t launch_build_bwd(const float *grad_c, const float *f1, int NQ, const float *f2, int B,
                             int D, int H, int W, float *df1, float *df2, float *ws, hipStream_t s);

@@ -24,7 +24,22 @@ MAX_RADIUS = 7
 EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr_lookup_bwd",
            "corr_pool_bwd", "corr_build_bwd_workspace", "corr_build_bwd", "corr_build_rows",
            "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows_workspace",
-           "corr_build_bwd_rows")
+           "corr_build_bwd_rows", "corr_build_workspace", "corr_build_ex")
+
+# Build algorithms (include/corr_mi355x.h).  F16X3 is the default: fp32 features split into
+# f16 hi/lo pairs, three f16 MFMAs per product, fp32 accumulate (~1e-6 of max|C| from the
+# exact-fp32 MFMA build; both are inside the north_star's 1e-4).  ERAFT_AMD_BUILD=fp32
+# selects the fp32-operand MFMA build instead.
+BUILD_FP32 = 0
+BUILD_F16X3 = 1
+_ALGOS = {"fp32": BUILD_FP32, "f16x3": BUILD_F16X3}
+
+
+def default_algo() -> int:
+    name = os.environ.get("ERAFT_AMD_BUILD", "f16x3").lower()
+    if name not in _ALGOS:
+        raise ValueError(f"ERAFT_AMD_BUILD must be one of {sorted(_ALGOS)} (got {name!r})")
+    return _ALGOS[name]
 
 _lib = None
 
@@ -64,8 +79,12 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.corr_build_bwd_rows_workspace.argtypes = [i, i, i, i, i]
     lib.corr_build_bwd_rows_workspace.restype = sz
     lib.corr_build_bwd_rows.argtypes = [vp, vp, i, vp, i, i, i, i, vp, vp, vp, sz, vp]
+    lib.corr_build_workspace.argtypes = [i, i, i, i, i, i]
+    lib.corr_build_workspace.restype = sz
+    lib.corr_build_ex.argtypes = [i, vp, i, vp, i, i, i, i, i, vp, vp, sz, vp]
     for f in ("corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd",
-              "corr_build_rows", "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows"):
+              "corr_build_rows", "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows",
+              "corr_build_ex"):
         getattr(lib, f).restype = i
     if path is None:
         _lib = lib
@@ -108,13 +127,32 @@ def _nq(t):
     return n
 
 
-def build(fmap1, fmap2, levels):
-    """corr_build_rows into caller-allocated levels [B*NQ, 1, H>>l, W>>l].  fmap1 may be a row
-    slab [B, D, rows, W] of the query map; fmap2 is the full target map [B, D, H, W]."""
+def build_workspace(fmap1, fmap2, algo=None):
+    """A device workspace for corr_build_ex (None when the algorithm needs none)."""
+    algo = default_algo() if algo is None else algo
+    B, D, H, W = fmap2.shape
+    n = load().corr_build_workspace(algo, B, D, _nq(fmap1), H, W)
+    if n == ctypes.c_size_t(-1).value:
+        raise CorrError(CORR_EUNSUPPORTED, f"build algorithm {algo} does not support D = {D}")
+    if n == 0:
+        return None
+    return torch.empty(n, dtype=torch.uint8, device=fmap1.device)
+
+
+def build(fmap1, fmap2, levels, algo=None, workspace=None):
+    """corr_build_ex into caller-allocated levels [B*NQ, 1, H>>l, W>>l].  fmap1 may be a row
+    slab [B, D, rows, W] of the query map; fmap2 is the full target map [B, D, H, W].
+    algo: BUILD_F16X3 (default, see default_algo) or BUILD_FP32."""
+    algo = default_algo() if algo is None else algo
     B, D, H, W = fmap2.shape
     a, b, pp = _dev(fmap1, "fmap1"), _dev(fmap2, "fmap2"), _ptrs(levels, "pyr")
+    if workspace is None:
+        workspace = build_workspace(fmap1, fmap2, algo)
+    wp = 0 if workspace is None else workspace.data_ptr()
+    wn = 0 if workspace is None else workspace.numel() * workspace.element_size()
     with torch.cuda.device(fmap1.device):
-        _check(load().corr_build_rows(a, _nq(fmap1), b, B, D, H, W, len(levels), pp, _stream(fmap1)))
+        _check(load().corr_build_ex(algo, a, _nq(fmap1), b, B, D, H, W, len(levels), pp, wp, wn,
+                                    _stream(fmap1)))
 
 
 def lookup(levels, coords, radius, out, H=None, W=None):

@@ -49,10 +49,38 @@ const char *corr_last_error(void);
  *   pyr[0][b*N + n][y][x] = sum_d fmap1[b][d][n] * fmap2[b][d][y*W + x] / sqrt(float(D))
  *   pyr[l][q][y][x]       = avg_pool2d(pyr[l-1], 2, stride 2)[q][y][x]   (floor)
  * `pyr` is a HOST array of `levels` device pointers.  levels == 1 gives CorrBlock.corr's
- * [B,H,W,1,H,W] volume.  fp32 in / fp32 MFMA accumulate / fp32 out.
+ * [B,H,W,1,H,W] volume.  fp32 in / fp32 MFMA accumulate / fp32 out (CORR_BUILD_FP32;
+ * corr_build_ex selects the faster CORR_BUILD_F16X3).
  */
 int corr_build(const float *fmap1, const float *fmap2, int B, int D, int H, int W, int levels,
                float *const *pyr, void *stream);
+
+/*
+ * Build algorithms for corr_build_ex (same outputs, same pyramid arithmetic; they differ only
+ * in how the fp32 dot products are formed — both accumulate in fp32):
+ *   CORR_BUILD_FP32   fp32 operands on v_mfma_f32_32x32x2_f32 (the corr_build path).
+ *   CORR_BUILD_F16X3  each fp32 feature x of pixel n is split as 2^e_n * (hi + lo), f16 hi/lo,
+ *                     e_n putting the pixel's largest |x| in [2^14, 2^15); three f16 MFMAs
+ *                     (hi*hi + hi*lo + lo*hi) per product into one fp32 accumulator.  Each
+ *                     feature is carried to 2^-22 relative (fp32: 2^-24), and each product to
+ *                     ~2^-21; features below 2^-38 of their pixel's largest flush to zero.
+ *                     Needs a workspace for the packed operands.  ~1.5-1.7x faster on gfx950.
+ */
+#define CORR_BUILD_FP32 0
+#define CORR_BUILD_F16X3 1
+
+/* Bytes of device workspace corr_build_ex(algo, ...) needs (0 for CORR_BUILD_FP32;
+ * (size_t)-1 if the algorithm does not support D). */
+size_t corr_build_workspace(int algo, int B, int D, int NQ, int H, int W);
+
+/*
+ * corr_build_rows with an explicit algorithm and caller-allocated workspace (>= the size
+ * corr_build_workspace returns; it may be reused across calls on the same stream).
+ * CORR_EUNSUPPORTED if `algo` cannot handle D.
+ */
+int corr_build_ex(int algo, const float *fmap1_rows, int NQ, const float *fmap2, int B, int D,
+                  int H, int W, int levels, float *const *pyr, void *workspace,
+                  size_t workspace_bytes, void *stream);
 
 /*
  * Window lookup.  Replaces CorrBlock.__call__ (model/corr.py:29-50) and bilinear_sampler

@@ -35,7 +35,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 
 def test_version_and_workspace(lib):
-    assert lib.corr_version() == 100
+    assert lib.corr_version() == 101
     # DSEC: 256 x 4800 slabs; at least one slab, deterministic plan
     ws = lib.corr_build_bwd_workspace(1, 256, 60, 80)
     assert ws >= 256 * 4800 * 4 and ws % (256 * 4800 * 4) == 0
@@ -74,3 +74,31 @@ def test_python_front_end_refuses_cpu_tensors():
     f = torch.zeros(1, 8, 16, 16)
     with pytest.raises(RuntimeError, match="MI355X"):
         CorrBlock(f, f)
+
+
+def test_build_ex_workspace_and_validation(lib):
+    # F16X3 workspace: hi/lo f16 operands (4 B per padded channel per pixel) + int32 exponents
+    n = lib.corr_build_workspace(1, 1, 256, 4800, 60, 80)
+    assert n >= 2 * 4800 * 256 * 4 + 2 * 4800 * 4
+    assert lib.corr_build_workspace(0, 1, 256, 4800, 60, 80) == 0  # fp32 needs none
+    assert lib.corr_build_workspace(1, 1, 10 ** 6, 4800, 60, 80) == ctypes.c_size_t(-1).value
+    pyr = (ctypes.c_void_p * 4)(256, 256, 256, 256)
+    rc = lib.corr_build_ex(1, 256, 4800, 256, 1, 256, 60, 80, 4, pyr, 256, 16, None)
+    assert rc == -1 and "workspace" in lib.corr_last_error().decode()
+    rc = lib.corr_build_ex(1, 256, 4800, 256, 1, 10 ** 6, 60, 80, 4, pyr, 256, 1 << 40, None)
+    assert rc == -2 and "too large" in lib.corr_last_error().decode()
+    rc = lib.corr_build_ex(7, 256, 4800, 256, 1, 256, 60, 80, 4, pyr, 256, 1 << 40, None)
+    assert rc == -1 and "unknown algorithm" in lib.corr_last_error().decode()
+    rc = lib.corr_build_ex(1, 256, 4800, 256, 1, 256, 60, 80, 4, pyr, 260, 1 << 40, None)
+    assert rc == -1 and "256-byte aligned" in lib.corr_last_error().decode()
+
+
+def test_build_algo_env(monkeypatch):
+    from eraft_amd import _lib
+    monkeypatch.delenv("ERAFT_AMD_BUILD", raising=False)
+    assert _lib.default_algo() == _lib.BUILD_F16X3
+    monkeypatch.setenv("ERAFT_AMD_BUILD", "fp32")
+    assert _lib.default_algo() == _lib.BUILD_FP32
+    monkeypatch.setenv("ERAFT_AMD_BUILD", "bf16")
+    with pytest.raises(ValueError):
+        _lib.default_algo()

@@ -37,8 +37,13 @@ def _fmaps(meta, dev=DEV):
     return f1, f2, torch.from_numpy(f1).to(dev), torch.from_numpy(f2).to(dev)
 
 
+ALGOS = ["f16x3", "fp32"]
+
+
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("name", BUILD_CASES)
-def test_build_matches_reference(name):
+def test_build_matches_reference(name, algo, monkeypatch):
+    monkeypatch.setenv("ERAFT_AMD_BUILD", algo)
     g = load(name)
     L, r = int(g["meta"][5]), int(g["meta"][6])
     _, _, t1, t2 = _fmaps(g["meta"])
@@ -124,7 +129,9 @@ def test_dsec_shape_against_reference_slices():
     (3, 7, 9, 13, 2, 1),
     (1, 33, 8, 8, 4, 4),        # smallest legal 4-level map (level 3 is 1x1 -> NaN lookups)
 ])
-def test_gpu_pyramid_and_lookup_vs_oracle(B, D, H, W, L, r):
+@pytest.mark.parametrize("algo", ALGOS)
+def test_gpu_pyramid_and_lookup_vs_oracle(B, D, H, W, L, r, algo, monkeypatch):
+    monkeypatch.setenv("ERAFT_AMD_BUILD", algo)
     f1 = prng.gauss(B * 1000 + D, (B, D, H, W))
     f2 = prng.gauss(B * 1000 + D + 1, (B, D, H, W))
     cb = _cb()(torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV), num_levels=L, radius=r)
@@ -143,6 +150,48 @@ def test_gpu_pyramid_and_lookup_vs_oracle(B, D, H, W, L, r):
         assert bit_equal(out, oracle.lookup(gpu, c, r))
     c = prng.special_coords(B, H, W)
     assert bit_equal(cb(torch.from_numpy(c).to(DEV)).cpu().numpy(), oracle.lookup(gpu, c, r))
+
+
+@pytest.mark.parametrize("case", ["channel_scales", "pixel_scales", "zeros", "tiny", "huge"])
+def test_build_f16x3_dynamic_range(case):
+    """The f16 split keeps fp32 accuracy over wide feature ranges: per-channel scales over
+    6 decades with the two maps' channel scales anti-correlated (the small features of one map
+    meet the large of the other), per-pixel scales over 20 decades, all-zero pixels, tiny and
+    near-overflow magnitudes.  (The split's floor: features below 2^-38 of their pixel's
+    largest flush to zero — 11+ decades, include/corr_mi355x.h.)  Bar: the north_star's 1e-4 (norm-relative per query row, against
+    the fp64 oracle), and the fp32-operand MFMA build on the same inputs."""
+    from eraft_amd import _lib
+    B, D, H, W = 1, 96, 12, 16
+    f1 = prng.gauss(11, (B, D, H, W)).astype(np.float64)
+    f2 = prng.gauss(12, (B, D, H, W)).astype(np.float64)
+    if case == "channel_scales":
+        s = 10.0 ** np.linspace(-3, 3, D)[None, :, None, None]
+        f1, f2 = f1 * s, f2 * s[:, ::-1]
+    elif case == "pixel_scales":
+        s = 10.0 ** np.linspace(-10, 10, H * W).reshape(1, 1, H, W)
+        f1, f2 = f1 * s, f2 * s[..., ::-1, ::-1]
+    elif case == "zeros":
+        f1[:, :, ::3] = 0.0
+        f2[:, :, :, ::5] = 0.0
+    elif case == "tiny":
+        f1, f2 = f1 * 1e-15, f2 * 1e-16
+    elif case == "huge":
+        f1, f2 = f1 * 1e17, f2 * 1e17
+    f1, f2 = f1.astype(np.float32), f2.astype(np.float32)
+    t1, t2 = torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV)
+    ref = oracle.corr_rows(f1, f2).reshape(B * H * W, H * W)
+    outs = {}
+    for algo in (_lib.BUILD_F16X3, _lib.BUILD_FP32):
+        lvl = torch.empty(B * H * W, 1, H, W, device=DEV)
+        _lib.build(t1, t2, [lvl], algo)
+        outs[algo] = lvl.cpu().numpy().reshape(B * H * W, H * W)
+    for algo, o in outs.items():
+        assert np.isfinite(o).all() == np.isfinite(ref).all()
+        scale = np.abs(ref).max(axis=1)
+        err = np.abs(o - ref).max(axis=1)
+        ok = scale > 0
+        assert (err[ok] / scale[ok]).max() < REL_TOL, (algo, (err[ok] / scale[ok]).max())
+        assert (err[~ok] == 0).all()
 
 
 def test_lookup_nan_and_inf_coords():

@@ -107,9 +107,11 @@ def test_row_partition_covers_rows():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("algo", ["f16x3", "fp32"])
 @pytest.mark.parametrize("G", [1, 2, 3, 8])
-def test_row_slab_kernels_match_full_on_gpu(G):
-    """G logical shards on one device through corr_build_rows / corr_lookup_rows."""
+def test_row_slab_kernels_match_full_on_gpu(G, algo, monkeypatch):
+    """G logical shards on one device through corr_build_ex / corr_lookup_rows."""
+    monkeypatch.setenv("ERAFT_AMD_BUILD", algo)
     from eraft_amd import CorrBlock
     from eraft_amd.sharded import HipRows, row_partition
     B, D, H, W, L, r = 2, 64, 20, 24, 4, 4
