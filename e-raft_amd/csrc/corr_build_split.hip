@@ -116,6 +116,78 @@ __global__ __launch_bounds__(256) void split_pack_kernel(PackArgs a) {
     }
 }
 
+// Register-resident pack (the default for D <= 512): 16 pixels per workgroup of 4 waves, lane
+// = 4 * pixel + unit, so every store instruction of a wave writes 16 consecutive pixels' four
+// 16-B units — one contiguous 1 KiB run of a chunk plane.  Wave w holds the chunks
+// kc = w, w + 4, ... : the lane loads the 8 features of its unit's k-octet (the hi and lo lanes
+// of an octet load the same addresses; the coalescer merges them), all loads issued before the
+// first use.  The per-pixel max is reduced over the quad with a DPP swap and over the 4 waves
+// through LDS.  Same arithmetic as split_pack_kernel, element for element (bit-identical packs).
+constexpr int kPackTP = 16, kPackW = 4;
+
+template <int CPT>
+__global__ __launch_bounds__(64 * kPackW) void split_pack_reg_kernel(PackArgs a) {
+    __shared__ float red[kPackW][kPackTP];
+    const int z = blockIdx.z, b = blockIdx.y, tid = threadIdx.x;
+    const int NP = a.np[z], D = a.D, nkc = a.KP / kSplitBK;
+    const int n0 = blockIdx.x * kPackTP;
+    if (n0 >= NP) return;  // the grid covers the larger of the two tensors (uniform exit)
+    const int lane = tid & 63, w = tid >> 6;
+    const int p = lane >> 2, u = lane & 3;  // u: (k-octet u >> 1, lo = u & 1)
+    const int n = min(n0 + p, NP - 1);      // clamped: unconditional loads
+    const float *src = a.f[z] + (size_t)b * D * NP + n;
+    float v[CPT][8];
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+        const int kc = w + kPackW * c;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int d = kc * kSplitBK + (u >> 1) * 8 + j;
+            v[c][j] = (kc < nkc && d < D) ? src[(size_t)d * NP] : 0.f;
+        }
+    }
+    float m = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[c][j]));
+    m = fmaxf(m, __shfl_xor(m, 2));  // the other k-octet of the pixel's chunks
+    if (u == 0) red[w][p] = m;
+    __syncthreads();
+    float mm = 0.f;
+#pragma unroll
+    for (int k = 0; k < kPackW; ++k) mm = fmaxf(mm, red[k][p]);
+    int s = 0;
+    if (mm > 0.f && mm <= 3.402823466e38f) {
+        int E;
+        (void)frexpf(mm, &E);  // mm < 2^E
+        s = 15 - E;            // mm * 2^s < 2^15: neither half overflows
+    }
+    const bool live = n0 + p < NP;
+    if (w == 0 && u == 0 && live) a.ex[z][(size_t)b * NP + n0 + p] = -s;
+    if (!live) return;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+        const int kc = w + kPackW * c;
+        if (kc >= nkc) break;
+        half8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float y = ldexpf(v[c][j], s);
+            const _Float16 hi = (_Float16)y;
+            o[j] = (u & 1) ? (__builtin_isinf(y) ? (_Float16)0.f : (_Float16)(y - (float)hi)) : hi;
+        }
+        a.pk[z][(((size_t)b * nkc + kc) * NP + n0 + p) * 4 + u] = __builtin_bit_cast(u32x4, o);
+    }
+}
+
+// Chunks per wave of the register pack for this KP, 0 = use the LDS pack.
+inline int split_pack_cpt(int KP) {
+    const int nkc = KP / kSplitBK;
+    const int cpt = (nkc + kPackW - 1) / kPackW;
+    return cpt <= 8 ? cpt : 0;
+}
+
 // Pixels per pack workgroup for this KP (LDS: TP*(KP+4)*4 + (256+TP)*4 <= 160 KiB); 0 = too large.
 inline int split_pack_tp(int KP) {
     for (int tp = 32; tp >= 4; tp >>= 1)
@@ -189,7 +261,6 @@ template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
 }
-constexpr int kQuadSwap2 = 0x4E;  // quad_perm [2,3,0,1]: lane 4k reads 4k+2
 constexpr int kQuadSwap1 = 0xB1;  // quad_perm [1,0,3,2]: lane 4k reads 4k+1
 constexpr int kRowShl4 = 0x104;   // lane i reads i+4 (same 16-lane row)
 constexpr int kRowShl8 = 0x108;   // lane i reads i+8
@@ -634,8 +705,9 @@ size_t build_split_workspace(int B, int D, int NQ, int H, int W) {
 
 bool build_split_supported(int D) { return split_pack_tp(split_kp(D)) > 0; }
 
+// lds_pack: force the LDS-tiled pack (any D; the register pack covers D <= 512).
 hipError_t launch_split_pack(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, void *ws,
-                             hipStream_t s) {
+                             hipStream_t s, bool lds_pack = false) {
     const SplitWs w = split_ws(ws, B, D, NQ, H, W);
     PackArgs a{};
     a.f[0] = f1, a.f[1] = f2;
@@ -644,6 +716,19 @@ hipError_t launch_split_pack(const float *f1, int NQ, const float *f2, int B, in
     a.np[0] = NQ, a.np[1] = H * W;
     a.D = D;
     a.KP = split_kp(D);
+    const int np = std::max(NQ, H * W);
+    if (!lds_pack) {
+        const dim3 grid((np + kPackTP - 1) / kPackTP, B, 2);
+        const dim3 blk(64 * kPackW);
+        switch (split_pack_cpt(a.KP)) {
+#define CORR_PACK_CASE(c) \
+    case c: hipLaunchKernelGGL(split_pack_reg_kernel<c>, grid, blk, 0, s, a); return hipGetLastError();
+            CORR_PACK_CASE(1) CORR_PACK_CASE(2) CORR_PACK_CASE(3) CORR_PACK_CASE(4)
+            CORR_PACK_CASE(5) CORR_PACK_CASE(6) CORR_PACK_CASE(7) CORR_PACK_CASE(8)
+#undef CORR_PACK_CASE
+            default: break;
+        }
+    }
     a.TP = split_pack_tp(a.KP);
     if (!a.TP) return hipErrorInvalidValue;
     const size_t lds = (size_t)a.TP * (a.KP + 4) * 4 + (256 + a.TP) * 4;
@@ -654,7 +739,6 @@ hipError_t launch_split_pack(const float *f1, int NQ, const float *f2, int B, in
         if (e != hipSuccess) return e;
         attr = true;
     }
-    const int np = std::max(NQ, H * W);
     hipLaunchKernelGGL(split_pack_kernel, dim3((np + a.TP - 1) / a.TP, B, 2), dim3(256), lds, s, a);
     return hipGetLastError();
 }

@@ -101,6 +101,21 @@ int main(int argc, char **argv) {
         vs.push_back({"x3   pack only", [&](float *o) {
                           return launch_split_pack(f1, (int)N, f2, sh.B, sh.D, sh.H, sh.W, ws, 0);
                       }});
+        vs.push_back({"x3   pack only LDS", [&](float *o) {
+                          return launch_split_pack(f1, (int)N, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, true);
+                      }});
+        {  // the register pack and the LDS pack must write identical bytes
+            hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f1, fe, 7u, 3.0f);
+            hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f2, fe, 8u, 0.01f);
+            std::vector<char> h0(wsb), h1(wsb);
+            CK(hipMemset(ws, 0, wsb));
+            CK(launch_split_pack(f1, (int)N, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, true));
+            CK(hipMemcpy(h0.data(), ws, wsb, hipMemcpyDeviceToHost));
+            CK(hipMemset(ws, 0, wsb));
+            CK(launch_split_pack(f1, (int)N, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, false));
+            CK(hipMemcpy(h1.data(), ws, wsb, hipMemcpyDeviceToHost));
+            printf("%-10s pack reg vs LDS: %s\n", sh.name, std::memcmp(h0.data(), h1.data(), wsb) ? "DIFFER" : "bit-identical");
+        }
         const size_t first_mfma = vs.size();
 #define MF(name, ...)                                                                                     \
         vs.push_back({name, [&](float *o) {                                                               \
