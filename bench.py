@@ -52,7 +52,11 @@ WORKLOADS = {
     "dsec": (1, 256, 60, 80, 4, 4, 12),
     "mvsec": (16, 256, 36, 44, 4, 4, 12),
     "hires1280": (1, 256, 120, 160, 4, 4, 12),
+    # BASELINE config 4: training step, batch 8 at 288x384 crops -> CorrBlock forward AND
+    # backward (grad w.r.t. both fmaps through all 12 lookups)
+    "train": (8, 256, 36, 48, 4, 4, 12),
 }
+TRAIN_WORKLOADS = {"train"}
 
 
 def parse():
@@ -64,6 +68,9 @@ def parse():
     ap.add_argument("--eager", action="store_true", help="launch eagerly instead of HIP graphs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sharded", action="store_true",
+                    help="row-shard ONE frame pair's query rows over the ranks (SURVEY §8e): RCCL "
+                         "broadcast of fmap2 + slab build + slab lookups; strong scaling")
     return ap.parse_args()
 
 
@@ -107,8 +114,9 @@ def build_traffic(workload, algo):
     return None if any(x is None for x in t) else sum(t)
 
 
-def cpu_baseline(workload, budget_s):
-    """The reference op chain on torch CPU, all host cores, bounded sample."""
+def cpu_baseline(workload, budget_s, train=False):
+    """The reference op chain on torch CPU, all host cores, bounded sample.  train: plus the
+    autograd backward to both fmaps through the 12 lookups (upstream grads randn)."""
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     from oracle import torch_ops
 
@@ -123,10 +131,18 @@ def cpu_baseline(workload, budget_s):
     base = torch.stack(torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")[::-1]).float()
     coords = [(base[None] + 0.5 * t * torch.randn(B, 2, H, W, generator=g)) for t in range(iters)]
 
+    gouts = [torch.randn(B, L * (2 * r + 1) ** 2, H, W, generator=g) for _ in range(iters)] if train else None
+    if train:
+        f1.requires_grad_(True)
+        f2.requires_grad_(True)
+
     def pair():
-        lv = torch_ops.cpu_build(f1, f2, L)
-        for c in coords:
-            torch_ops.cpu_lookup(lv, c, r)
+        with torch.set_grad_enabled(train):
+            lv = torch_ops.cpu_build(f1, f2, L)
+            outs = [torch_ops.cpu_lookup(lv, c, r) for c in coords]
+            if train:
+                torch.autograd.backward(outs, gouts)
+                f1.grad = f2.grad = None
 
     pair()  # warm
     times = []
@@ -148,7 +164,8 @@ def cpu_baseline(workload, budget_s):
     except OSError:
         pass
     return {"value": round(B / med, 3), "unit": "frame-pairs/s", "cores": cores, "kind": "port",
-            "sample": f"{len(times)} frame pairs (build + {iters} lookups, torch CPU op chain of "
+            "sample": f"{len(times)} frame pairs (build + {iters} lookups{' + autograd backward' if train else ''}"
+                      f", torch CPU op chain of "
                       f"model/corr.py), median {med * 1e3:.1f} ms, best {times[0] * 1e3:.1f} ms; "
                       f"{cpu}"}
 
@@ -182,32 +199,72 @@ def main():
               for t in range(iters)]
 
     # persistent buffers: pyramid + one output per lookup (as the GRU loop would consume them)
-    pyr = _alloc_pyramid(B, H, W, L, f1)
-    outs = [torch.empty(B, L * K, H, W, device=dev) for _ in range(iters)]
+    sharded = args.sharded
+    if sharded:
+        # every rank draws the same pair (same seed); rank 0's fmap2 is what the broadcast carries
+        from eraft_amd.sharded import _alloc_pyramid_rows, row_partition
+        if args.workload in TRAIN_WORKLOADS:
+            raise SystemExit("--sharded times the forward path (build + lookups)")
+        g = torch.Generator(device=dev).manual_seed(1234)
+        f1 = torch.randn(B, D, H, W, device=dev, generator=g)
+        f2 = torch.randn(B, D, H, W, device=dev, generator=g)
+        coords = [(base + 0.5 * t * torch.randn(B, 2, H, W, device=dev, generator=g)).contiguous()
+                  for t in range(iters)]
+        h0, h1 = row_partition(H, world, rank)
+        f1 = f1[:, :, h0:h1].contiguous()
+        coords = [c[:, :, h0:h1].contiguous() for c in coords]
+        pyr = _alloc_pyramid_rows(B, (h1 - h0) * W, H, W, L, f2)
+        outs = [torch.empty(B, L * K, h1 - h0, W, device=dev) for _ in range(iters)]
+    else:
+        pyr = _alloc_pyramid(B, H, W, L, f1)
+        outs = [torch.empty(B, L * K, H, W, device=dev) for _ in range(iters)]
 
     algo = _lib.default_algo()
     ws = _lib.build_workspace(f1, f2, algo)  # packed f16 operands (F16X3), reused every step
 
-    def run_build():
+    def build_only():
         _lib.build(f1, f2, pyr, algo, ws)
+
+    def run_build():
+        if sharded and world > 1:
+            dist.broadcast(f2, src=0)  # RCCL over xGMI: fmap2 to every row shard
+        build_only()
 
     def run_lookups():
         for c, o in zip(coords, outs):
-            _lib.lookup(pyr, c, r, o)
+            _lib.lookup(pyr, c, r, o, H, W)
+
+    train = args.workload in TRAIN_WORKLOADS
+    if train:
+        # backward of the 12 lookups + pyramid + product (eraft.py:128 detaches coords): one
+        # gradient pyramid accumulated by every lookup, folded once, then the two MFMA GEMMs
+        gouts = [torch.randn(B, L * K, H, W, device=dev, generator=g) for _ in range(iters)]
+        gpyr = _alloc_pyramid(B, H, W, L, f1, zero=True)
+        gbuf = gpyr[0]._base  # the one allocation behind every level view
+
+        def run_bwd():
+            gbuf.zero_()
+            for c, go in zip(coords, gouts):
+                _lib.lookup_bwd(c, go, r, gpyr)
+            _lib.pool_bwd(gpyr, H, W)
+            return _lib.build_bwd(gpyr[0], f1, f2)
 
     stream = torch.cuda.Stream(device=dev)
     with torch.cuda.stream(stream):
         # first call through the public drop-in API (validates the same path end to end)
-        cb = CorrBlock(f1, f2, num_levels=L, radius=r)
-        cb(coords[0])
+        if not sharded:
+            cb = CorrBlock(f1, f2, num_levels=L, radius=r)
+            cb(coords[0])
         run_build()
         run_lookups()
         torch.cuda.synchronize()
         def pair():
             run_build()
             run_lookups()
+            if train:
+                run_bwd()
 
-        if args.eager:
+        if args.eager or (sharded and world > 1):  # collectives stay out of graph capture
             step = pair
         else:
             g_pair = torch.cuda.CUDAGraph()
@@ -240,13 +297,20 @@ def main():
         g_b, g_l = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_b, stream=stream):
             for _ in range(REP):
-                run_build()
+                build_only()
         with torch.cuda.graph(g_l, stream=stream):
             for _ in range(REP):
                 run_lookups()
-        kb, kl = [], []
+        kb, kl, kw = [], [], []
+        timed = [(g_b, kb), (g_l, kl)]
+        if train:
+            g_w = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_w, stream=stream):
+                for _ in range(REP):
+                    run_bwd()
+            timed.append((g_w, kw))
         for _ in range(5):
-            for g, acc in ((g_b, kb), (g_l, kl)):
+            for g, acc in timed:
                 a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record(stream)
                 g.replay()
@@ -255,6 +319,7 @@ def main():
                 acc.append(a.elapsed_time(z))
         kb.sort()
         kl.sort()
+        kw.sort()
 
     elapsed = t1 - t0
     if world > 1:
@@ -265,13 +330,21 @@ def main():
     build_ms = kb[len(kb) // 2] / REP
     look_ms = kl[len(kl) // 2] / (REP * iters)
 
-    pairs = B * args.steps * world
+    pairs = B * args.steps * (1 if sharded else world)
     value = pairs / elapsed
     fl = build_flops(B, D, H, W)
     lb = lookup_bytes(B, H, W, L, r)
+    if sharded:  # per-rank kernels process the rank's slab (rank 0 owns the largest)
+        frac_rows = (h1 - h0) / H
+        fl *= frac_rows
+        lb *= frac_rows
     ach_tf = fl / (build_ms * 1e-3) / 1e12
     look_gbs = lb / (look_ms * 1e-3) / 1e9
-    hbm_gbs = (build_bytes(B, D, H, W, L) + iters * lb) / (build_ms + iters * look_ms) / 1e6
+    bb = build_bytes(B, D, H, W, L)
+    if sharded:
+        lvn = sum((H >> l) * (W >> l) for l in range(L))
+        bb = B * D * (h1 - h0 + H) * W * 4 + B * (h1 - h0) * W * lvn * 4
+    hbm_gbs = (bb + iters * lb) / (build_ms + iters * look_ms) / 1e6
 
     if rank == 0:
         res = {
@@ -283,21 +356,24 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (randn fmaps, coords_grid + randn flow), resident in HBM",
-            "config": {"workload": f"CorrBlock build + {iters} lookups, {args.workload} "
+            "config": {"workload": f"CorrBlock build + {iters} lookups{' + backward' if train else ''}, "
+                                   f"{args.workload} "
                                    f"fmaps [{B},{D},{H},{W}], {L} levels, radius {r}",
                        "global_batch": B * world, "launch": "eager" if args.eager else "hipgraph",
-                       "parallelism": f"replicas x{world} (independent frame pairs per GPU)"},
+                       "parallelism": (f"row-sharded x{world} (query rows of one pair per GPU, "
+                                       "fmap2 RCCL broadcast)") if sharded else
+                                      f"replicas x{world} (independent frame pairs per GPU)"},
             "build_algo": BUILD_ALGO[algo],
             "roofline": {"bound": "mfma", "kernel": BUILD_KERNELS[algo],
                          "achieved": round(ach_tf, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(ach_tf / PEAK_FP32_MFMA_TFLOPS, 4),
                          "traffic": build_traffic(args.workload, algo),
                          "avg_us": round(build_ms * 1e3, 2), "flops_per_launch": fl,
-                         "bytes_per_launch": build_bytes(B, D, H, W, L),
+                         "bytes_per_launch": bb,
                          "note": BUILD_NOTE[algo]},
             "roofline_lookup": {"bound": "hbm", "kernel": "lookup_kernel",
                                 "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -311,11 +387,19 @@ def main():
                if algo == _lib.BUILD_F16X3 else {}),
             "kernel_timing": f"HIP events around {REP} back-to-back launches per graph on the "
                              "launch stream, median of 5",
+            **({"backward": {
+                "phase": f"zero grad pyramid + {iters} lookup_bwd_kernel + pool_bwd + 2 MFMA GEMMs "
+                         "(dF1 = dC F2^T, dF2 = F1^T dC) + split-K reduce",
+                "avg_us": round(kw[len(kw) // 2] / REP * 1e3, 2),
+                "gemm_flops": 2 * fl,
+                "gemm_tflops_lower_bound": round(2 * fl / (kw[len(kw) // 2] / REP * 1e-3) / 1e12, 2),
+                "note": "whole backward phase time; per-kernel split in the rocprofv3 trace"}}
+               if train else {}),
             "step_gpu_us": round(step_gpu_ms * 1e3, 2),
             "hbm_gbs_algorithmic": round(hbm_gbs, 1),
         }
         if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline(wl, args.cpu_seconds)
+            cb = cpu_baseline(wl, args.cpu_seconds, train)
             res["cpu_baseline"] = cb
             res["speedup_vs_cpu"] = round(value / cb["value"], 1)
         print(json.dumps(res))

@@ -312,20 +312,36 @@ __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
 template <int S>
 struct LookupBwdSmem {
     static constexpr int WIN = S + 2;
-    static constexpr int WSTR = (WIN * WIN) | 1;
+    static constexpr int WSTR = (WIN * WIN) | 1;  // odd stride: lane = query writes conflict-free
     float g[S * S][kQB];   // upstream gradient tile
     float tx[3][S][kQB];   // floor, lo, hi per x-tap
     float ty[3][S][kQB];
     int ax[kQB], ay[kQB];
-    float win[kQB * WSTR];  // irregular path only
+    float win[kQB * WSTR];  // per-query neighbourhood sums (cell (cy, cx) at cy * WIN + cx)
 };
 
+constexpr int lookup_bwd_threads(int S) { return 64 * (S + 2); }
+
+// Backward, three phases (S + 2 waves, 64 queries):
+//   1. thread (q, t < S): tap t of query q on both axes + the gradient row of x-tap t -> LDS;
+//   2. lane = query, wave = neighbourhood COLUMN cx: every cell (cx, cy) of the column sums its
+//      contributions in the reference's scatter order (x-tap i outer, y-tap j inner; one
+//      corner per (i, j)) — reads conflict-free (query-fastest LDS rows), sums -> win;
+//   3. lane = consecutive cells of one query: coalesced read-modify-write of the gradient
+//      pyramid, G = G + sum (one RMW per cell, no atomics: the cells are the query's own).
+// Regular workgroups (floor(tap t) = floor(tap 0) + t on both axes) use the closed form — cell
+// (cx, cy) of the (S+1)^2 block gets se(cx-1, cy-1), ne(cx-1, cy), sw(cx, cy-1), nw(cx, cy) —
+// with all of a column's taps in registers.  Other workgroups find each column's / row's taps
+// as the contiguous ranges {i : floor_i - anchor in {c - 1, c}} (floors are monotone in the
+// tap index), which reduces to the same four terms, in the same order, for regular taps.
+// Workgroups where some corner falls outside the (S+2)^2 neighbourhood (|coords| near 2^20)
+// take the sequential per-query scatter (wave 0, lane = query) of the previous design.
 template <int S>
-__global__ __launch_bounds__(64 * S) void lookup_bwd_kernel(const float *__restrict__ coords,
-                                                            const float *__restrict__ grad_out,
-                                                            int B, int NQ, int H, int W, int L,
-                                                            LevelPtrs gpyr) {
-    constexpr int R = (S - 1) / 2, K = S * S, NT = 64 * S;
+__global__ __launch_bounds__(lookup_bwd_threads(S)) void lookup_bwd_kernel(const float *__restrict__ coords,
+                                                                           const float *__restrict__ grad_out,
+                                                                           int B, int NQ, int H, int W, int L,
+                                                                           LevelPtrs gpyr) {
+    constexpr int R = (S - 1) / 2, K = S * S, NT = lookup_bwd_threads(S);
     using SM = LookupBwdSmem<S>;
     constexpr int WIN = SM::WIN, WS = WIN * WIN, WSTR = SM::WSTR;
     constexpr int C = S + 1;  // cells per axis reached by regular taps
@@ -344,81 +360,133 @@ __global__ __launch_bounds__(64 * S) void lookup_bwd_kernel(const float *__restr
 
     const int tid = threadIdx.x;
     const int q = tid & (kQB - 1);
-    const int t = tid >> 6;
+    const int t = tid >> 6;  // wave: tap in phase 1, neighbourhood column in phase 2
     const int n = n0 + q;
     const bool qok = n < N;
 
     // ---- 1. taps and the upstream gradient tile ----
-    const float cxv = qok ? coords[((size_t)b * 2 + 0) * N + n] : 0.0f;
-    const float cyv = qok ? coords[((size_t)b * 2 + 1) * N + n] : 0.0f;
-    const Axis a = tap_axis(cxv, inv_scale, t, R, Wl);
-    const Axis c = tap_axis(cyv, inv_scale, t, R, Hl);
-    sm.tx[0][t][q] = a.f;
-    sm.tx[1][t][q] = a.lo;
-    sm.tx[2][t][q] = a.hi;
-    sm.ty[0][t][q] = c.f;
-    sm.ty[1][t][q] = c.lo;
-    sm.ty[2][t][q] = c.hi;
-    if (t == 0) {
-        sm.ax[q] = anchor_of(a.f);
-        sm.ay[q] = anchor_of(c.f);
-    }
-    {
+    Axis a{}, c{};
+    if (t < S) {
+        const float cxv = qok ? coords[((size_t)b * 2 + 0) * N + n] : 0.0f;
+        const float cyv = qok ? coords[((size_t)b * 2 + 1) * N + n] : 0.0f;
+        a = tap_axis(cxv, inv_scale, t, R, Wl);
+        c = tap_axis(cyv, inv_scale, t, R, Hl);
         const float *g = grad_out + (((size_t)b * L + l) * K + (size_t)t * S) * N + n;
         float v[S];
 #pragma unroll
         for (int u = 0; u < S; ++u) v[u] = qok ? g[(size_t)u * N] : 0.0f;
+        sm.tx[0][t][q] = a.f;
+        sm.tx[1][t][q] = a.lo;
+        sm.tx[2][t][q] = a.hi;
+        sm.ty[0][t][q] = c.f;
+        sm.ty[1][t][q] = c.lo;
+        sm.ty[2][t][q] = c.hi;
+        if (t == 0) {
+            sm.ax[q] = anchor_of(a.f);
+            sm.ay[q] = anchor_of(c.f);
+        }
 #pragma unroll
         for (int u = 0; u < S; ++u) sm.g[t * S + u][q] = v[u];
     }
     __syncthreads();
-    // regular: floor(tap t) == floor(tap 0) + t on both axes (or the query has no in-map corner)
     const float fx0 = sm.tx[0][0][q], fy0 = sm.ty[0][0][q];
     const bool far = anchor_of(fx0) == kFarAnchor || anchor_of(fy0) == kFarAnchor;
-    const bool reg = far || (a.f - fx0 == (float)t && c.f - fy0 == (float)t);
+    const bool reg = t >= S || far || (a.f - fx0 == (float)t && c.f - fy0 == (float)t);
+    const bool cov = t > 0 || window_covers<S>(fx0, sm.tx[0][S - 1][q], fy0, sm.ty[0][S - 1][q]);
     const int irregular = __syncthreads_or(!reg);
+    const int uncovered = __syncthreads_or(!cov);
 
-    if (!irregular) {
-        // ---- 2a. gather: cell (cx, cy), cx, cy in [0, S] of each query ----
-        constexpr int CELLS = kQB * C * C;
-        constexpr int PER = (CELLS + NT - 1) / NT;
-        float sum[PER], old[PER];
-        size_t dst[PER];
-        bool live[PER];
+    if (!uncovered) {
+        float *wq = &sm.win[q * WSTR];
+        const int cx = t;
+        if (!irregular) {
+            // ---- 2a. closed form: column cx of the (S+1)^2 block ----
+            if (cx < C && !far) {
+                float wlo = 0.f, whi = 0.f;  // x weights: lo of tap cx, hi of tap cx - 1
+                if (cx < S) wlo = sm.tx[1][cx][q];
+                if (cx >= 1) whi = sm.tx[2][cx - 1][q];
+                float ylo[S], yhi[S], gp[S], gc[S];
 #pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int item = tid + NT * u;
-            const int qq = item / (C * C);
-            const int e = item - qq * (C * C);
-            const int cy = e / C, cx = e - cy * C;
-            const int X = sm.ax[qq] + cx, Y = sm.ay[qq] + cy;
-            live[u] = item < CELLS && n0 + qq < N && X >= 0 && X < Wl && Y >= 0 && Y < Hl;
-            float s = 0.0f;
-            if (live[u]) {
-                if (cx >= 1 && cy >= 1)  // se corner of tap (cx-1, cy-1)
-                    s = s + __fmul_rn(sm.g[(cx - 1) * S + cy - 1][qq],
-                                      __fmul_rn(sm.ty[2][cy - 1][qq], sm.tx[2][cx - 1][qq]));
-                if (cx >= 1 && cy < S)  // ne corner of tap (cx-1, cy)
-                    s = s + __fmul_rn(sm.g[(cx - 1) * S + cy][qq],
-                                      __fmul_rn(sm.ty[1][cy][qq], sm.tx[2][cx - 1][qq]));
-                if (cx < S && cy >= 1)  // sw corner of tap (cx, cy-1)
-                    s = s + __fmul_rn(sm.g[cx * S + cy - 1][qq],
-                                      __fmul_rn(sm.ty[2][cy - 1][qq], sm.tx[1][cx][qq]));
-                if (cx < S && cy < S)  // nw corner of tap (cx, cy)
-                    s = s + __fmul_rn(sm.g[cx * S + cy][qq],
-                                      __fmul_rn(sm.ty[1][cy][qq], sm.tx[1][cx][qq]));
+                for (int j = 0; j < S; ++j) {
+                    ylo[j] = sm.ty[1][j][q];
+                    yhi[j] = sm.ty[2][j][q];
+                    gp[j] = cx >= 1 ? sm.g[(cx - 1) * S + j][q] : 0.f;
+                    gc[j] = cx < S ? sm.g[cx * S + j][q] : 0.f;
+                }
+#pragma unroll
+                for (int cy = 0; cy < C; ++cy) {
+                    float s = 0.0f;
+                    if (cx >= 1 && cy >= 1) s = s + __fmul_rn(gp[cy - 1], __fmul_rn(yhi[cy - 1], whi));  // se
+                    if (cx >= 1 && cy < S) s = s + __fmul_rn(gp[cy], __fmul_rn(ylo[cy], whi));           // ne
+                    if (cx < S && cy >= 1) s = s + __fmul_rn(gc[cy - 1], __fmul_rn(yhi[cy - 1], wlo));   // sw
+                    if (cx < S && cy < S) s = s + __fmul_rn(gc[cy], __fmul_rn(ylo[cy], wlo));            // nw
+                    wq[cy * WIN + cx] = s;
+                }
             }
-            sum[u] = s;
-            dst[u] = live[u] ? (qbase + qq) * mapsz + (size_t)Y * Wl + X : 0;
-            old[u] = live[u] ? G[dst[u]] : 0.0f;
-        }
+        } else if (!far) {
+            // ---- 2b. general taps: contiguous hit ranges per column / row ----
+            float dy[S];
 #pragma unroll
-        for (int u = 0; u < PER; ++u)
-            if (live[u]) G[dst[u]] = old[u] + sum[u];
+            for (int j = 0; j < S; ++j) dy[j] = sm.ty[0][j][q] - fy0;
+            int i0 = 0, i1 = 0;
+#pragma unroll
+            for (int i = 0; i < S; ++i) {
+                const float d = sm.tx[0][i][q] - fx0;
+                i0 += d < (float)(cx - 1);
+                i1 += d <= (float)cx;
+            }
+#pragma unroll
+            for (int cy = 0; cy < WIN; ++cy) {
+                int j0 = 0, j1 = 0;
+#pragma unroll
+                for (int j = 0; j < S; ++j) {
+                    j0 += dy[j] < (float)(cy - 1);
+                    j1 += dy[j] <= (float)cy;
+                }
+                float s = 0.0f;
+                for (int i = i0; i < i1; ++i) {
+                    const float wx = (sm.tx[0][i][q] - fx0 == (float)cx) ? sm.tx[1][i][q] : sm.tx[2][i][q];
+                    for (int j = j0; j < j1; ++j) {
+                        const float wy = (sm.ty[0][j][q] - fy0 == (float)cy) ? sm.ty[1][j][q] : sm.ty[2][j][q];
+                        s = s + __fmul_rn(sm.g[i * S + j][q], __fmul_rn(wy, wx));
+                    }
+                }
+                wq[cy * WIN + cx] = s;
+            }
+        }
+        __syncthreads();
+        // ---- 3. coalesced read-modify-write of the query's cells ----
+        auto rmw = [&](auto cc_tag) {
+            constexpr int CC = decltype(cc_tag)::value;
+            constexpr int CELLS = kQB * CC * CC;
+            constexpr int PER = (CELLS + NT - 1) / NT;
+            float sum[PER], old[PER];
+            size_t dst[PER];
+            bool live[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int item = tid + NT * u;
+                const int qq = item / (CC * CC);
+                const int e = item - qq * (CC * CC);
+                const int cy = e / CC, cx2 = e - cy * CC;
+                const int X = sm.ax[qq] + cx2, Y = sm.ay[qq] + cy;
+                live[u] = item < CELLS && n0 + qq < N && X >= 0 && X < Wl && Y >= 0 && Y < Hl;
+                sum[u] = live[u] ? sm.win[qq * WSTR + cy * WIN + cx2] : 0.0f;
+                dst[u] = live[u] ? (qbase + qq) * mapsz + (size_t)Y * Wl + X : 0;
+                old[u] = live[u] ? G[dst[u]] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < PER; ++u)
+                if (live[u]) G[dst[u]] = old[u] + sum[u];
+        };
+        if (!irregular)
+            rmw(std::integral_constant<int, C>{});
+        else
+            rmw(std::integral_constant<int, WIN>{});
         return;
     }
 
-    // ---- 2b. irregular workgroup: sequential per-query scatter (wave 0, lane = query) ----
+    // ---- 2c. uncovered workgroup: sequential per-query scatter (wave 0, lane = query) ----
     for (int g = tid; g < kQB * WSTR; g += NT) sm.win[g] = 0.0f;
     __syncthreads();
     if (t == 0 && qok) {
@@ -495,7 +563,7 @@ template <int S>
 hipError_t launch_lookup_bwd_s(const float *coords, const float *grad_out, int B, int NQ, int H,
                                int W, int L, const LevelPtrs &gpyr, hipStream_t s) {
     const int nqb = (NQ + kQB - 1) / kQB;
-    hipLaunchKernelGGL(lookup_bwd_kernel<S>, dim3(nqb * B, L), dim3(64 * S), 0, s, coords, grad_out,
+    hipLaunchKernelGGL(lookup_bwd_kernel<S>, dim3(nqb * B, L), dim3(lookup_bwd_threads(S)), 0, s, coords, grad_out,
                        B, NQ, H, W, L, gpyr);
     return hipGetLastError();
 }

@@ -10,7 +10,10 @@ is O(N^2) (1920x1280: 5.9 GB per pair), so the build partitions the QUERY pixels
     rows plus the FULL fmap2 -> one RCCL broadcast of fmap2 per frame pair (over xGMI);
   * lookups produce the rank's output rows; an optional all-gather assembles the full
     [B, L*K, H, W] tensor when a replicated consumer needs it;
-  * backward: dfmap1 is row-local; dfmap2 is a sum of per-rank partials -> all-reduce.
+  * backward (training): every lookup's backward accumulates into the rank's gradient
+    pyramid slab; the build's backward folds it and runs the two GEMMs on the slab, giving
+    the slab's dfmap1 rows (row-local, no exchange) and a PARTIAL dfmap2 (the slab's queries
+    only) -> one all-reduce (RCCL) of B*D*H*W floats per frame pair.
 
 Per-query arithmetic is unchanged, so sharded results are bit-identical to one GPU.
 The compute goes through libcorr_mi355x.so's *_rows entry points (``HipRows`` below).
@@ -50,6 +53,25 @@ class HipRows:
         _lib.lookup(levels, coords_rows, radius, out, H, W)
         return out
 
+    @staticmethod
+    def zero_pyramid(B, NQ, H, W, num_levels, like):
+        lv = _alloc_pyramid_rows(B, NQ, H, W, num_levels, like)
+        lv[0]._base.zero_()
+        return lv
+
+    @staticmethod
+    def lookup_bwd(coords_rows, grad_rows, radius, grad_levels, H, W):
+        _lib.lookup_bwd(coords_rows, grad_rows, radius, grad_levels, H, W)
+
+    @staticmethod
+    def pool_bwd(grad_levels, H, W):
+        _lib.pool_bwd(grad_levels, H, W)
+
+    @staticmethod
+    def build_bwd(grad_c, f1_rows, f2):
+        """-> (dfmap1 of the slab, this slab's partial dfmap2)."""
+        return _lib.build_bwd(grad_c, f1_rows, f2)
+
 
 def _alloc_pyramid_rows(B, NQ, H, W, num_levels, like):
     shapes = [(H >> l, W >> l) for l in range(num_levels)]
@@ -60,6 +82,54 @@ def _alloc_pyramid_rows(B, NQ, H, W, num_levels, like):
         tot += (s + 3) // 4 * 4
     buf = torch.empty(tot, dtype=torch.float32, device=like.device)
     return [buf[o:o + s].view(B * NQ, 1, h, w) for o, s, (h, w) in zip(offs, sizes, shapes)]
+
+
+class _ShardState:
+    __slots__ = ("levels", "grad_levels", "B", "NQ", "H", "W", "backend", "group")
+
+
+class _ShardBuildFn(torch.autograd.Function):
+    """Build of the rank's slab; backward = pool fold + slab GEMMs + all-reduce of dfmap2."""
+
+    @staticmethod
+    def forward(ctx, f1_rows, f2, num_levels, st):
+        st.levels = st.backend.build(f1_rows, f2, num_levels) if st.NQ > 0 else None
+        ctx.save_for_backward(f1_rows, f2)
+        ctx.st, ctx.num_levels = st, num_levels
+        return f1_rows.new_zeros(())  # autograd anchor of the lookups
+
+    @staticmethod
+    def backward(ctx, _):
+        f1_rows, f2 = ctx.saved_tensors
+        st = ctx.st
+        gl, st.grad_levels = st.grad_levels, None
+        if gl is None:  # no lookup reached the loss on this rank
+            gl = st.backend.zero_pyramid(st.B, st.NQ, st.H, st.W, ctx.num_levels, f2)
+        if st.NQ > 0:
+            st.backend.pool_bwd(gl, st.H, st.W)
+            df1, df2 = st.backend.build_bwd(gl[0], f1_rows, f2)
+        else:  # a rank without rows still joins the all-reduce
+            df1, df2 = torch.zeros_like(f1_rows), torch.zeros_like(f2)
+        if dist.get_world_size(st.group) > 1:
+            dist.all_reduce(df2, group=st.group)
+        return df1, df2, None, None
+
+
+class _ShardLookupFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, coords_rows, token, radius, st):
+        ctx.save_for_backward(coords_rows)
+        ctx.st, ctx.radius = st, radius
+        return st.backend.lookup(st.levels, coords_rows, radius, st.H, st.W)
+
+    @staticmethod
+    def backward(ctx, grad_rows):
+        (coords_rows,) = ctx.saved_tensors
+        st = ctx.st
+        if st.grad_levels is None:
+            st.grad_levels = st.backend.zero_pyramid(st.B, st.NQ, st.H, st.W, len(st.levels), coords_rows)
+        st.backend.lookup_bwd(coords_rows, grad_rows.contiguous(), ctx.radius, st.grad_levels, st.H, st.W)
+        return None, torch.zeros((), dtype=torch.float32, device=coords_rows.device), None, None
 
 
 class RowShardedCorrBlock:
@@ -83,12 +153,27 @@ class RowShardedCorrBlock:
         self.h0, self.h1 = row_partition(H, self.world, self.rank)
         self.backend = backend
         if broadcast and self.world > 1:
-            dist.broadcast(fmap2, src=src, group=group)
+            with torch.no_grad():
+                dist.broadcast(fmap2, src=src, group=group)
         f1 = fmap1 if fmap1_is_slab else fmap1[:, :, self.h0:self.h1]
         if f1.shape[2] != self.h1 - self.h0:
             raise ValueError(f"fmap1 slab has {f1.shape[2]} rows, rank {self.rank} owns "
                              f"{self.h1 - self.h0}")
         self.fmap2 = fmap2
+        self._token = None
+        if torch.is_grad_enabled() and (f1.requires_grad or fmap2.requires_grad):
+            # training: autograd through the slab; dfmap2 is all-reduced over `group`
+            st = _ShardState()
+            st.B, st.NQ, st.H, st.W = B, (self.h1 - self.h0) * W, H, W
+            st.backend, st.group, st.grad_levels, st.levels = backend, group, None, None
+            self._st = st
+            if self.h1 > self.h0:
+                self._token = _ShardBuildFn.apply(f1.contiguous(), fmap2, num_levels, st)
+                self.corr_pyramid = st.levels
+            else:
+                self._token = _ShardBuildFn.apply(f1, fmap2, num_levels, st)
+                self.corr_pyramid = None
+            return
         self.corr_pyramid = (backend.build(f1.contiguous(), fmap2, num_levels)
                              if self.h1 > self.h0 else None)
 
@@ -102,7 +187,11 @@ class RowShardedCorrBlock:
         coords = coords.contiguous()
         K = (2 * self.radius + 1) ** 2
         if self.corr_pyramid is None:
-            return coords.new_empty((self.B, self.num_levels * K, 0, self.W))
+            out = coords.new_empty((self.B, self.num_levels * K, 0, self.W))
+            # keep the rank in the autograd graph so its backward joins the all-reduce
+            return out + self._token if self._token is not None and torch.is_grad_enabled() else out
+        if self._token is not None and torch.is_grad_enabled():
+            return _ShardLookupFn.apply(coords.detach(), self._token, self.radius, self._st)
         return self.backend.lookup(self.corr_pyramid, coords, self.radius, self.H, self.W)
 
     def gather(self, out_rows):

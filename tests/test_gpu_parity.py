@@ -205,14 +205,25 @@ def test_lookup_nan_and_inf_coords():
     assert bit_equal(cb(torch.from_numpy(c).to(DEV)).cpu().numpy(), oracle.lookup(gpu, c, r))
 
 
+@pytest.mark.parametrize("kind", ["random", "grid", "huge"])
 @pytest.mark.parametrize("B,D,H,W,L,r", [(2, 16, 18, 24, 4, 4), (1, 8, 17, 23, 3, 3), (1, 256, 60, 80, 4, 4)])
-def test_lookup_bwd_bitexact_vs_oracle(B, D, H, W, L, r):
+def test_lookup_bwd_bitexact_vs_oracle(B, D, H, W, L, r, kind):
     """One lookup's input-gradient from a zeroed pyramid: same tap / corner order as the
-    oracle -> bit-identical; then the avg-pool backward fold, also bit-identical."""
+    oracle -> bit-identical; then the avg-pool backward fold, also bit-identical.
+    kind: random coords (regular taps: closed-form gather), the integer pixel grid (the
+    cold-start first iteration; tap floors jitter -> general range gather), and a few
+    coordinates near 2^20 (taps outside the neighbourhood -> sequential scatter path)."""
     from eraft_amd import _lib
     from eraft_amd.corr import _alloc_pyramid
     K = (2 * r + 1) ** 2
     c = prng.lookup_coords(5, B, H, W, 3.0)
+    if kind == "grid":
+        ys, xs = np.meshgrid(np.arange(H, dtype=np.float32), np.arange(W, dtype=np.float32), indexing="ij")
+        c[:, 0], c[:, 1] = xs, ys
+        c[:, :, 1::3, ::2] += np.float32(0.5)
+    elif kind == "huge":
+        c[0, 0, 1, :3] = [1048000.5, -1048001.25, 1048575.0]
+        c[0, 1, 2, :2] = [1047999.75, 3.0]
     c[0, :, 0, :3] = np.float32(np.nan)  # NaN coords contribute nothing
     go = prng.gauss(6, (B, L * K, H, W))
     ref = oracle.lookup_bwd(c, go, [np.zeros((B * H * W, 1, h, w), np.float32)

@@ -39,7 +39,44 @@ class OracleRows:
 
     @staticmethod
     def lookup(levels, coords_rows, radius, H, W):
-        return torch.from_numpy(oracle.lookup_rows(levels, coords_rows.numpy(), H, W, radius))
+        return torch.from_numpy(oracle.lookup_rows(levels, np.asarray(coords_rows.detach()), H, W, radius))
+
+    # backward: the slab is embedded in a full-size problem whose other query rows carry zero
+    # gradient, so the oracle's full-map backward gives exactly the slab's contributions
+
+    @staticmethod
+    def zero_pyramid(B, NQ, H, W, num_levels, like):
+        return [torch.zeros(B * NQ, 1, H >> l, W >> l) for l in range(num_levels)]
+
+    @staticmethod
+    def lookup_bwd(coords_rows, grad_rows, radius, grad_levels, H, W):
+        B, _, rows, _ = coords_rows.shape
+        h0 = OracleRows.h0
+        fc = np.zeros((B, 2, H, W), np.float32)
+        fc[:, :, h0:h0 + rows] = coords_rows.numpy()
+        fg = np.zeros((B, grad_rows.shape[1], H, W), np.float32)
+        fg[:, :, h0:h0 + rows] = grad_rows.numpy()
+        gp = [np.zeros((B * H * W, 1, H >> l, W >> l), np.float32) for l in range(len(grad_levels))]
+        oracle.lookup_bwd(fc, fg, gp, radius)
+        for acc, g in zip(grad_levels, gp):
+            part = g.reshape(B, H * W, -1)[:, h0 * W:(h0 + rows) * W].reshape(acc.shape)
+            acc += torch.from_numpy(np.ascontiguousarray(part))
+
+    @staticmethod
+    def pool_bwd(grad_levels, H, W):
+        oracle.pool_bwd([g.numpy() for g in grad_levels], H, W)
+
+    @staticmethod
+    def build_bwd(grad_c, f1_rows, f2):
+        B, D, rows, W = f1_rows.shape
+        H = f2.shape[2]
+        h0 = OracleRows.h0
+        gc = np.zeros((B, H * W, H * W), np.float32)
+        gc[:, h0 * W:(h0 + rows) * W] = grad_c.numpy().reshape(B, rows * W, H * W)
+        f1 = np.zeros((B, D, H, W), np.float32)
+        f1[:, :, h0:h0 + rows] = f1_rows.detach().numpy()
+        df1, df2 = oracle.corr_bwd(gc.reshape(B * H * W, H * W), f1, f2.detach().numpy())
+        return torch.from_numpy(np.ascontiguousarray(df1[:, :, h0:h0 + rows])), torch.from_numpy(df2)
 
 
 def _free_port():
@@ -94,6 +131,59 @@ def test_row_sharded_matches_unsharded(world, shape):
     assert covered == list(range(H))
 
 
+def _train_worker(rank, world, port, shape, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from eraft_amd.sharded import RowShardedCorrBlock, row_partition
+
+        B, D, H, W, L, r, T = shape
+        f1 = torch.from_numpy(prng.gauss(1, (B, D, H, W))).requires_grad_(True)
+        f2 = torch.from_numpy(prng.gauss(2, (B, D, H, W))).requires_grad_(True)
+        h0, h1 = row_partition(H, world, rank)
+        OracleRows.h0 = h0
+        blk = RowShardedCorrBlock(f1, f2, L, r, backend=OracleRows)
+        loss = 0
+        for t in range(T):
+            c = torch.from_numpy(prng.lookup_coords(10 + t, B, H, W, 3.0))
+            g = torch.from_numpy(prng.gauss(20 + t, (B, L * (2 * r + 1) ** 2, H, W)))
+            loss = loss + (blk(c) * g[:, :, h0:h1]).sum()
+        loss.backward()
+        q.put((rank, h0, h1, f1.grad.numpy(), f2.grad.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,shape", [(2, (1, 8, 12, 16, 3, 3, 2)), (3, (2, 6, 8, 12, 2, 2, 3)),
+                                         (3, (1, 4, 2, 8, 1, 1, 2))])  # last: rank 2 owns no rows
+def test_row_sharded_training_grads(world, shape):
+    """dfmap1 rows are rank-local; dfmap2 = all-reduce of the slab partials == unsharded."""
+    B, D, H, W, L, r, T = shape
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_worker, args=(g, world, port, shape, q)) for g in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    f1, f2 = prng.gauss(1, (B, D, H, W)), prng.gauss(2, (B, D, H, W))
+    K = (2 * r + 1) ** 2
+    cl = [prng.lookup_coords(10 + t, B, H, W, 3.0) for t in range(T)]
+    gl = [prng.gauss(20 + t, (B, L * K, H, W)) for t in range(T)]
+    rdf1, rdf2 = oracle.fmap_grads(f1, f2, cl, gl, L, r)
+    df1 = np.zeros_like(rdf1)
+    for rank, h0, h1, g1, g2 in res:
+        assert not np.any(g1[:, :, :h0]) and not np.any(g1[:, :, h1:])  # row-local dfmap1
+        df1[:, :, h0:h1] = g1[:, :, h0:h1]
+        # every rank holds the all-reduced dfmap2
+        assert np.abs(g2 - rdf2).max() <= 1e-5 * np.abs(rdf2).max()
+    assert np.abs(df1 - rdf1).max() <= 1e-5 * np.abs(rdf1).max()
+
+
 def test_row_partition_covers_rows():
     from eraft_amd.sharded import row_partition
     for H in (1, 7, 60, 160):
@@ -131,3 +221,39 @@ def test_row_slab_kernels_match_full_on_gpu(G, algo, monkeypatch):
             assert bit_equal(lv[l].cpu().numpy(), ref_l.cpu().numpy())
         out = HipRows.lookup(lv, c[:, :, h0:h1].contiguous(), r, H, W)
         assert bit_equal(out.cpu().numpy(), full[:, :, h0:h1].cpu().numpy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [2, 3])
+def test_row_slab_backward_on_gpu(G):
+    """Slab backward through the HIP *_rows kernels (lookup_bwd_rows, pool_bwd, build_bwd_rows)
+    as G logical shards: dfmap1 rows match the unsharded autograd, and the sum of the slab
+    partial dfmap2 (what the all-reduce forms) matches its dfmap2."""
+    from eraft_amd import CorrBlock
+    from eraft_amd.sharded import HipRows, row_partition
+    B, D, H, W, L, r, T = 2, 64, 20, 24, 4, 4, 3
+    dev = "cuda:0"
+    f1 = torch.from_numpy(prng.gauss(1, (B, D, H, W))).to(dev).requires_grad_(True)
+    f2 = torch.from_numpy(prng.gauss(2, (B, D, H, W))).to(dev).requires_grad_(True)
+    K = (2 * r + 1) ** 2
+    cl = [torch.from_numpy(prng.lookup_coords(10 + t, B, H, W, 3.0)).to(dev) for t in range(T)]
+    gl = [torch.from_numpy(prng.gauss(20 + t, (B, L * K, H, W))).to(dev) for t in range(T)]
+    blk = CorrBlock(f1, f2, L, r)
+    loss = sum((blk(c) * g).sum() for c, g in zip(cl, gl))
+    loss.backward()
+    rdf1, rdf2 = f1.grad.cpu().numpy(), f2.grad.cpu().numpy()
+    df1 = np.zeros_like(rdf1)
+    df2 = np.zeros_like(rdf2)
+    with torch.no_grad():
+        for g in range(G):
+            h0, h1 = row_partition(H, G, g)
+            f1s = f1[:, :, h0:h1].contiguous()
+            gp = HipRows.zero_pyramid(B, (h1 - h0) * W, H, W, L, f2)
+            for c, go in zip(cl, gl):
+                HipRows.lookup_bwd(c[:, :, h0:h1].contiguous(), go[:, :, h0:h1].contiguous(), r, gp, H, W)
+            HipRows.pool_bwd(gp, H, W)
+            d1, d2 = HipRows.build_bwd(gp[0], f1s, f2)
+            df1[:, :, h0:h1] = d1.cpu().numpy()
+            df2 += d2.cpu().numpy()
+    assert np.abs(df1 - rdf1).max() <= 1e-4 * np.abs(rdf1).max()
+    assert np.abs(df2 - rdf2).max() <= 1e-4 * np.abs(rdf2).max()
