@@ -532,17 +532,18 @@ __global__ __launch_bounds__(lookup_bwd_threads(S)) void lookup_bwd_kernel(const
 
 // avg_pool2d backward, one level: fine[q][y][x] += coarse[q][y/2][x/2] * 0.25 on the pooled
 // region (y < 2*Hc, x < 2*Wc); floor-dropped rows / cols receive nothing.
+// Idx: 32-bit cell index whenever the level fits (no 64-bit divisions).
+template <typename Idx>
 __global__ __launch_bounds__(256) void pool_bwd_kernel(const float *__restrict__ coarse,
                                                        float *__restrict__ fine, long BN, int Hf,
                                                        int Wf) {
     const int Hc = Hf >> 1, Wc = Wf >> 1;
     const int Hr = 2 * Hc, Wr = 2 * Wc;
-    const size_t per = (size_t)Hr * Wr;
-    const size_t total = (size_t)BN * per;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (size_t)gridDim.x * blockDim.x) {
+    const Idx per = (Idx)Hr * Wr;
+    const Idx total = (Idx)BN * per;
+    for (Idx i = (Idx)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (Idx)gridDim.x * blockDim.x) {
         const size_t qq = i / per;
-        const int rem = (int)(i - qq * per);
+        const int rem = (int)(i - (Idx)qq * per);
         const int y = rem / Wr, x = rem - y * Wr;
         float *d = fine + qq * Hf * Wf + (size_t)y * Wf + x;
         *d = *d + coarse[qq * Hc * Wc + (size_t)(y >> 1) * Wc + (x >> 1)] * 0.25f;
@@ -606,9 +607,13 @@ hipError_t launch_pool_bwd(const LevelPtrs &gpyr, long BN, int H, int W, int lev
         const int Hf = H >> (l - 1), Wf = W >> (l - 1);
         const size_t total = (size_t)BN * (2 * (Hf >> 1)) * (2 * (Wf >> 1));
         if (total == 0) continue;
-        const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
-        hipLaunchKernelGGL(pool_bwd_kernel, dim3(grid), dim3(256), 0, s, gpyr.p[l], gpyr.p[l - 1], BN,
-                           Hf, Wf);
+        const int grid = (int)((total + 255) / 256 < 32768 ? (total + 255) / 256 : 32768);
+        if (total + (size_t)grid * 256 < (1ull << 32))
+            hipLaunchKernelGGL(pool_bwd_kernel<unsigned>, dim3(grid), dim3(256), 0, s, gpyr.p[l], gpyr.p[l - 1],
+                               BN, Hf, Wf);
+        else
+            hipLaunchKernelGGL(pool_bwd_kernel<size_t>, dim3(grid), dim3(256), 0, s, gpyr.p[l], gpyr.p[l - 1],
+                               BN, Hf, Wf);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
