@@ -205,6 +205,37 @@ int corr_build_bwd_rows(const float *grad_c, const float *fmap1_rows, int NQ, co
                       fn);
 }
 
+size_t corr_build_bwd_ex_workspace(int algo, int B, int D, int NQ, int H, int W) {
+    if (B < 1 || D < 1 || NQ < 1 || H < 1 || W < 1) return 0;
+    if (algo == CORR_BUILD_FP32) return build_bwd_workspace(B, D, NQ, H, W);
+    if (algo == CORR_BUILD_F16X3) return build_bwd_split_workspace(B, D, NQ, H, W);
+    return (size_t)-1;
+}
+
+int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, int NQ, const float *fmap2, int B,
+                      int D, int H, int W, float *dfmap1_rows, float *dfmap2, void *workspace,
+                      size_t workspace_bytes, void *stream) {
+    static const char *fn = "corr_build_bwd_ex";
+    if (algo == CORR_BUILD_FP32)
+        return corr_build_bwd_rows(grad_c, fmap1_rows, NQ, fmap2, B, D, H, W, dfmap1_rows, dfmap2, workspace,
+                                   workspace_bytes, stream);
+    g_err[0] = 0;
+    if (algo != CORR_BUILD_F16X3) return fail(CORR_EUNSUPPORTED, "%s: unknown algorithm %d", fn, algo);
+    int rc = check_dims(fn, B, NQ, H, W, 1);
+    if (rc) return rc;
+    if (D < 1) return fail(CORR_EINVAL, "%s: D must be >= 1 (got %d)", fn, D);
+    if ((rc = check_ptr(fn, grad_c, "grad_c")) || (rc = check_ptr(fn, fmap1_rows, "fmap1")) ||
+        (rc = check_ptr(fn, fmap2, "fmap2")) || (rc = check_ptr(fn, dfmap1_rows, "dfmap1")) ||
+        (rc = check_ptr(fn, dfmap2, "dfmap2")))
+        return rc;
+    const size_t need = build_bwd_split_workspace(B, D, NQ, H, W);
+    if (workspace_bytes < need || !workspace)
+        return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
+    return hip_status(launch_build_bwd_split(grad_c, fmap1_rows, NQ, fmap2, B, D, H, W, dfmap1_rows, dfmap2,
+                                             workspace, (hipStream_t)stream),
+                      fn);
+}
+
 int corr_build_bwd(const float *grad_c, const float *fmap1, const float *fmap2, int B, int D,
                    int H, int W, float *dfmap1, float *dfmap2, void *workspace,
                    size_t workspace_bytes, void *stream) {

@@ -230,6 +230,14 @@ hipError_t run_gemm(bool b_kcontig, const float *A, const float *Bm, float *C, i
 
 }  // namespace
 
+// Ordered split-K sum + 1/sqrt(D) for corr_bwd_split.hip's slabs ([split][per] floats).
+hipError_t launch_splitk_reduce(const float *ws, float *C, int splits, size_t per, float sD, hipStream_t s) {
+    const int grid = (int)std::min<size_t>((per + 255) / 256, 8192);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, ws, C, splits, per, 1.0f / sD,
+                       is_pow2(sD) ? 1 : 0, sD);
+    return hipGetLastError();
+}
+
 size_t build_bwd_workspace(int B, int D, int NQ, int H, int W) {
     const int N = H * W;
     // every GEMM goes through the slab path when sqrt(D) is not a power of two

@@ -1,0 +1,488 @@
+// corr_bwd_split.hip — the backward GEMMs of the all-pairs product on the f16 MFMA at fp32
+// accuracy (the CORR_BUILD_F16X3 scheme of corr_build_split.hip, applied to autograd of
+// model/corr.py:58-60):
+//
+//   dF1[b][d][n] = sum_m F2[b][d][m] * dC[b][n][m] / sqrt(D)    rows d of F2,  rows n of dC  (k = m)
+//   dF2[b][d][m] = sum_n F1[b][d][n] * dC[b][n][m] / sqrt(D)    rows d of F1,  cols m of dC  (k = n)
+//
+// Both are "C = A * B^T" with A and B read along k.  Every operand row r is packed once as
+// x = 2^e_r (hi + lo) in f16 (e_r puts the row's largest |x| in [2^14, 2^15)), chunk-major
+//   pk[b][kc][r][4 x 16 B]  = hi(k 16kc..+7), lo(same), hi(k 16kc+8..+15), lo(same)
+// and the GEMM accumulates lo_A hi_B + hi_A lo_B + hi_A hi_B on v_mfma_f32_32x32x16_f16 into
+// one fp32 accumulator (each f16 x f16 product exact in fp32).  The epilogue applies
+// 2^(e_A + e_B); K is split over workgroups (partial slabs, summed in split order by
+// splitk_reduce_kernel of corr_bwd.hip, which applies 1/sqrt(D)) — deterministic, no atomics.
+//
+// Packs: the row maxima of F1, F2 and dC and the column maxima of dC come from one reading
+// pass (absmax_kernel, unsigned atomicMax on the bits of non-negative floats: exact and order
+// free), then split_convert_kernel writes the f16 pairs (lane = 4 * row + unit, so each
+// store instruction writes 16 rows' chunks = 1 KiB contiguous).
+#include <algorithm>
+#include <cmath>
+
+#include "corr_build_common.h"
+
+namespace corr {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+constexpr int kBK = 16;  // k per chunk = one MFMA k-step
+
+// Row / column |max| of X[b] (rows x cols, row-major, ld = cols).  Block: 256 threads over
+// 256 columns x kRowsPer rows.  rmax / cmax: zeroed uint arrays (float bits), may be null.
+constexpr int kRowsPer = 16;
+__global__ __launch_bounds__(256) void absmax_kernel(const float *__restrict__ X, int rows, int cols,
+                                                     unsigned *__restrict__ rmax, unsigned *__restrict__ cmax) {
+    __shared__ float red[kRowsPer][4];
+    const int b = blockIdx.z;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    const int r0 = blockIdx.y * kRowsPer;
+    const float *x = X + (size_t)b * rows * cols;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float v[kRowsPer];
+#pragma unroll
+    for (int i = 0; i < kRowsPer; ++i)
+        v[i] = (c < cols && r0 + i < rows) ? fabsf(x[(size_t)(r0 + i) * cols + c]) : 0.f;
+    if (cmax && c < cols) {
+        float m = 0.f;
+#pragma unroll
+        for (int i = 0; i < kRowsPer; ++i) m = fmaxf(m, v[i]);  // fmaxf drops NaN
+        if (m > 0.f) atomicMax(&cmax[(size_t)b * cols + c], __float_as_uint(m));
+    }
+    if (rmax) {
+#pragma unroll
+        for (int i = 0; i < kRowsPer; ++i) {
+            float m = v[i];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+            if (lane == 0) red[i][w] = m;
+        }
+        __syncthreads();
+        if (threadIdx.x < kRowsPer && r0 + (int)threadIdx.x < rows) {
+            const int i = threadIdx.x;
+            const float m = fmaxf(fmaxf(red[i][0], red[i][1]), fmaxf(red[i][2], red[i][3]));
+            if (m > 0.f) atomicMax(&rmax[(size_t)b * rows + r0 + i], __float_as_uint(m));
+        }
+    }
+}
+
+// Exponent of a row from its max (as split_pack_kernel): max * 2^s < 2^15.
+__device__ __forceinline__ int split_shift(float mm) {
+    int s = 0;
+    if (mm > 0.f && mm <= 3.402823466e38f) {
+        int E;
+        (void)frexpf(mm, &E);
+        s = 15 - E;
+    }
+    return s;
+}
+
+// f16 pairs of operand rows: element (r, k) of batch b at X[b * sb + r * sr + k * sk].
+// Block: 4 waves x 16 rows; lane = 4 * row + unit; grid.x over row blocks, grid.y over
+// chunk groups (each thread walks its chunks), grid.z = batch.
+struct ConvArgs {
+    const float *X;
+    long sb, sr, sk;
+    int rows, K, nkc;
+    const unsigned *mx;  // [B][rows] float bits of the row max
+    u32x4 *pk;           // [B][nkc][rows][4]
+    int *ex;             // [B][rows] = -s
+};
+
+__global__ __launch_bounds__(256) void split_convert_kernel(ConvArgs a) {
+    const int b = blockIdx.z;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = blockIdx.x * 64 + w * 16 + (lane >> 2), u = lane & 3;
+    if (r >= a.rows) return;
+    const int s = split_shift(__uint_as_float(a.mx[(size_t)b * a.rows + r]));
+    if (blockIdx.y == 0 && u == 0) a.ex[(size_t)b * a.rows + r] = -s;
+    const float *x = a.X + (size_t)b * a.sb + (size_t)r * a.sr;
+    for (int kc = blockIdx.y; kc < a.nkc; kc += gridDim.y) {
+        const int k0 = kc * kBK + (u >> 1) * 8;
+        float v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) v[t] = (k0 + t < a.K) ? x[(size_t)(k0 + t) * a.sk] : 0.f;
+        half8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float y = ldexpf(v[j], s);
+            const _Float16 hi = (_Float16)y;
+            o[j] = (u & 1) ? (__builtin_isinf(y) ? (_Float16)0.f : (_Float16)(y - (float)hi)) : hi;
+        }
+        a.pk[(((size_t)b * a.nkc + kc) * a.rows + r) * 4 + u] = __builtin_bit_cast(u32x4, o);
+    }
+}
+
+// Row-contiguous operand (sk == 1: F1, F2 rows and dC rows): lane = u + 4 r + 16 c covers
+// 4 rows x 4 chunks per wave — each row's 4 chunks are 256 contiguous bytes read as float4
+// pairs, and each chunk's 4 rows are 256 contiguous bytes of the pack.  Block: 4 waves =
+// 16 rows; grid.y walks chunk quads.
+__global__ __launch_bounds__(256) void split_convert_rows_kernel(ConvArgs a) {
+    const int b = blockIdx.z;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int u = lane & 3, rr = (lane >> 2) & 3, c = lane >> 4;
+    const int r = blockIdx.x * 16 + w * 4 + rr;
+    if (r >= a.rows) return;
+    const int s = split_shift(__uint_as_float(a.mx[(size_t)b * a.rows + r]));
+    if (blockIdx.y == 0 && c == 0 && u == 0) a.ex[(size_t)b * a.rows + r] = -s;
+    const float *x = a.X + (size_t)b * a.sb + (size_t)r * a.sr;
+    const bool vec = (a.K % 8) == 0 && ((a.sr | a.sb) % 4) == 0;
+    for (int kc = blockIdx.y * 4 + c; kc < a.nkc; kc += gridDim.y * 4) {
+        const int k0 = kc * kBK + (u >> 1) * 8;
+        float v[8];
+        if (vec && k0 + 8 <= a.K) {
+            const float4 p0 = *reinterpret_cast<const float4 *>(x + k0);
+            const float4 p1 = *reinterpret_cast<const float4 *>(x + k0 + 4);
+            v[0] = p0.x, v[1] = p0.y, v[2] = p0.z, v[3] = p0.w;
+            v[4] = p1.x, v[5] = p1.y, v[6] = p1.z, v[7] = p1.w;
+        } else {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) v[t] = (k0 + t < a.K) ? x[k0 + t] : 0.f;
+        }
+        half8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float y = ldexpf(v[j], s);
+            const _Float16 hi = (_Float16)y;
+            o[j] = (u & 1) ? (__builtin_isinf(y) ? (_Float16)0.f : (_Float16)(y - (float)hi)) : hi;
+        }
+        a.pk[(((size_t)b * a.nkc + kc) * a.rows + r) * 4 + u] = __builtin_bit_cast(u32x4, o);
+    }
+}
+
+// Column operand (sr == 1: dC^T, rows = dC columns m, k = query n): lane = row, so each of
+// the 16 loads of a chunk is one 256-B coalesced row segment of dC.  The wave's 64 rows x
+// 4 units are staged in LDS and stored as 4 contiguous 1 KiB runs.  Block: 4 waves = 256 rows.
+__global__ __launch_bounds__(256) void split_convert_cols_kernel(ConvArgs a) {
+    __shared__ u32x4 tile[4][64 * 4];
+    const int b = blockIdx.z;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int rw = blockIdx.x * 256 + w * 64;  // the wave's first row
+    const int r = rw + lane;
+    const bool live = r < a.rows;
+    const int s = live ? split_shift(__uint_as_float(a.mx[(size_t)b * a.rows + r])) : 0;
+    if (live && blockIdx.y == 0) a.ex[(size_t)b * a.rows + r] = -s;
+    const float *x = a.X + (size_t)b * a.sb + (live ? r : 0);
+    const int vunits = min(256, 4 * max(0, a.rows - rw));
+    for (int kc = blockIdx.y; kc < a.nkc; kc += gridDim.y) {  // uniform trip count
+        float v[kBK];
+#pragma unroll
+        for (int t = 0; t < kBK; ++t) {
+            const int k = kc * kBK + t;
+            v[t] = (live && k < a.K) ? x[(size_t)k * a.sk] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            half8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float y = ldexpf(v[(u >> 1) * 8 + j], s);
+                const _Float16 hi = (_Float16)y;
+                o[j] = (u & 1) ? (__builtin_isinf(y) ? (_Float16)0.f : (_Float16)(y - (float)hi)) : hi;
+            }
+            tile[w][lane * 4 + u] = __builtin_bit_cast(u32x4, o);
+        }
+        __syncthreads();
+        u32x4 *dst = a.pk + (((size_t)b * a.nkc + kc) * a.rows + rw) * 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int e = lane + 64 * i;
+            if (e < vunits) dst[e] = tile[w][e];
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// The GEMM: C[b][i][j] (+)= sum_k A[b][i][k] B[b][j][k].  4 waves (2 along i x 2 along j),
+// each 64 i x 128 j (2 x 4 blocks of 32 x 32), workgroup 128 x 256; K chunks staged through
+// LDS double-buffered, the next chunk's global loads in flight during the MFMAs.
+// ---------------------------------------------------------------------------------------
+constexpr int kWI = 2, kWJ = 2, kMI = 2, kNJ = 4;
+constexpr int kTI = 32 * kMI * kWI;   // 128
+constexpr int kTJ = 32 * kNJ * kWJ;   // 256
+constexpr int kRows = kTI + kTJ;      // LDS rows per stage (64 B each)
+constexpr int kNT = 256;
+constexpr int kRPP = kNT / 4;         // rows per staging pass
+constexpr int kLPT = kRows / kRPP;    // 16-B loads per thread per chunk
+constexpr int kLI = kTI / kRPP;       // passes of A rows
+static_assert(kRows % kRPP == 0 && kTI % kRPP == 0, "staging tiles the chunk");
+
+__device__ __forceinline__ int swz(int j, int u) { return j * 4 + (u ^ ((j >> 2) & 3)); }
+
+struct SGemmParams {
+    const u32x4 *pkA, *pkB;
+    const int *exA, *exB;
+    float *C;             // slab base: C[split][b][i][j] (ldc = NJ)
+    int B, NI, NJ, nkc;   // batch, rows of A, rows of B, K chunks
+    int ti, tj, splits, kc_per;
+    float alpha;          // applied only when direct (one split)
+    int direct;
+};
+
+__global__ __launch_bounds__(kNT, 2) void split_gemm_kernel(SGemmParams p) {
+    __shared__ __attribute__((aligned(16))) u32x4 lds[2 * kRows * 4];
+    __shared__ int lex[kRows];
+    int id = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int tj = id % p.tj;
+    id /= p.tj;
+    const int ti = id % p.ti;
+    id /= p.ti;
+    const int split = id % p.splits;
+    const int b = id / p.splits;
+    const int i0 = ti * kTI, j0 = tj * kTJ;
+    const int kc0 = split * p.kc_per, kc1 = min(p.nkc, kc0 + p.kc_per);
+
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+    const int wv = tid >> 6, wi = wv / kWJ, wj = wv % kWJ;
+    const int unit = tid & 3, r0 = tid >> 2;
+
+    const u32x4 *src[kLPT];
+    size_t plane[kLPT];
+#pragma unroll
+    for (int k = 0; k < kLPT; ++k) {
+        const int row = r0 + kRPP * k;
+        if (k < kLI) {
+            const int i = min(i0 + row, p.NI - 1);  // clamped rows feed discarded outputs
+            src[k] = p.pkA + ((size_t)b * p.nkc * p.NI + i) * 4 + unit;
+            plane[k] = (size_t)p.NI * 4;
+        } else {
+            const int j = min(j0 + row - kTI, p.NJ - 1);
+            src[k] = p.pkB + ((size_t)b * p.nkc * p.NJ + j) * 4 + unit;
+            plane[k] = (size_t)p.NJ * 4;
+        }
+    }
+    for (int row = tid; row < kRows; row += kNT)
+        lex[row] = row < kTI ? p.exA[(size_t)b * p.NI + min(i0 + row, p.NI - 1)]
+                             : p.exB[(size_t)b * p.NJ + min(j0 + row - kTI, p.NJ - 1)];
+
+    u32x4 rg[kLPT];
+    auto load_chunk = [&](int kc) {
+#pragma unroll
+        for (int k = 0; k < kLPT; ++k) rg[k] = src[k][kc * plane[k]];
+    };
+    auto store_chunk = [&](int st) {
+        u32x4 *S = lds + (size_t)st * kRows * 4;
+#pragma unroll
+        for (int k = 0; k < kLPT; ++k) S[swz(r0 + kRPP * k, unit)] = rg[k];
+    };
+
+    f32x16 acc[kMI][kNJ];
+#pragma unroll
+    for (int m = 0; m < kMI; ++m)
+#pragma unroll
+        for (int n = 0; n < kNJ; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
+
+    const int arow0 = wi * (32 * kMI) + l32, brow0 = kTI + wj * (32 * kNJ) + l32;
+    if (kc0 < kc1) {
+        load_chunk(kc0);
+        store_chunk(0);
+    }
+    __syncthreads();
+    for (int kc = kc0; kc < kc1; ++kc) {
+        const int st = (kc - kc0) & 1;
+        if (kc + 1 < kc1) load_chunk(kc + 1);
+        const u32x4 *S = lds + (size_t)st * kRows * 4;
+        half8 ah[kMI], al[kMI], bh[kNJ], bl[kNJ];
+#pragma unroll
+        for (int m = 0; m < kMI; ++m) {
+            ah[m] = __builtin_bit_cast(half8, S[swz(arow0 + 32 * m, 2 * h)]);
+            al[m] = __builtin_bit_cast(half8, S[swz(arow0 + 32 * m, 2 * h + 1)]);
+        }
+#pragma unroll
+        for (int n = 0; n < kNJ; ++n) {
+            bh[n] = __builtin_bit_cast(half8, S[swz(brow0 + 32 * n, 2 * h)]);
+            bl[n] = __builtin_bit_cast(half8, S[swz(brow0 + 32 * n, 2 * h + 1)]);
+        }
+#pragma unroll
+        for (int m = 0; m < kMI; ++m)
+#pragma unroll
+            for (int n = 0; n < kNJ; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bh[n], acc[m][n], 0, 0, 0);
+#pragma unroll
+        for (int m = 0; m < kMI; ++m)
+#pragma unroll
+            for (int n = 0; n < kNJ; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bl[n], acc[m][n], 0, 0, 0);
+#pragma unroll
+        for (int m = 0; m < kMI; ++m)
+#pragma unroll
+            for (int n = 0; n < kNJ; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh[n], acc[m][n], 0, 0, 0);
+        if (kc + 1 < kc1) store_chunk(st ^ 1);
+        __syncthreads();
+    }
+
+    // epilogue: register g of lane (h, l32) in block (m, n) = C row i0 + wi*64 + 32m +
+    // (g & 3) + 8 (g >> 2) + 4h, column j0 + wj*128 + 32n + l32 (32 consecutive floats per
+    // half-wave store)
+    const size_t slab = (size_t)p.B * p.NI * p.NJ;  // one split's partial sums, [B][NI][NJ]
+    float *C = p.C + (p.direct ? 0 : (size_t)split * slab) + (size_t)b * p.NI * p.NJ;
+#pragma unroll
+    for (int n = 0; n < kNJ; ++n) {
+        const int jl = wj * (32 * kNJ) + 32 * n + l32;
+        const int j = j0 + jl;
+        const int ej = lex[kTI + jl];
+#pragma unroll
+        for (int m = 0; m < kMI; ++m) {
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const int il = wi * (32 * kMI) + 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
+                const int i = i0 + il;
+                float x = ldexpf(acc[m][n][g], lex[il] + ej);
+                if (p.direct) x = x * p.alpha;
+                if (i < p.NI && j < p.NJ) C[(size_t)i * p.NJ + j] = x;
+            }
+        }
+    }
+}
+
+int plan_split_k(int NI, int NJ, int nkc, int batch) {
+    const long tiles = (long)((NI + kTI - 1) / kTI) * ((NJ + kTJ - 1) / kTJ) * batch;
+    long splits = (512 + tiles - 1) / tiles;
+    splits = std::min<long>(splits, std::max(1, nkc / 8));  // >= 128 k per split
+    return (int)std::max(1L, splits);
+}
+
+inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct BwdWs {
+    u32x4 *pkA, *pkB;
+    int *exA, *exB;
+    unsigned *mxA, *mxB, *mxC;  // row max of A, row max of B (dC rows), column max of dC
+    float *slab;
+};
+
+// One region per operand pair: A rows (D), B rows (up to max(N, NQ)), K up to max(N, NQ).
+BwdWs carve(void *ws, int B, int D, int NQ, int N) {
+    const size_t R = std::max(NQ, N), KP = (size_t)(std::max(NQ, N) + kBK - 1) / kBK * kBK;
+    char *w = (char *)ws;
+    BwdWs r;
+    r.pkA = (u32x4 *)w;
+    w += al256((size_t)B * KP * D * 4);
+    r.pkB = (u32x4 *)w;
+    w += al256((size_t)B * KP * R * 4);
+    r.exA = (int *)w;
+    w += al256((size_t)B * D * 4);
+    r.exB = (int *)w;
+    w += al256((size_t)B * R * 4);
+    r.mxA = (unsigned *)w;
+    w += al256((size_t)B * D * 4);
+    r.mxB = (unsigned *)w;
+    w += al256((size_t)B * R * 4);
+    r.mxC = (unsigned *)w;
+    w += al256((size_t)B * R * 4);
+    r.slab = (float *)w;
+    return r;
+}
+
+size_t slab_floats(int B, int D, int NQ, int N) {
+    const int K1 = (N + kBK - 1) / kBK, K2 = (NQ + kBK - 1) / kBK;
+    const size_t s1 = (size_t)plan_split_k(D, NQ, K1, B) * B * D * NQ;
+    const size_t s2 = (size_t)plan_split_k(D, N, K2, B) * B * D * N;
+    return std::max(s1, s2);
+}
+
+hipError_t absmax(const float *X, int B, int rows, int cols, unsigned *rmax, unsigned *cmax, hipStream_t s) {
+    if (rmax) {
+        hipError_t e = hipMemsetAsync(rmax, 0, (size_t)B * rows * 4, s);
+        if (e != hipSuccess) return e;
+    }
+    if (cmax) {
+        hipError_t e = hipMemsetAsync(cmax, 0, (size_t)B * cols * 4, s);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(absmax_kernel, dim3((cols + 255) / 256, (rows + kRowsPer - 1) / kRowsPer, B), dim3(256), 0, s,
+                       X, rows, cols, rmax, cmax);
+    return hipGetLastError();
+}
+
+hipError_t convert(const float *X, long sb, long sr, long sk, int B, int rows, int K, const unsigned *mx, u32x4 *pk,
+                   int *ex, hipStream_t s) {
+    ConvArgs a{X, sb, sr, sk, rows, K, (K + kBK - 1) / kBK, mx, pk, ex};
+    if (sk == 1) {
+        const int rb = (rows + 15) / 16, nq = (a.nkc + 3) / 4;
+        const int gy = std::max(1, std::min(nq, 4096 / std::max(1, rb * B)));
+        hipLaunchKernelGGL(split_convert_rows_kernel, dim3(rb, gy, B), dim3(256), 0, s, a);
+    } else if (sr == 1) {
+        const int rb = (rows + 255) / 256;
+        const int gy = std::max(1, std::min(a.nkc, 4096 / std::max(1, rb * B)));
+        hipLaunchKernelGGL(split_convert_cols_kernel, dim3(rb, gy, B), dim3(256), 0, s, a);
+    } else {
+        const int rb = (rows + 63) / 64;
+        const int gy = std::max(1, std::min(a.nkc, 2048 / std::max(1, rb * B)));
+        hipLaunchKernelGGL(split_convert_kernel, dim3(rb, gy, B), dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+// C[b] (NI x NJ) = A[b] B[b]^T / sqrt(D) from packed operands; slabs + ordered reduce.
+hipError_t gemm(const BwdWs &w, int B, int NI, int NJ, int K, float sD, float *C, hipStream_t s);
+
+}  // namespace
+
+hipError_t launch_splitk_reduce(const float *ws, float *C, int splits, size_t per, float sD, hipStream_t s);
+
+namespace {
+hipError_t gemm(const BwdWs &w, int B, int NI, int NJ, int K, float sD, float *C, hipStream_t s) {
+    SGemmParams p{};
+    p.pkA = w.pkA;
+    p.pkB = w.pkB;
+    p.exA = w.exA;
+    p.exB = w.exB;
+    p.B = B;
+    p.NI = NI;
+    p.NJ = NJ;
+    p.nkc = (K + kBK - 1) / kBK;
+    p.ti = (NI + kTI - 1) / kTI;
+    p.tj = (NJ + kTJ - 1) / kTJ;
+    p.splits = plan_split_k(NI, NJ, p.nkc, B);
+    p.kc_per = (p.nkc + p.splits - 1) / p.splits;
+    p.splits = (p.nkc + p.kc_per - 1) / p.kc_per;
+    const bool exact = is_pow2(sD);
+    p.alpha = 1.0f / sD;
+    p.direct = p.splits == 1 && exact;
+    p.C = p.direct ? C : w.slab;
+    const long grid = (long)p.ti * p.tj * p.splits * B;
+    hipLaunchKernelGGL(split_gemm_kernel, dim3((unsigned)grid), dim3(kNT), 0, s, p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || p.direct) return e;
+    return launch_splitk_reduce(w.slab, C, p.splits, (size_t)B * NI * NJ, sD, s);
+}
+}  // namespace
+
+size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W) {
+    const int N = H * W;
+    const size_t R = std::max(NQ, N), KP = (size_t)(std::max(NQ, N) + kBK - 1) / kBK * kBK;
+    return al256((size_t)B * KP * D * 4) + al256((size_t)B * KP * R * 4) + al256((size_t)B * D * 4) +
+           al256((size_t)B * R * 4) + al256((size_t)B * D * 4) + 2 * al256((size_t)B * R * 4) +
+           slab_floats(B, D, NQ, N) * sizeof(float);
+}
+
+// grad_c [B][NQ][N]; f1 [B][D][NQ]; f2 [B][D][N].
+hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, const float *f2, int B, int D, int H,
+                                  int W, float *df1, float *df2, void *ws, hipStream_t s) {
+    const int N = H * W;
+    const float sD = std::sqrt((float)D);
+    const BwdWs w = carve(ws, B, D, NQ, N);
+    hipError_t e;
+#define CK_(x)                          \
+    if ((e = (x)) != hipSuccess) return e;
+    // dF1 = F2 . dC^T : A = F2 rows d (k = m), B = dC rows n (k = m)
+    CK_(absmax(grad_c, B, NQ, N, w.mxB, w.mxC, s));  // one pass: dC row and column maxima
+    CK_(absmax(f2, B, D, N, w.mxA, nullptr, s));
+    CK_(convert(f2, (long)D * N, N, 1, B, D, N, w.mxA, w.pkA, w.exA, s));
+    CK_(convert(grad_c, (long)NQ * N, N, 1, B, NQ, N, w.mxB, w.pkB, w.exB, s));
+    CK_(gemm(w, B, D, NQ, N, sD, df1, s));
+    // dF2 = F1 . dC : A = F1 rows d (k = n), B = dC columns m (k = n)
+    CK_(absmax(f1, B, D, NQ, w.mxA, nullptr, s));
+    CK_(convert(f1, (long)D * NQ, NQ, 1, B, D, NQ, w.mxA, w.pkA, w.exA, s));
+    CK_(convert(grad_c, (long)NQ * N, 1, N, B, N, NQ, w.mxC, w.pkB, w.exB, s));
+    CK_(gemm(w, B, D, N, NQ, sD, df2, s));
+#undef CK_
+    return hipSuccess;
+}
+
+}  // namespace corr

@@ -24,7 +24,8 @@ MAX_RADIUS = 7
 EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr_lookup_bwd",
            "corr_pool_bwd", "corr_build_bwd_workspace", "corr_build_bwd", "corr_build_rows",
            "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows_workspace",
-           "corr_build_bwd_rows", "corr_build_workspace", "corr_build_ex")
+           "corr_build_bwd_rows", "corr_build_workspace", "corr_build_ex",
+           "corr_build_bwd_ex_workspace", "corr_build_bwd_ex")
 
 # Build algorithms (include/corr_mi355x.h).  F16X3 is the default: fp32 features split into
 # f16 hi/lo pairs, three f16 MFMAs per product, fp32 accumulate (~1e-6 of max|C| from the
@@ -82,9 +83,12 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.corr_build_workspace.argtypes = [i, i, i, i, i, i]
     lib.corr_build_workspace.restype = sz
     lib.corr_build_ex.argtypes = [i, vp, i, vp, i, i, i, i, i, vp, vp, sz, vp]
+    lib.corr_build_bwd_ex_workspace.argtypes = [i, i, i, i, i, i]
+    lib.corr_build_bwd_ex_workspace.restype = sz
+    lib.corr_build_bwd_ex.argtypes = [i, vp, vp, i, vp, i, i, i, i, vp, vp, vp, sz, vp]
     for f in ("corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd",
               "corr_build_rows", "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows",
-              "corr_build_ex"):
+              "corr_build_ex", "corr_build_bwd_ex"):
         getattr(lib, f).restype = i
     if path is None:
         _lib = lib
@@ -184,20 +188,24 @@ def pool_bwd(grad_levels, H, W):
         _check(load().corr_pool_bwd(gp, BN, H, W, len(grad_levels), _stream(grad_levels[0])))
 
 
-def build_bwd(grad_c, fmap1, fmap2):
+def build_bwd(grad_c, fmap1, fmap2, algo=None):
     """Returns (dfmap1, dfmap2) for grad_c = dLoss/dcorr ([B*NQ, H*W] or any view of it).
-    With a row slab fmap1, dfmap1 is the slab's and dfmap2 is this slab's partial sum."""
+    With a row slab fmap1, dfmap1 is the slab's and dfmap2 is this slab's partial sum.
+    algo: BUILD_F16X3 (default, as the forward) or BUILD_FP32 (corr_build_bwd_ex)."""
+    algo = default_algo() if algo is None else algo
     B, D, H, W = fmap2.shape
     for t, nm in ((grad_c, "grad_c"), (fmap1, "fmap1"), (fmap2, "fmap2")):
         _dev(t, nm)
     lib = load()
     NQ = _nq(fmap1)
-    ws_bytes = lib.corr_build_bwd_rows_workspace(B, D, NQ, H, W)
+    ws_bytes = lib.corr_build_bwd_ex_workspace(algo, B, D, NQ, H, W)
+    if ws_bytes == ctypes.c_size_t(-1).value:
+        raise CorrError(CORR_EUNSUPPORTED, f"unknown backward algorithm {algo}")
     df1 = torch.empty_like(fmap1)
     df2 = torch.empty_like(fmap2)
-    ws = torch.empty(max(1, ws_bytes // 4), dtype=torch.float32, device=fmap1.device)
+    ws = torch.empty(max(1, (ws_bytes + 3) // 4), dtype=torch.float32, device=fmap1.device)
     with torch.cuda.device(fmap1.device):
-        _check(lib.corr_build_bwd_rows(grad_c.data_ptr(), fmap1.data_ptr(), NQ, fmap2.data_ptr(), B, D,
-                                       H, W, df1.data_ptr(), df2.data_ptr(), ws.data_ptr(), ws_bytes,
-                                       _stream(fmap1)))
+        _check(lib.corr_build_bwd_ex(algo, grad_c.data_ptr(), fmap1.data_ptr(), NQ, fmap2.data_ptr(), B,
+                                     D, H, W, df1.data_ptr(), df2.data_ptr(), ws.data_ptr(),
+                                     ws.numel() * 4, _stream(fmap1)))
     return df1, df2

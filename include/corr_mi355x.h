@@ -147,6 +147,20 @@ int corr_build_bwd_rows(const float *grad_c, const float *fmap1_rows, int NQ, co
                         int B, int D, int H, int W, float *dfmap1_rows, float *dfmap2,
                         void *workspace, size_t workspace_bytes, void *stream);
 
+/*
+ * Backward GEMMs with an explicit algorithm (the corr_build_ex counterpart of
+ * corr_build_bwd_rows; same outputs and contract).  CORR_BUILD_FP32 is corr_build_bwd_rows;
+ * CORR_BUILD_F16X3 packs F1, F2 (per feature row d) and dC (per query row for dfmap1, per
+ * target column for dfmap2) as 2^e (hi + lo) f16 pairs and runs three f16 MFMAs per product
+ * into fp32 accumulators, split-K partial sums reduced in split order (deterministic).
+ * Workspace: corr_build_bwd_ex_workspace(algo, ...) bytes ((size_t)-1: unknown algo).
+ * Replaces the autograd of model/corr.py:58-60 (bmm + division by sqrt(D)).
+ */
+size_t corr_build_bwd_ex_workspace(int algo, int B, int D, int NQ, int H, int W);
+int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, int NQ,
+                      const float *fmap2, int B, int D, int H, int W, float *dfmap1_rows,
+                      float *dfmap2, void *workspace, size_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -240,16 +240,25 @@ def test_lookup_bwd_bitexact_vs_oracle(B, D, H, W, L, r, kind):
 
 
 @pytest.mark.parametrize("B,D,H,W", [(1, 256, 60, 80), (2, 32, 18, 24), (1, 20, 17, 23), (8, 16, 12, 16)])
-def test_build_bwd_vs_oracle(B, D, H, W):
+@pytest.mark.parametrize("algo", ["f16x3", "fp32"])
+@pytest.mark.parametrize("spread", [False, True])
+def test_build_bwd_vs_oracle(B, D, H, W, algo, spread):
+    """Backward GEMMs (both algorithms) vs the fp64-accumulating oracle.  spread: rows and
+    columns of dC and the fmap rows scaled over 1e-6..1e6 (the f16 split rescales per row /
+    column; the norm-relative bar is the north_star's 1e-4)."""
     from eraft_amd import _lib
     N = H * W
     f1, f2 = prng.gauss(11, (B, D, H, W)), prng.gauss(12, (B, D, H, W))
     gc = prng.gauss(13, (B * N, N))
+    if spread:
+        gc *= (10.0 ** ((prng.uniform(14, (B * N, 1)) - 0.5) * 12)).astype(np.float32)
+        gc *= (10.0 ** ((prng.uniform(15, (1, N)) - 0.5) * 6)).astype(np.float32)
+        f1 *= (10.0 ** ((prng.uniform(16, (B, D, 1, 1)) - 0.5) * 6)).astype(np.float32)
     if B * N * N * D > 3e9:
         pytest.skip("oracle too slow")
     d1, d2 = oracle.corr_bwd(gc.reshape(B * N, 1, H, W), f1, f2)
     g1, g2 = _lib.build_bwd(torch.from_numpy(gc).to(DEV), torch.from_numpy(f1).to(DEV),
-                            torch.from_numpy(f2).to(DEV))
+                            torch.from_numpy(f2).to(DEV), _lib._ALGOS[algo])
     assert norm_rel(g1.cpu().numpy(), d1) < REL_TOL
     assert norm_rel(g2.cpu().numpy(), d2) < REL_TOL
 
