@@ -64,7 +64,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="dsec", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="dsec", choices=sorted(WORKLOADS) + ["e2e"],
+                    help="e2e: BASELINE config 2, the full E-RAFT forward (eraft_amd.model) at DSEC "
+                         "480x640, warm start, 12 GRU iterations, random-init weights")
     ap.add_argument("--eager", action="store_true", help="launch eagerly instead of HIP graphs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -170,6 +172,97 @@ def cpu_baseline(workload, budget_s, train=False):
                       f"{cpu}"}
 
 
+def run_e2e(args, world, rank, dev):
+    """BASELINE config 2: full E-RAFT forward (encoders on MIOpen, the HIP CorrBlock, 12 GRU
+    iterations, convex upsampling) on 15-bin voxel pairs at 480x640, warm start (flow_init at
+    1/8 resolution), random-init weights.  One step = one frame pair, eager launches."""
+    from eraft_amd.model import ERAFT
+    torch.manual_seed(0)
+    bins, H, W, iters = 15, 480, 640, 12
+    model = ERAFT({"subtype": "warm_start"}, n_first_channels=bins).to(dev).eval()
+    g = torch.Generator(device=dev).manual_seed(7 + rank)
+
+    def voxels():
+        v = torch.randn(1, bins, H, W, device=dev, generator=g)
+        return v * (torch.rand(1, bins, H, W, device=dev, generator=g) < 0.15)
+
+    im1, im2 = voxels(), voxels()
+    finit = 2.0 * torch.randn(1, 2, H // 8, W // 8, device=dev, generator=g)
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            model(im1, im2, iters=iters, flow_init=finit)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            model(im1, im2, iters=iters, flow_init=finit)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    res = {
+        "metric": METRIC + " [config 2: full E-RAFT forward]",
+        "value": round(args.steps * world / elapsed, 2), "unit": "frame-pairs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic 15-bin voxel grids (15% nonzero, randn), random-init weights",
+        "config": {"workload": "E-RAFT forward, DSEC 480x640 warm start, 12 GRU iters, HIP CorrBlock",
+                   "global_batch": world, "launch": "eager",
+                   "parallelism": f"replicas x{world}"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_e2e(model, im1, im2, finit, iters, args.cpu_seconds)
+        res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
+    if rank == 0:
+        print(json.dumps(res))
+
+
+def cpu_e2e(model, im1, im2, finit, iters, budget_s):
+    """The same model on the host cores with the reference CorrBlock op chain (the oracle's
+    torch-CPU restatement of model/corr.py) in place of the HIP one."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from oracle import torch_ops
+    import eraft_amd.model as M
+
+    class CpuCorrBlock:
+        def __init__(self, f1, f2, num_levels=4, radius=4):
+            self.levels, self.radius = torch_ops.cpu_build(f1, f2, num_levels), radius
+
+        def __call__(self, coords):
+            return torch_ops.cpu_lookup(self.levels, coords, self.radius)
+
+    cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(cores)
+    orig = M.CorrBlock
+    M.CorrBlock = CpuCorrBlock
+    cpu_model = model.to("cpu")
+    a, b, f = im1.cpu(), im2.cpu(), finit.cpu()
+    times = []
+    try:
+        with torch.no_grad():
+            cpu_model(a, b, iters=iters, flow_init=f)  # warm
+            t_end = time.perf_counter() + budget_s
+            while time.perf_counter() < t_end or len(times) < 2:
+                t0 = time.perf_counter()
+                cpu_model(a, b, iters=iters, flow_init=f)
+                times.append(time.perf_counter() - t0)
+    finally:
+        M.CorrBlock = orig
+        torch.set_num_threads(prev)
+    times.sort()
+    med = times[len(times) // 2]
+    return {"value": round(1.0 / med, 3), "unit": "frame-pairs/s", "cores": cores, "kind": "port",
+            "sample": f"{len(times)} full E-RAFT forwards on torch CPU (reference CorrBlock op chain), "
+                      f"median {med * 1e3:.0f} ms"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -182,6 +275,12 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    if args.workload == "e2e":
+        run_e2e(args, world, rank, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     from eraft_amd import CorrBlock, _lib
     from eraft_amd.corr import _alloc_pyramid
