@@ -236,6 +236,27 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
                       fn);
 }
 
+size_t corr_forward_splat_workspace(int B, int H, int W) {
+    if (B < 1 || H < 1 || W < 1) return 0;
+    return splat_workspace(B, H, W);
+}
+
+int corr_forward_splat(const float *flow, int B, int H, int W, float *out, void *workspace,
+                       size_t workspace_bytes, void *stream) {
+    static const char *fn = "corr_forward_splat";
+    g_err[0] = 0;
+    if (B < 1 || H < 1 || W < 1)
+        return fail(CORR_EINVAL, "%s: B, H, W must be >= 1 (got %d, %d, %d)", fn, B, H, W);
+    if ((long long)H * W * 4 >= (1ll << 31))
+        return fail(CORR_EINVAL, "%s: %dx%d is too large", fn, H, W);
+    int rc;
+    if ((rc = check_ptr(fn, flow, "flow")) || (rc = check_ptr(fn, out, "out"))) return rc;
+    const size_t need = splat_workspace(B, H, W);
+    if (workspace_bytes < need || !workspace)
+        return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
+    return hip_status(launch_forward_splat(flow, B, H, W, out, workspace, (hipStream_t)stream), fn);
+}
+
 int corr_build_bwd(const float *grad_c, const float *fmap1, const float *fmap2, int B, int D,
                    int H, int W, float *dfmap1, float *dfmap2, void *workspace,
                    size_t workspace_bytes, void *stream) {

@@ -25,7 +25,8 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
            "corr_pool_bwd", "corr_build_bwd_workspace", "corr_build_bwd", "corr_build_rows",
            "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows_workspace",
            "corr_build_bwd_rows", "corr_build_workspace", "corr_build_ex",
-           "corr_build_bwd_ex_workspace", "corr_build_bwd_ex")
+           "corr_build_bwd_ex_workspace", "corr_build_bwd_ex", "corr_forward_splat_workspace",
+           "corr_forward_splat")
 
 # Build algorithms (include/corr_mi355x.h).  F16X3 is the default: fp32 features split into
 # f16 hi/lo pairs, three f16 MFMAs per product, fp32 accumulate (~1e-6 of max|C| from the
@@ -86,9 +87,12 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.corr_build_bwd_ex_workspace.argtypes = [i, i, i, i, i, i]
     lib.corr_build_bwd_ex_workspace.restype = sz
     lib.corr_build_bwd_ex.argtypes = [i, vp, vp, i, vp, i, i, i, i, vp, vp, vp, sz, vp]
+    lib.corr_forward_splat_workspace.argtypes = [i, i, i]
+    lib.corr_forward_splat_workspace.restype = sz
+    lib.corr_forward_splat.argtypes = [vp, i, i, i, vp, vp, sz, vp]
     for f in ("corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd",
               "corr_build_rows", "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows",
-              "corr_build_ex", "corr_build_bwd_ex"):
+              "corr_build_ex", "corr_build_bwd_ex", "corr_forward_splat"):
         getattr(lib, f).restype = i
     if path is None:
         _lib = lib
@@ -209,3 +213,16 @@ def build_bwd(grad_c, fmap1, fmap2, algo=None):
                                      D, H, W, df1.data_ptr(), df2.data_ptr(), ws.data_ptr(),
                                      ws.numel() * 4, _stream(fmap1)))
     return df1, df2
+
+
+def forward_splat(flow, out):
+    """corr_forward_splat: flow [B, 2, H, W] -> out (same shape), caller-allocated."""
+    B, C, H, W = flow.shape
+    if C != 2:
+        raise ValueError(f"flow must be [B, 2, H, W] (got {tuple(flow.shape)})")
+    f, o = _dev(flow, "flow"), _dev(out, "out")
+    lib = load()
+    n = lib.corr_forward_splat_workspace(B, H, W)
+    ws = torch.empty(max(1, (n + 3) // 4), dtype=torch.int32, device=flow.device)
+    with torch.cuda.device(flow.device):
+        _check(lib.corr_forward_splat(f, B, H, W, o, ws.data_ptr(), ws.numel() * 4, _stream(flow)))

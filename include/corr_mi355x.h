@@ -161,6 +161,18 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
                       const float *fmap2, int B, int D, int H, int W, float *dfmap1_rows,
                       float *dfmap2, void *workspace, size_t workspace_bytes, void *stream);
 
+/*
+ * Warm-start forward splat.  Replaces forward_interpolate_pytorch (utils/image_utils.py:52-83)
+ * with grid_sample_values (:10-50): flow [B][2][H][W] -> out [B][2][H][W], every source pixel
+ * splatted to its floor / ceil neighbours with bilinear weights, out = sum(z w) / (sum(w) +
+ * 1e-15).  Deterministic and bit-identical to the reference's CPU put_(accumulate=True) order
+ * (corner-major, source order; an integer coordinate's floor == ceil corner counts twice, as
+ * in the reference).  Workspace: corr_forward_splat_workspace(B, H, W) bytes.
+ */
+size_t corr_forward_splat_workspace(int B, int H, int W);
+int corr_forward_splat(const float *flow, int B, int H, int W, float *out, void *workspace,
+                       size_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,6 +20,8 @@
  *   autograd of the above (eraft.py:128 detaches coords)
  *                                                   -> oracle_lookup_bwd, oracle_pool_bwd,
  *                                                      oracle_corr_bwd
+ *   utils/image_utils.py:10-83  forward_interpolate_pytorch / grid_sample_values
+ *                         (warm-start forward splat) -> oracle_forward_splat
  *
  * Build with -ffp-contract=off: every fp32 operation below is meant to round exactly once,
  * and fmaf() is used only where the reference's ATen kernel fuses.
@@ -258,4 +260,43 @@ void oracle_lookup(const float *const *pyr, const float *coords, int B, int H, i
 void oracle_lookup_bwd(const float *coords, const float *grad_out, int B, int H, int W, int L,
                        int r, float *const *grad_pyr) {
     oracle_lookup_bwd_rows(coords, grad_out, B, H * W, H, W, L, r, grad_pyr);
+}
+
+/*
+ * Warm-start forward splat, utils/image_utils.py:52-83 (forward_interpolate_pytorch) and
+ * :10-50 (grid_sample_values), per batch item and channel:
+ *   x = x0 + dx, y = y0 + dy (fp32); for x_v in (floor x, ceil x), then y_v in (floor y,
+ *   ceil y) (:27-28): w = (1 - |x - x_v|) * (1 - |y - y_v|) (:33); in-bounds points
+ *   (0 <= x_v < W, 0 <= y_v < H, :30) accumulate z*w and w at index x_v + W*y_v with
+ *   put_(accumulate=True) (:37-38) — on CPU a sequential pass in source order, one pass per
+ *   corner; an integer x or y has floor == ceil, so that corner is counted twice (kept).
+ *   out = values / (weights + 1e-15) (:46).  flow, out: [B][2][H][W].
+ */
+void oracle_forward_splat(const float *flow, int B, int H, int W, float *out) {
+    const long N = (long)H * W;
+    float *val = (float *)malloc(sizeof(float) * N);
+    float *acc = (float *)malloc(sizeof(float) * N);
+    for (int b = 0; b < B; ++b) {
+        const float *dx = flow + ((long)b * 2 + 0) * N, *dy = flow + ((long)b * 2 + 1) * N;
+        for (int c = 0; c < 2; ++c) {
+            const float *z = c == 0 ? dx : dy;
+            memset(val, 0, sizeof(float) * N);
+            memset(acc, 0, sizeof(float) * N);
+            for (int px = 0; px < 2; ++px)
+                for (int py = 0; py < 2; ++py)
+                    for (long p = 0; p < N; ++p) {
+                        const float x = (float)(p % W) + dx[p], y = (float)(p / W) + dy[p];
+                        const float xv = px ? ceilf(x) : floorf(x), yv = py ? ceilf(y) : floorf(y);
+                        if (!(xv < (float)W && xv >= 0.0f && yv < (float)H && yv >= 0.0f)) continue;
+                        const float w = (1.0f - fabsf(x - xv)) * (1.0f - fabsf(y - yv));
+                        const long idx = (long)(xv + (float)W * yv);
+                        val[idx] = val[idx] + z[p] * w;
+                        acc[idx] = acc[idx] + w;
+                    }
+            float *o = out + ((long)b * 2 + c) * N;
+            for (long t = 0; t < N; ++t) o[t] = val[t] / (acc[t] + 1e-15f);
+        }
+    }
+    free(val);
+    free(acc);
 }

@@ -47,8 +47,9 @@ def _load():
         lib.oracle_lookup_bwd.argtypes = [vp, vp, i, i, i, i, i, vp]
         lib.oracle_pool_bwd.argtypes = [vp, l, i, i, i]
         lib.oracle_corr_bwd.argtypes = [vp, vp, vp, i, i, i, vp, vp]
+        lib.oracle_forward_splat.argtypes = [vp, i, i, i, vp]
         for f in ("oracle_corr_rows", "oracle_avg_pool2x2", "oracle_lookup",
-                  "oracle_lookup_bwd", "oracle_pool_bwd", "oracle_corr_bwd"):
+                  "oracle_lookup_bwd", "oracle_pool_bwd", "oracle_corr_bwd", "oracle_forward_splat"):
             getattr(lib, f).restype = None
         _lib = lib
     return _lib
@@ -164,3 +165,12 @@ def fmap_grads(f1, f2, coords_list, grads_list, num_levels=4, radius=4):
         lookup_bwd(c, g, gp, radius)
     pool_bwd(gp, H, W)
     return corr_bwd(gp[0], f1, f2)
+
+
+def forward_splat(flow) -> np.ndarray:
+    """utils/image_utils.py:52-83 forward_interpolate_pytorch: [B, 2, H, W] -> [B, 2, H, W]."""
+    flow = _c(flow)
+    B, _, H, W = flow.shape
+    out = np.empty_like(flow)
+    _load().oracle_forward_splat(_p(flow), B, H, W, _p(out))
+    return out

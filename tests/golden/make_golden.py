@@ -132,7 +132,29 @@ def case_e2e(name, seed, H=480, W=640, bins=15, iters=12):
          flow_init=finit.numpy(), low_warm=low_w.numpy(), up_warm_sub=ups_w[-1][..., ::4, ::4].numpy())
 
 
+def case_splat(name, seed):
+    """Warm-start forward splat (utils/image_utils.py:10-83, forward_interpolate_pytorch):
+    flows with fractional, exactly-integer (floor == ceil: the reference counts that corner
+    twice), out-of-bounds and colliding targets; B = 2 at 17 x 23 and B = 1 at 60 x 80."""
+    from utils.image_utils import forward_interpolate_pytorch
+    out = {}
+    cases = [("a", 2, 17, 23, 3.0), ("b", 1, 60, 80, 6.0)]
+    for tag, B, H, W, sig in cases:
+        f = prng.gauss(seed, (B, 2, H, W), sig)
+        f[:, :, ::4, ::3] = np.round(f[:, :, ::4, ::3])          # integer displacements
+        f[0, 0, 1, :5] = [40.0, -40.0, 0.0, -0.5, 1e4]           # far out / exact / half
+        f[0, 1, 2, :4] = [0.0, 0.0, -3.0, 2.5]
+        f[0, :, 3, :6] = 0.0                                     # several sources, one target
+        out[f"flow_{tag}"] = f
+        out[f"splat_{tag}"] = forward_interpolate_pytorch(torch.from_numpy(f)).numpy()
+        seed += 1
+    save(name, **out)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "splat":
+        case_splat("g_splat", 31)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "e2e":
         case_e2e("g_e2e_dsec", 21)
         sys.exit(0)

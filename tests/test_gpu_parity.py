@@ -14,7 +14,7 @@ from oracle import oracle
 
 pytestmark = pytest.mark.gpu
 
-BUILD_CASES = [n for n in golden_names() if not n.startswith(("g_bwd", "g_dsec", "g_e2e"))]
+BUILD_CASES = [n for n in golden_names() if not n.startswith(("g_bwd", "g_dsec", "g_e2e", "g_splat"))]
 DEV = "cuda:0"
 
 
@@ -307,3 +307,33 @@ def test_errors_fail_loudly():
     cb = CB(g, g, num_levels=2)
     with pytest.raises(ValueError):
         cb(torch.zeros(1, 2, 4, 4, device=DEV))
+
+
+def _splat_flows():
+    g = load("g_splat")
+    cases = [(g[f"flow_{t}"], g[f"splat_{t}"]) for t in "ab"]
+    e = load("g_e2e_dsec")
+    cases.append((e["low"], e["flow_init"]))
+    return cases
+
+
+def test_forward_splat_bitexact_vs_reference_golden():
+    """corr_forward_splat vs the reference's own forward_interpolate_pytorch outputs."""
+    from eraft_amd import forward_interpolate_pytorch
+    for flow, ref in _splat_flows():
+        out = forward_interpolate_pytorch(torch.from_numpy(flow).to(DEV))
+        assert bit_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("B,H,W,sigma", [(3, 36, 48, 2.0), (1, 120, 160, 8.0), (2, 7, 5, 30.0)])
+def test_forward_splat_bitexact_vs_oracle(B, H, W, sigma):
+    """Random flows (dense collisions at sigma 2, far-out points at sigma 30) + integer and NaN
+    displacements, repeat runs identical (no float atomics)."""
+    from eraft_amd import forward_interpolate_pytorch
+    f = prng.gauss(41, (B, 2, H, W), sigma)
+    f[:, :, ::3, ::2] = np.round(f[:, :, ::3, ::2])
+    f[0, :, 0, :2] = np.float32(np.nan)
+    t = torch.from_numpy(f).to(DEV)
+    out = forward_interpolate_pytorch(t).cpu().numpy()
+    assert bit_equal(out, oracle.forward_splat(f))
+    assert bit_equal(forward_interpolate_pytorch(t).cpu().numpy(), out)

@@ -11,7 +11,7 @@ import prng
 from _util import REL_TOL, bit_equal, golden_names, load, norm_rel
 from oracle import oracle, torch_ops
 
-BUILD_CASES = [n for n in golden_names() if not n.startswith(("g_bwd", "g_dsec", "g_e2e"))]
+BUILD_CASES = [n for n in golden_names() if not n.startswith(("g_bwd", "g_dsec", "g_e2e", "g_splat"))]
 
 
 def _inputs(meta):
@@ -129,3 +129,15 @@ def test_oracle_grad_matches_finite_difference():
     fd = (J(f1 + eps * v1, f2 + eps * v2) - J(f1 - eps * v1, f2 - eps * v2)) / (2 * eps)
     an = float((df1.astype(np.float64) * v1).sum() + (df2.astype(np.float64) * v2).sum())
     assert abs(fd - an) <= 2e-2 * max(1.0, abs(an))
+
+
+def test_oracle_forward_splat_matches_reference_golden():
+    """Warm-start splat (utils/image_utils.py:52-83) restated in C: bit-identical to the
+    reference on the splat fixtures (fractional, integer, far-out and colliding flows) and on
+    the E2E golden's own flow_init = forward_interpolate_pytorch(cold low-res flow)."""
+    from oracle import oracle
+    g = load("g_splat")
+    for t in "ab":
+        assert bit_equal(oracle.forward_splat(g[f"flow_{t}"]), g[f"splat_{t}"]), t
+    e = load("g_e2e_dsec")
+    assert bit_equal(oracle.forward_splat(e["low"]), e["flow_init"])

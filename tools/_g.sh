@@ -1,4 +1,3 @@
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gt.log 2>&1; rc=$?; tail -25 gpurun_out/gt.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python bench.py --workload train --steps 20 --no-cpu-baseline > gpurun_out/bt.json && python3 -c "import json; d=json.load(open('gpurun_out/bt.json')); print(d['value'], d['step_gpu_us'], d['backward'])"
