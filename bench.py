@@ -175,7 +175,8 @@ def cpu_baseline(workload, budget_s, train=False):
 def run_e2e(args, world, rank, dev):
     """BASELINE config 2: full E-RAFT forward (encoders on MIOpen, the HIP CorrBlock, 12 GRU
     iterations, convex upsampling) on 15-bin voxel pairs at 480x640, warm start (flow_init at
-    1/8 resolution), random-init weights.  One step = one frame pair, eager launches."""
+    1/8 resolution), random-init weights.  One step = one frame pair, replayed from one HIP
+    graph (--eager: launched op by op)."""
     from eraft_amd.model import ERAFT
     torch.manual_seed(0)
     bins, H, W, iters = 15, 480, 640, 12
@@ -188,16 +189,38 @@ def run_e2e(args, world, rank, dev):
 
     im1, im2 = voxels(), voxels()
     finit = 2.0 * torch.randn(1, 2, H // 8, W // 8, device=dev, generator=g)
+    launch = "eager"
     with torch.no_grad():
         for _ in range(args.warmup):
             model(im1, im2, iters=iters, flow_init=finit)
+        torch.cuda.synchronize()
+        step = lambda: model(im1, im2, iters=iters, flow_init=finit)  # noqa: E731
+        if not args.eager:
+            # the whole forward (MIOpen convs, GRU elementwise ops, the HIP CorrBlock) as ONE
+            # HIP graph: the GRU loop is otherwise bound by ~70 launches per iteration
+            try:
+                s = torch.cuda.Stream(device=dev)
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    step()
+                torch.cuda.current_stream().wait_stream(s)
+                gph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gph):
+                    step()
+                gph.replay()
+                torch.cuda.synchronize()
+                step, launch = gph.replay, "hipgraph"
+            except Exception as exc:  # noqa: BLE001 — report and stay eager
+                print(f"e2e: graph capture failed ({exc}); eager", file=sys.stderr)
+        for _ in range(2):
+            step()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            model(im1, im2, iters=iters, flow_init=finit)
+            step()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
     elapsed = t1 - t0
@@ -213,7 +236,7 @@ def run_e2e(args, world, rank, dev):
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic 15-bin voxel grids (15% nonzero, randn), random-init weights",
         "config": {"workload": "E-RAFT forward, DSEC 480x640 warm start, 12 GRU iters, HIP CorrBlock",
-                   "global_batch": world, "launch": "eager",
+                   "global_batch": world, "launch": launch,
                    "parallelism": f"replicas x{world}"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
