@@ -236,6 +236,17 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
                       fn);
 }
 
+int corr_convex_upsample(const float *flow, const float *mask, int N, int h, int w, float *out, void *stream) {
+    static const char *fn = "corr_convex_upsample";
+    g_err[0] = 0;
+    if (N < 1 || h < 1 || w < 1)
+        return fail(CORR_EINVAL, "%s: N, h, w must be >= 1 (got %d, %d, %d)", fn, N, h, w);
+    int rc;
+    if ((rc = check_ptr(fn, flow, "flow")) || (rc = check_ptr(fn, mask, "mask")) || (rc = check_ptr(fn, out, "out")))
+        return rc;
+    return hip_status(launch_convex_upsample(flow, mask, N, h, w, out, (hipStream_t)stream), fn);
+}
+
 size_t corr_forward_splat_workspace(int B, int H, int W) {
     if (B < 1 || H < 1 || W < 1) return 0;
     return splat_workspace(B, H, W);

@@ -45,6 +45,8 @@ hipError_t launch_build_split(const float *f1, int NQ, const float *f2, int B, i
 size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W);
 hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, const float *f2, int B, int D, int H,
                                   int W, float *df1, float *df2, void *ws, hipStream_t s);
+hipError_t launch_convex_upsample(const float *flow, const float *mask, int N, int h, int w, float *out,
+                                  hipStream_t s);
 size_t splat_workspace(int B, int H, int W);
 hipError_t launch_forward_splat(const float *flow, int B, int H, int W, float *out, void *ws, hipStream_t s);
 size_t build_bwd_workspace(int B, int D, int NQ, int H, int W);

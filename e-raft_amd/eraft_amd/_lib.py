@@ -26,7 +26,7 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
            "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows_workspace",
            "corr_build_bwd_rows", "corr_build_workspace", "corr_build_ex",
            "corr_build_bwd_ex_workspace", "corr_build_bwd_ex", "corr_forward_splat_workspace",
-           "corr_forward_splat")
+           "corr_forward_splat", "corr_convex_upsample")
 
 # Build algorithms (include/corr_mi355x.h).  F16X3 is the default: fp32 features split into
 # f16 hi/lo pairs, three f16 MFMAs per product, fp32 accumulate (~1e-6 of max|C| from the
@@ -90,9 +90,11 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.corr_forward_splat_workspace.argtypes = [i, i, i]
     lib.corr_forward_splat_workspace.restype = sz
     lib.corr_forward_splat.argtypes = [vp, i, i, i, vp, vp, sz, vp]
+    lib.corr_convex_upsample.argtypes = [vp, vp, i, i, i, vp, vp]
     for f in ("corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd",
               "corr_build_rows", "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows",
-              "corr_build_ex", "corr_build_bwd_ex", "corr_forward_splat"):
+              "corr_build_ex", "corr_build_bwd_ex", "corr_forward_splat",
+              "corr_convex_upsample"):
         getattr(lib, f).restype = i
     if path is None:
         _lib = lib
@@ -226,3 +228,14 @@ def forward_splat(flow, out):
     ws = torch.empty(max(1, (n + 3) // 4), dtype=torch.int32, device=flow.device)
     with torch.cuda.device(flow.device):
         _check(lib.corr_forward_splat(f, B, H, W, o, ws.data_ptr(), ws.numel() * 4, _stream(flow)))
+
+
+def convex_upsample(flow, mask, out):
+    """corr_convex_upsample: flow [N, 2, h, w], mask [N, 576, h, w] -> out [N, 2, 8h, 8w]."""
+    N, C, h, w = flow.shape
+    if C != 2 or tuple(mask.shape) != (N, 576, h, w) or tuple(out.shape) != (N, 2, 8 * h, 8 * w):
+        raise ValueError(f"convex_upsample: flow {tuple(flow.shape)}, mask {tuple(mask.shape)}, "
+                         f"out {tuple(out.shape)}")
+    f, m, o = _dev(flow, "flow"), _dev(mask, "mask"), _dev(out, "out")
+    with torch.cuda.device(flow.device):
+        _check(load().corr_convex_upsample(f, m, N, h, w, o, _stream(flow)))

@@ -209,7 +209,15 @@ class ERAFT(nn.Module):
 
     @staticmethod
     def upsample_flow(flow, mask):
-        """Convex combination of 3x3 neighbours, x8 (eraft.py:75-86)."""
+        """Convex combination of 3x3 neighbours, x8 (eraft.py:75-86).  Inference runs the
+        one-pass HIP kernel (corr_convex_upsample); under autograd (training) the torch
+        composition below keeps the gradient (it is also what bench.py's CPU baseline runs)."""
+        if flow.is_cuda and not (torch.is_grad_enabled() and (flow.requires_grad or mask.requires_grad)):
+            from . import _lib
+            n, _, h, w = flow.shape
+            out = torch.empty((n, 2, 8 * h, 8 * w), dtype=torch.float32, device=flow.device)
+            _lib.convex_upsample(flow.float().contiguous(), mask.float().contiguous(), out)
+            return out
         n, _, h, w = flow.shape
         mask = torch.softmax(mask.view(n, 1, 9, 8, 8, h, w), dim=2)
         up = F.unfold(8 * flow, [3, 3], padding=1).view(n, 2, 9, 1, 1, h, w)

@@ -170,6 +170,16 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
  * in the reference).  Workspace: corr_forward_splat_workspace(B, H, W) bytes.
  */
 size_t corr_forward_splat_workspace(int B, int H, int W);
+
+/*
+ * Convex upsampling of the 1/8-resolution flow after every GRU iteration.  Replaces
+ * ERAFT.upsample_flow (model/eraft.py:75-86): softmax over the 9 taps of mask
+ * [N][9*64][h][w], weighted sum of the zero-padded 3x3 neighbourhood of 8*flow [N][2][h][w]
+ * -> out [N][2][8h][8w], in one pass (fp32; tolerance-level parity, the reference's
+ * reduction order is ATen's).
+ */
+int corr_convex_upsample(const float *flow, const float *mask, int N, int h, int w, float *out,
+                         void *stream);
 int corr_forward_splat(const float *flow, int B, int H, int W, float *out, void *workspace,
                        size_t workspace_bytes, void *stream);
 

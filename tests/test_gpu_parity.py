@@ -337,3 +337,22 @@ def test_forward_splat_bitexact_vs_oracle(B, H, W, sigma):
     out = forward_interpolate_pytorch(t).cpu().numpy()
     assert bit_equal(out, oracle.forward_splat(f))
     assert bit_equal(forward_interpolate_pytorch(t).cpu().numpy(), out)
+
+
+@pytest.mark.parametrize("N,h,w,scale", [(1, 60, 80, 1.0), (2, 7, 9, 30.0)])
+def test_convex_upsample_vs_reference_formula(N, h, w, scale):
+    """corr_convex_upsample vs the reference's upsample_flow composition (eraft.py:75-86)
+    evaluated in float64 on the host: |diff| <= 1e-5 of max|out| (large logits: softmax
+    saturation)."""
+    import torch.nn.functional as F
+    from eraft_amd import _lib
+    flow = prng.gauss(51, (N, 2, h, w), 3.0)
+    mask = prng.gauss(52, (N, 576, h, w), scale)
+    f64, m64 = torch.from_numpy(flow).double(), torch.from_numpy(mask).double()
+    m = torch.softmax(m64.view(N, 1, 9, 8, 8, h, w), dim=2)
+    up = F.unfold(8 * f64, [3, 3], padding=1).view(N, 2, 9, 1, 1, h, w)
+    ref = torch.sum(m * up, dim=2).permute(0, 1, 4, 2, 5, 3).reshape(N, 2, 8 * h, 8 * w).numpy()
+    out = torch.empty(N, 2, 8 * h, 8 * w, device=DEV)
+    _lib.convex_upsample(torch.from_numpy(flow).to(DEV), torch.from_numpy(mask).to(DEV), out)
+    o = out.cpu().numpy()
+    assert np.abs(o - ref).max() <= 1e-5 * np.abs(ref).max()
