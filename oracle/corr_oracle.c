@@ -300,3 +300,52 @@ void oracle_forward_splat(const float *flow, int B, int H, int W, float *out) {
     free(val);
     free(acc);
 }
+
+/*
+ * DSEC event -> voxel grid, utils/dsec_utils.py:26-64 (VoxelGrid.convert), events as
+ * loader/loader_dsec.py:245-257 prepares them (float32 x, y, t in [0, 1], p in {0, 1}):
+ *   t_n = ((C-1) * (t - t[0])) / (t[M-1] - t[0]) (:33); x0, y0, t0 = trunc(x, y, t_n) (:35-37);
+ *   value = 2p - 1 (:39); corners x_l in (x0, x0+1) outer, y_l in (y0, y0+1) inner, t_l = t0
+ *   (:41-44, the t loop is commented out in the reference); in-bounds corners (:45) add
+ *   ((value * (1-|x_l-x|)) * (1-|y_l-y|)) * (1-|t_l-t_n|) (:46) at H*W*t_l + W*y_l + x_l with
+ *   put_(accumulate=True) (:52) — sequential per corner pass, in event order.
+ *   normalize (:54-62): over the nonzero cells, v = (v - mean) / std (unbiased std; when
+ *   std is not > 0: v - mean).  mean and std are accumulated in fp64 here and rounded to
+ *   fp32 (the reference's fp32 reduction order is ATen's: tolerance-level for this step).
+ */
+void oracle_voxel_grid(const float *x, const float *y, const float *t, const float *p, long M, int C, int H,
+                       int W, int normalize, float *out) {
+    const long CHW = (long)C * H * W;
+    memset(out, 0, sizeof(float) * CHW);
+    if (M < 1) return;
+    const float t0 = t[0], dt = t[M - 1] - t[0];
+    for (int xi = 0; xi < 2; ++xi)
+        for (int yi = 0; yi < 2; ++yi)
+            for (long e = 0; e < M; ++e) {
+                const float tn = ((float)(C - 1) * (t[e] - t0)) / dt;
+                const int xl = (int)x[e] + xi, yl = (int)y[e] + yi, tl = (int)tn;
+                if (!(xl < W && xl >= 0 && yl < H && yl >= 0 && tl >= 0 && tl < C)) continue;
+                const float value = 2.0f * p[e] - 1.0f;
+                const float w = value * (1.0f - fabsf((float)xl - x[e])) * (1.0f - fabsf((float)yl - y[e])) *
+                                (1.0f - fabsf((float)tl - tn));
+                const long idx = (long)H * W * tl + (long)W * yl + xl;
+                out[idx] = out[idx] + w;
+            }
+    if (!normalize) return;
+    long n = 0;
+    double s = 0.0;
+    for (long i = 0; i < CHW; ++i)
+        if (out[i] != 0.0f) {
+            s += out[i];
+            ++n;
+        }
+    if (n == 0) return;
+    const double mean = s / (double)n;
+    double q = 0.0;
+    for (long i = 0; i < CHW; ++i)
+        if (out[i] != 0.0f) q += ((double)out[i] - mean) * ((double)out[i] - mean);
+    const float mf = (float)mean;
+    const float sf = n > 1 ? (float)sqrt(q / (double)(n - 1)) : NAN;
+    for (long i = 0; i < CHW; ++i)
+        if (out[i] != 0.0f) out[i] = sf > 0.0f ? (out[i] - mf) / sf : out[i] - mf;
+}

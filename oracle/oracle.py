@@ -48,8 +48,10 @@ def _load():
         lib.oracle_pool_bwd.argtypes = [vp, l, i, i, i]
         lib.oracle_corr_bwd.argtypes = [vp, vp, vp, i, i, i, vp, vp]
         lib.oracle_forward_splat.argtypes = [vp, i, i, i, vp]
+        lib.oracle_voxel_grid.argtypes = [vp, vp, vp, vp, l, i, i, i, i, vp]
         for f in ("oracle_corr_rows", "oracle_avg_pool2x2", "oracle_lookup",
-                  "oracle_lookup_bwd", "oracle_pool_bwd", "oracle_corr_bwd", "oracle_forward_splat"):
+                  "oracle_lookup_bwd", "oracle_pool_bwd", "oracle_corr_bwd", "oracle_forward_splat",
+                  "oracle_voxel_grid"):
             getattr(lib, f).restype = None
         _lib = lib
     return _lib
@@ -173,4 +175,14 @@ def forward_splat(flow) -> np.ndarray:
     B, _, H, W = flow.shape
     out = np.empty_like(flow)
     _load().oracle_forward_splat(_p(flow), B, H, W, _p(out))
+    return out
+
+
+def voxel_grid(ev, C, H, W, normalize) -> np.ndarray:
+    """utils/dsec_utils.py:26-64 VoxelGrid.convert: ev = [4, M] rows x, y, t, p -> [C, H, W]."""
+    ev = _c(ev)
+    M = ev.shape[1]
+    out = np.empty((C, H, W), np.float32)
+    rows = [np.ascontiguousarray(ev[k]) for k in range(4)]
+    _load().oracle_voxel_grid(*[_p(r) for r in rows], M, C, H, W, int(bool(normalize)), _p(out))
     return out

@@ -151,7 +151,38 @@ def case_splat(name, seed):
     save(name, **out)
 
 
+def case_voxel(name, seed):
+    """DSEC event -> voxel grid (utils/dsec_utils.py:19-64 VoxelGrid.convert, normalize=True
+    and False) on events shaped as loader_dsec.py:245-257 makes them: float32 rectified x, y
+    (fractional, some out of the frame), t normalised to [0, 1], p in {0, 1}; repeated pixels
+    collide.  Inputs from prng; outputs from the reference, run single-threaded as its own
+    entry point pins it (main.py:2-5): put_(accumulate=True) on CPU is chunked over threads,
+    so its summation order (and the low bits) depend on the thread count; one thread = the
+    sequential event order."""
+    from utils.dsec_utils import VoxelGrid
+    torch.set_num_threads(1)
+    out = {}
+    for tag, M, C, H, W in (("a", 3000, 5, 12, 16), ("b", 40000, 15, 48, 64)):
+        u = prng.uniform(seed, (4, M))
+        x = (u[0] * (W + 2) - 1.0).astype(np.float32)
+        y = (u[1] * (H + 2) - 1.0).astype(np.float32)
+        x[::7] = np.floor(x[::7])                       # integer coordinates
+        t = np.sort(u[2]).astype(np.float32)
+        t = (t - t[0]) / (t[-1] - t[0])
+        p = (u[3] > 0.5).astype(np.float32)
+        ev = {k: torch.from_numpy(v.copy()) for k, v in (("x", x), ("y", y), ("t", t), ("p", p))}
+        out[f"ev_{tag}"] = np.stack([x, y, t, p])
+        out[f"meta_{tag}"] = np.array([M, C, H, W], np.int64)
+        out[f"raw_{tag}"] = VoxelGrid((C, H, W), normalize=False).convert(ev).numpy()
+        out[f"norm_{tag}"] = VoxelGrid((C, H, W), normalize=True).convert(ev).numpy()
+        seed += 1
+    save(name, **out)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "voxel":
+        case_voxel("g_voxel", 41)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "splat":
         case_splat("g_splat", 31)
         sys.exit(0)

@@ -11,7 +11,7 @@ import prng
 from _util import REL_TOL, bit_equal, golden_names, load, norm_rel
 from oracle import oracle, torch_ops
 
-BUILD_CASES = [n for n in golden_names() if not n.startswith(("g_bwd", "g_dsec", "g_e2e", "g_splat"))]
+BUILD_CASES = [n for n in golden_names() if not n.startswith(("g_bwd", "g_dsec", "g_e2e", "g_splat", "g_voxel"))]
 
 
 def _inputs(meta):
@@ -141,3 +141,16 @@ def test_oracle_forward_splat_matches_reference_golden():
         assert bit_equal(oracle.forward_splat(g[f"flow_{t}"]), g[f"splat_{t}"]), t
     e = load("g_e2e_dsec")
     assert bit_equal(oracle.forward_splat(e["low"]), e["flow_init"])
+
+
+def test_oracle_voxel_grid_matches_reference_golden():
+    """DSEC event -> voxel grid (utils/dsec_utils.py:26-64) restated in C: the raw grid is
+    bit-identical to the reference (single-threaded, as main.py:2-5 runs it); the normalised
+    grid is within 1e-6 of max|v| (mean / std reductions: fp64 here, ATen's order there)."""
+    from oracle import oracle
+    g = load("g_voxel")
+    for t in "ab":
+        M, C, H, W = (int(v) for v in g[f"meta_{t}"])
+        assert bit_equal(oracle.voxel_grid(g[f"ev_{t}"], C, H, W, False), g[f"raw_{t}"]), t
+        n, ref = oracle.voxel_grid(g[f"ev_{t}"], C, H, W, True), g[f"norm_{t}"]
+        assert np.abs(n - ref).max() <= 1e-6 * np.abs(ref).max(), t
