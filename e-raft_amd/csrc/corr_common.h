@@ -48,6 +48,9 @@ hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, 
 hipError_t launch_convex_upsample(const float *flow, const float *mask, int N, int h, int w, float *out,
                                   hipStream_t s);
 size_t splat_workspace(int B, int H, int W);
+size_t voxel_workspace(int M, int C, int H, int W);
+hipError_t launch_voxel_grid(const float *x, const float *y, const float *t, const float *p, int M, int C, int H,
+                             int W, int normalize, float *out, void *ws, hipStream_t s);
 hipError_t launch_forward_splat(const float *flow, int B, int H, int W, float *out, void *ws, hipStream_t s);
 size_t build_bwd_workspace(int B, int D, int NQ, int H, int W);
 hipError_t launch_build_bwd(const float *grad_c, const float *f1, int NQ, const float *f2, int B,

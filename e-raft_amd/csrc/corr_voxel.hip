@@ -1,0 +1,201 @@
+// corr_voxel.hip — the DSEC event -> voxel-grid representation, the producer of every frame
+// pair's network input (utils/dsec_utils.py:26-64 VoxelGrid.convert, called by
+// loader/loader_dsec.py:245-257 on the host CPU in the reference).
+//
+// Each event e (float32 x, y, t in [0, 1], p in {0, 1}) votes into C temporal bins:
+//   t_n = ((C-1)(t - t_0)) / (t_{M-1} - t_0); corners (x_l, y_l) in {x0, x0+1} x {y0, y0+1}
+//   (x0 = trunc x), t_l = trunc t_n; weight ((2p-1)(1-|x_l-x|))(1-|y_l-y|))(1-|t_l-t_n|);
+//   in-bounds corners accumulate at H*W*t_l + W*y_l + x_l.
+// The reference accumulates with put_(accumulate=True) — single-threaded (main.py:2-5 pins one
+// thread) that is a sequential pass per corner in event order.  As in corr_splat.hip the
+// accumulation is made deterministic and order-exact without float atomics: count entries per
+// cell, scan, bucket the entry indices, then each cell sums its bucket in ascending entry
+// order (entry = corner * M + event).  Buckets here can be long (many events on one pixel), so
+// a bucket is sorted in place first (insertion sort; typical sizes are a few to tens).
+// Optional normalisation (:54-62) over the nonzero cells: one workgroup reduces count, sum and
+// sum of squared deviations in fp64 (fixed partition + tree: deterministic), then
+// v = (v - mean) / std in fp32 (std unbiased; v - mean when std is not > 0).
+#include <cmath>
+
+#include "corr_common.h"
+
+namespace corr {
+namespace {
+
+struct VoxEntry {
+    float w;
+    int cell;  // -1: out of bounds
+};
+
+struct VoxArgs {
+    const float *x, *y, *t, *p;
+    int M, C, H, W;
+};
+
+__device__ __forceinline__ VoxEntry vox_entry(const VoxArgs &a, int e) {
+    const int corner = e / a.M, i = e - corner * a.M;
+    const float t0 = a.t[0], dt = __fsub_rn(a.t[a.M - 1], t0);
+    const float tn = __fdiv_rn(__fmul_rn((float)(a.C - 1), __fsub_rn(a.t[i], t0)), dt);
+    const float xf = a.x[i], yf = a.y[i];
+    const int xl = (int)xf + (corner >> 1), yl = (int)yf + (corner & 1), tl = (int)tn;
+    VoxEntry r;
+    const bool in = xl < a.W && xl >= 0 && yl < a.H && yl >= 0 && tl >= 0 && tl < a.C;
+    r.cell = in ? (tl * a.H + yl) * a.W + xl : -1;
+    const float value = __fsub_rn(__fmul_rn(2.0f, a.p[i]), 1.0f);
+    float w = __fmul_rn(value, __fsub_rn(1.0f, fabsf(__fsub_rn((float)xl, xf))));
+    w = __fmul_rn(w, __fsub_rn(1.0f, fabsf(__fsub_rn((float)yl, yf))));
+    r.w = __fmul_rn(w, __fsub_rn(1.0f, fabsf(__fsub_rn((float)tl, tn))));
+    return r;
+}
+
+__global__ __launch_bounds__(256) void vox_count_kernel(VoxArgs a, int *__restrict__ cnt) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= 4 * a.M) return;
+    const VoxEntry v = vox_entry(a, e);
+    if (v.cell >= 0) atomicAdd(&cnt[v.cell], 1);
+}
+
+// Exclusive scan of n counts, one 1024-thread workgroup.
+__global__ __launch_bounds__(1024) void vox_scan_kernel(const int *__restrict__ cnt, int n, int *__restrict__ off) {
+    __shared__ int part[1024];
+    const int tid = threadIdx.x;
+    const int per = (n + 1023) / 1024;
+    const int lo = min(n, tid * per), hi = min(n, lo + per);
+    int s = 0;
+    for (int i = lo; i < hi; ++i) s += cnt[i];
+    part[tid] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int v = tid >= d ? part[tid - d] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int run = tid ? part[tid - 1] : 0;
+    for (int i = lo; i < hi; ++i) {
+        off[i] = run;
+        run += cnt[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void vox_fill_kernel(VoxArgs a, const int *__restrict__ off, int *__restrict__ fill,
+                                                       int *__restrict__ ent) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= 4 * a.M) return;
+    const VoxEntry v = vox_entry(a, e);
+    if (v.cell >= 0) ent[off[v.cell] + atomicAdd(&fill[v.cell], 1)] = e;
+}
+
+// One thread per cell: sort its bucket (ascending entry index = the reference's order), sum.
+__global__ __launch_bounds__(256) void vox_gather_kernel(VoxArgs a, const int *__restrict__ cnt,
+                                                         const int *__restrict__ off, int *__restrict__ ent,
+                                                         float *__restrict__ out) {
+    const int n = a.C * a.H * a.W;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= n) return;
+    const int k = cnt[c];
+    int *b = ent + off[c];
+    for (int i = 1; i < k; ++i) {  // insertion sort, in place (the bucket is this thread's)
+        const int v = b[i];
+        int j = i - 1;
+        while (j >= 0 && b[j] > v) {
+            b[j + 1] = b[j];
+            --j;
+        }
+        b[j + 1] = v;
+    }
+    float s = 0.0f;
+    for (int i = 0; i < k; ++i) s = __fadd_rn(s, vox_entry(a, b[i]).w);
+    out[c] = s;
+}
+
+// Normalisation statistics over the nonzero cells (one workgroup, fp64, deterministic):
+// st[0] = mean, st[1] = std (fp32-rounded), st[2] = count.
+__global__ __launch_bounds__(1024) void vox_stats_kernel(const float *__restrict__ v, int n, float *__restrict__ st) {
+    __shared__ double rs[1024];
+    __shared__ long long rc[1024];
+    const int tid = threadIdx.x;
+    double s = 0.0;
+    long long c = 0;
+    for (int i = tid; i < n; i += 1024)
+        if (v[i] != 0.0f) {
+            s += v[i];
+            ++c;
+        }
+    rs[tid] = s;
+    rc[tid] = c;
+    __syncthreads();
+    for (int d = 512; d >= 1; d >>= 1) {
+        if (tid < d) {
+            rs[tid] += rs[tid + d];
+            rc[tid] += rc[tid + d];
+        }
+        __syncthreads();
+    }
+    const long long cnt = rc[0];
+    const double mean = cnt ? rs[0] / (double)cnt : 0.0;
+    __syncthreads();
+    double q = 0.0;
+    for (int i = tid; i < n; i += 1024)
+        if (v[i] != 0.0f) q += ((double)v[i] - mean) * ((double)v[i] - mean);
+    rs[tid] = q;
+    __syncthreads();
+    for (int d = 512; d >= 1; d >>= 1) {
+        if (tid < d) rs[tid] += rs[tid + d];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        st[0] = (float)mean;
+        st[1] = cnt > 1 ? (float)sqrt(rs[0] / (double)(cnt - 1)) : __int_as_float(0x7fc00000);
+        st[2] = (float)cnt;
+    }
+}
+
+__global__ __launch_bounds__(256) void vox_normalize_kernel(float *__restrict__ v, int n, const float *__restrict__ st) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float x = v[i];
+    if (x == 0.0f) return;
+    const float mean = st[0], sd = st[1];
+    v[i] = sd > 0.0f ? __fdiv_rn(__fsub_rn(x, mean), sd) : __fsub_rn(x, mean);
+}
+
+inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace
+
+// cnt [CHW] | off [CHW] | fill [CHW] | ent [4M] | stats [4] (int32 / float)
+size_t voxel_workspace(int M, int C, int H, int W) {
+    const size_t n = (size_t)C * H * W;
+    return 3 * al256(n * 4) + al256((size_t)4 * M * 4) + 256;
+}
+
+hipError_t launch_voxel_grid(const float *x, const float *y, const float *t, const float *p, int M, int C, int H,
+                             int W, int normalize, float *out, void *ws, hipStream_t s) {
+    const size_t n = (size_t)C * H * W;
+    char *w = (char *)ws;
+    int *cnt = (int *)w, *off = (int *)(w + al256(n * 4)), *fill = (int *)(w + 2 * al256(n * 4));
+    int *ent = (int *)(w + 3 * al256(n * 4));
+    float *st = (float *)(w + 3 * al256(n * 4) + al256((size_t)4 * M * 4));
+    hipError_t e = hipMemsetAsync(cnt, 0, n * 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(fill, 0, n * 4, s);
+    if (e != hipSuccess) return e;
+    VoxArgs a{x, y, t, p, M, C, H, W};
+    const unsigned ge = (unsigned)((4 * (size_t)M + 255) / 256), gc = (unsigned)((n + 255) / 256);
+    if (M > 0) {
+        hipLaunchKernelGGL(vox_count_kernel, dim3(ge), dim3(256), 0, s, a, cnt);
+        hipLaunchKernelGGL(vox_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, (int)n, off);
+        hipLaunchKernelGGL(vox_fill_kernel, dim3(ge), dim3(256), 0, s, a, off, fill, ent);
+    } else {
+        e = hipMemsetAsync(off, 0, n * 4, s);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(vox_gather_kernel, dim3(gc), dim3(256), 0, s, a, cnt, off, ent, out);
+    if (normalize) {
+        hipLaunchKernelGGL(vox_stats_kernel, dim3(1), dim3(1024), 0, s, out, (int)n, st);
+        hipLaunchKernelGGL(vox_normalize_kernel, dim3(gc), dim3(256), 0, s, out, (int)n, st);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace corr

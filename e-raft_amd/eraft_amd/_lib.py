@@ -26,7 +26,8 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
            "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows_workspace",
            "corr_build_bwd_rows", "corr_build_workspace", "corr_build_ex",
            "corr_build_bwd_ex_workspace", "corr_build_bwd_ex", "corr_forward_splat_workspace",
-           "corr_forward_splat", "corr_convex_upsample")
+           "corr_forward_splat", "corr_convex_upsample", "corr_voxel_grid_workspace",
+           "corr_voxel_grid")
 
 # Build algorithms (include/corr_mi355x.h).  F16X3 is the default: fp32 features split into
 # f16 hi/lo pairs, three f16 MFMAs per product, fp32 accumulate (~1e-6 of max|C| from the
@@ -91,10 +92,13 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.corr_forward_splat_workspace.restype = sz
     lib.corr_forward_splat.argtypes = [vp, i, i, i, vp, vp, sz, vp]
     lib.corr_convex_upsample.argtypes = [vp, vp, i, i, i, vp, vp]
+    lib.corr_voxel_grid_workspace.argtypes = [i, i, i, i]
+    lib.corr_voxel_grid_workspace.restype = sz
+    lib.corr_voxel_grid.argtypes = [vp, vp, vp, vp, i, i, i, i, i, vp, vp, sz, vp]
     for f in ("corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd",
               "corr_build_rows", "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows",
               "corr_build_ex", "corr_build_bwd_ex", "corr_forward_splat",
-              "corr_convex_upsample"):
+              "corr_convex_upsample", "corr_voxel_grid"):
         getattr(lib, f).restype = i
     if path is None:
         _lib = lib
@@ -239,3 +243,20 @@ def convex_upsample(flow, mask, out):
     f, m, o = _dev(flow, "flow"), _dev(mask, "mask"), _dev(out, "out")
     with torch.cuda.device(flow.device):
         _check(load().corr_convex_upsample(f, m, N, h, w, o, _stream(flow)))
+
+
+def voxel_grid(x, y, t, p, out, normalize):
+    """corr_voxel_grid: float32 device event arrays (x, y, t, p) -> out [C, H, W]."""
+    C, H, W = out.shape
+    M = x.numel()
+    for v, nm in ((y, "y"), (t, "t"), (p, "p")):
+        if v.numel() != M:
+            raise ValueError(f"{nm} has {v.numel()} events, x has {M}")
+    ptrs = [_dev(v, nm) if M else 0 for v, nm in ((x, "x"), (y, "y"), (t, "t"), (p, "p"))]
+    o = _dev(out, "out")
+    lib = load()
+    n = lib.corr_voxel_grid_workspace(M, C, H, W)
+    ws = torch.empty(max(1, (n + 3) // 4), dtype=torch.int32, device=out.device)
+    with torch.cuda.device(out.device):
+        _check(lib.corr_voxel_grid(*ptrs, M, C, H, W, int(bool(normalize)), o, ws.data_ptr(), ws.numel() * 4,
+                                   _stream(out)))

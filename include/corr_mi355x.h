@@ -172,6 +172,20 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
 size_t corr_forward_splat_workspace(int B, int H, int W);
 
 /*
+ * DSEC event -> voxel grid.  Replaces VoxelGrid.convert (utils/dsec_utils.py:26-64) as the DSEC
+ * loader calls it (loader/loader_dsec.py:245-257): events as float32 device arrays x, y, t
+ * (t in [0, 1], ascending), p in {0, 1}; out [C][H][W].  Bilinear in x and y, nearest-lower
+ * bin in t (the reference's t loop is commented out); the raw grid is bit-identical to the
+ * reference run single-threaded (main.py:2-5) — deterministic, no float atomics.  normalize:
+ * nonzero cells -> (v - mean) / std (unbiased std; fp64 statistics, tolerance-level).
+ * Workspace: corr_voxel_grid_workspace(n_events, C, H, W) bytes.
+ */
+size_t corr_voxel_grid_workspace(int n_events, int C, int H, int W);
+int corr_voxel_grid(const float *x, const float *y, const float *t, const float *p, int n_events,
+                    int C, int H, int W, int normalize, float *out, void *workspace,
+                    size_t workspace_bytes, void *stream);
+
+/*
  * Convex upsampling of the 1/8-resolution flow after every GRU iteration.  Replaces
  * ERAFT.upsample_flow (model/eraft.py:75-86): softmax over the 9 taps of mask
  * [N][9*64][h][w], weighted sum of the zero-padded 3x3 neighbourhood of 8*flow [N][2][h][w]
