@@ -12,8 +12,8 @@
 // cell, scan, bucket the entry indices, then each cell sums its bucket in ascending entry
 // order (entry = corner * M + event).  Buckets here can be long (many events on one pixel), so
 // a bucket is sorted in place first (insertion sort; typical sizes are a few to tens).
-// Optional normalisation (:54-62) over the nonzero cells: one workgroup reduces count, sum and
-// sum of squared deviations in fp64 (fixed partition + tree: deterministic), then
+// Optional normalisation (:54-62) over the nonzero cells: count, sum and sum of squared
+// deviations in fp64 (fixed partitions over 512 workgroups + ordered tree: deterministic), then
 // v = (v - mean) / std in fp32 (std unbiased; v - mean when std is not > 0).
 #include <cmath>
 
@@ -55,26 +55,76 @@ __global__ __launch_bounds__(256) void vox_count_kernel(VoxArgs a, int *__restri
     if (v.cell >= 0) atomicAdd(&cnt[v.cell], 1);
 }
 
-// Exclusive scan of n counts, one 1024-thread workgroup.
-__global__ __launch_bounds__(1024) void vox_scan_kernel(const int *__restrict__ cnt, int n, int *__restrict__ off) {
+// Exclusive scan of n counts: tiles of kTile cells (1024 threads x 8 consecutive cells);
+// (1) tile sums, (2) one workgroup scans the tile sums, (3) each tile scans itself from its
+// offset.  Integer sums: any order is exact.
+constexpr int kTile = 8192;
+
+__global__ __launch_bounds__(1024) void vox_tile_sum_kernel(const int *__restrict__ cnt, int n, int *__restrict__ tsum) {
+    __shared__ int red[1024];
+    const int base = blockIdx.x * kTile, tid = threadIdx.x;
+    int s = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int i = base + j * 1024 + tid;
+        s += i < n ? cnt[i] : 0;
+    }
+    red[tid] = s;
+    __syncthreads();
+    for (int d = 512; d >= 1; d >>= 1) {
+        if (tid < d) red[tid] += red[tid + d];
+        __syncthreads();
+    }
+    if (tid == 0) tsum[blockIdx.x] = red[0];
+}
+
+// Exclusive scan of n (small) values in one workgroup.
+__global__ __launch_bounds__(1024) void vox_scan_small_kernel(int *__restrict__ v, int n) {
     __shared__ int part[1024];
     const int tid = threadIdx.x;
     const int per = (n + 1023) / 1024;
     const int lo = min(n, tid * per), hi = min(n, lo + per);
     int s = 0;
-    for (int i = lo; i < hi; ++i) s += cnt[i];
+    for (int i = lo; i < hi; ++i) s += v[i];
     part[tid] = s;
     __syncthreads();
     for (int d = 1; d < 1024; d <<= 1) {
-        const int v = tid >= d ? part[tid - d] : 0;
+        const int x = tid >= d ? part[tid - d] : 0;
         __syncthreads();
-        part[tid] += v;
+        part[tid] += x;
         __syncthreads();
     }
     int run = tid ? part[tid - 1] : 0;
     for (int i = lo; i < hi; ++i) {
-        off[i] = run;
-        run += cnt[i];
+        const int c = v[i];
+        v[i] = run;
+        run += c;
+    }
+}
+
+__global__ __launch_bounds__(1024) void vox_tile_scan_kernel(const int *__restrict__ cnt, int n,
+                                                             const int *__restrict__ toff, int *__restrict__ off) {
+    __shared__ int part[1024];
+    const int tid = threadIdx.x, base = blockIdx.x * kTile + tid * 8;
+    int c[8], s = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        c[j] = base + j < n ? cnt[base + j] : 0;
+        s += c[j];
+    }
+    part[tid] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int x = tid >= d ? part[tid - d] : 0;
+        __syncthreads();
+        part[tid] += x;
+        __syncthreads();
+    }
+    int run = toff[blockIdx.x] + (tid ? part[tid - 1] : 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (base + j < n) off[base + j] = run;
+        run += c[j];
     }
 }
 
@@ -109,45 +159,76 @@ __global__ __launch_bounds__(256) void vox_gather_kernel(VoxArgs a, const int *_
     out[c] = s;
 }
 
-// Normalisation statistics over the nonzero cells (one workgroup, fp64, deterministic):
-// st[0] = mean, st[1] = std (fp32-rounded), st[2] = count.
-__global__ __launch_bounds__(1024) void vox_stats_kernel(const float *__restrict__ v, int n, float *__restrict__ st) {
-    __shared__ double rs[1024];
-    __shared__ long long rc[1024];
+// Normalisation statistics over the nonzero cells, fp64, deterministic: kStatBlocks
+// workgroups reduce fixed grid-stride partitions (tree in LDS), one workgroup folds the
+// partials in block order.  pass 0: count and sum -> mean; pass 1: squared deviations -> std.
+// st: [0] mean, [1] std (fp32), [2] count; part: kStatBlocks x {sum, count}.
+constexpr int kStatBlocks = 512;
+
+__global__ __launch_bounds__(256) void vox_stat_partial_kernel(const float *__restrict__ v, int n, int pass,
+                                                               const float *__restrict__ st,
+                                                               double *__restrict__ part) {
+    __shared__ double rs[256];
+    __shared__ double rc[256];
     const int tid = threadIdx.x;
-    double s = 0.0;
-    long long c = 0;
-    for (int i = tid; i < n; i += 1024)
-        if (v[i] != 0.0f) {
-            s += v[i];
-            ++c;
+    const double mean64 = pass ? part[2 * kStatBlocks] : 0.0;  // pass 1: the fp64 mean
+    (void)st;
+    double s = 0.0, c = 0.0;
+    for (int i = blockIdx.x * 256 + tid; i < n; i += kStatBlocks * 256) {
+        const float x = v[i];
+        if (x != 0.0f) {
+            if (pass) {
+                const double d = (double)x - mean64;
+                s += d * d;
+            } else {
+                s += x;
+                c += 1.0;
+            }
         }
+    }
     rs[tid] = s;
     rc[tid] = c;
     __syncthreads();
-    for (int d = 512; d >= 1; d >>= 1) {
+    for (int d = 128; d >= 1; d >>= 1) {
         if (tid < d) {
             rs[tid] += rs[tid + d];
             rc[tid] += rc[tid + d];
         }
         __syncthreads();
     }
-    const long long cnt = rc[0];
-    const double mean = cnt ? rs[0] / (double)cnt : 0.0;
+    if (tid == 0) {
+        part[2 * blockIdx.x] = rs[0];
+        if (!pass) part[2 * blockIdx.x + 1] = rc[0];
+    }
+}
+
+__global__ __launch_bounds__(kStatBlocks) void vox_stat_final_kernel(double *__restrict__ part, int pass,
+                                                                     float *__restrict__ st) {
+    __shared__ double rs[kStatBlocks];
+    __shared__ double rc[kStatBlocks];
+    const int tid = threadIdx.x;
+    rs[tid] = part[2 * tid];
+    rc[tid] = part[2 * tid + 1];
     __syncthreads();
-    double q = 0.0;
-    for (int i = tid; i < n; i += 1024)
-        if (v[i] != 0.0f) q += ((double)v[i] - mean) * ((double)v[i] - mean);
-    rs[tid] = q;
-    __syncthreads();
-    for (int d = 512; d >= 1; d >>= 1) {
-        if (tid < d) rs[tid] += rs[tid + d];
+    for (int d = kStatBlocks / 2; d >= 1; d >>= 1) {
+        if (tid < d) {
+            rs[tid] += rs[tid + d];
+            if (!pass) rc[tid] += rc[tid + d];
+        }
         __syncthreads();
     }
     if (tid == 0) {
-        st[0] = (float)mean;
-        st[1] = cnt > 1 ? (float)sqrt(rs[0] / (double)(cnt - 1)) : __int_as_float(0x7fc00000);
-        st[2] = (float)cnt;
+        if (!pass) {
+            const double cnt = rc[0];
+            const double mean = cnt > 0 ? rs[0] / cnt : 0.0;
+            part[2 * kStatBlocks] = mean;      // fp64 mean for pass 1
+            part[2 * kStatBlocks + 1] = cnt;
+            st[0] = (float)mean;
+            st[2] = (float)cnt;
+        } else {
+            const double cnt = part[2 * kStatBlocks + 1];
+            st[1] = cnt > 1 ? (float)sqrt(rs[0] / (cnt - 1)) : __int_as_float(0x7fc00000);
+        }
     }
 }
 
@@ -164,10 +245,11 @@ inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
 
-// cnt [CHW] | off [CHW] | fill [CHW] | ent [4M] | stats [4] (int32 / float)
+// cnt [CHW] | off [CHW] | fill [CHW] | ent [4M] | tile sums | stats [4] float | partials (fp64)
 size_t voxel_workspace(int M, int C, int H, int W) {
-    const size_t n = (size_t)C * H * W;
-    return 3 * al256(n * 4) + al256((size_t)4 * M * 4) + 256;
+    const size_t n = (size_t)C * H * W, tiles = (n + kTile - 1) / kTile;
+    return 3 * al256(n * 4) + al256((size_t)4 * M * 4) + al256(tiles * 4) + 256 +
+           al256((2 * kStatBlocks + 2) * sizeof(double));
 }
 
 hipError_t launch_voxel_grid(const float *x, const float *y, const float *t, const float *p, int M, int C, int H,
@@ -176,7 +258,10 @@ hipError_t launch_voxel_grid(const float *x, const float *y, const float *t, con
     char *w = (char *)ws;
     int *cnt = (int *)w, *off = (int *)(w + al256(n * 4)), *fill = (int *)(w + 2 * al256(n * 4));
     int *ent = (int *)(w + 3 * al256(n * 4));
-    float *st = (float *)(w + 3 * al256(n * 4) + al256((size_t)4 * M * 4));
+    const size_t tiles = (n + kTile - 1) / kTile;
+    int *tsum = (int *)(w + 3 * al256(n * 4) + al256((size_t)4 * M * 4));
+    float *st = (float *)((char *)tsum + al256(tiles * 4));
+    double *part = (double *)((char *)st + 256);
     hipError_t e = hipMemsetAsync(cnt, 0, n * 4, s);
     if (e == hipSuccess) e = hipMemsetAsync(fill, 0, n * 4, s);
     if (e != hipSuccess) return e;
@@ -184,7 +269,9 @@ hipError_t launch_voxel_grid(const float *x, const float *y, const float *t, con
     const unsigned ge = (unsigned)((4 * (size_t)M + 255) / 256), gc = (unsigned)((n + 255) / 256);
     if (M > 0) {
         hipLaunchKernelGGL(vox_count_kernel, dim3(ge), dim3(256), 0, s, a, cnt);
-        hipLaunchKernelGGL(vox_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, (int)n, off);
+        hipLaunchKernelGGL(vox_tile_sum_kernel, dim3((unsigned)tiles), dim3(1024), 0, s, cnt, (int)n, tsum);
+        hipLaunchKernelGGL(vox_scan_small_kernel, dim3(1), dim3(1024), 0, s, tsum, (int)tiles);
+        hipLaunchKernelGGL(vox_tile_scan_kernel, dim3((unsigned)tiles), dim3(1024), 0, s, cnt, (int)n, tsum, off);
         hipLaunchKernelGGL(vox_fill_kernel, dim3(ge), dim3(256), 0, s, a, off, fill, ent);
     } else {
         e = hipMemsetAsync(off, 0, n * 4, s);
@@ -192,7 +279,10 @@ hipError_t launch_voxel_grid(const float *x, const float *y, const float *t, con
     }
     hipLaunchKernelGGL(vox_gather_kernel, dim3(gc), dim3(256), 0, s, a, cnt, off, ent, out);
     if (normalize) {
-        hipLaunchKernelGGL(vox_stats_kernel, dim3(1), dim3(1024), 0, s, out, (int)n, st);
+        for (int pass = 0; pass < 2; ++pass) {
+            hipLaunchKernelGGL(vox_stat_partial_kernel, dim3(kStatBlocks), dim3(256), 0, s, out, (int)n, pass, st, part);
+            hipLaunchKernelGGL(vox_stat_final_kernel, dim3(1), dim3(kStatBlocks), 0, s, part, pass, st);
+        }
         hipLaunchKernelGGL(vox_normalize_kernel, dim3(gc), dim3(256), 0, s, out, (int)n, st);
     }
     return hipGetLastError();
