@@ -236,6 +236,27 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
                       fn);
 }
 
+int corr_lookup_conv(const float *const *pyr, const float *coords, int B, int H, int W, int levels, int radius,
+                     const float *weight_t, const float *bias, int relu, float *out, void *stream) {
+    static const char *fn = "corr_lookup_conv";
+    g_err[0] = 0;
+    int rc = check_dims(fn, B, H * W, H, W, levels);
+    if (rc) return rc;
+    if (radius != 4) return fail(CORR_EUNSUPPORTED, "%s: built for radius 4 (got %d)", fn, radius);
+    if (!pyr) return fail(CORR_EINVAL, "%s: pyr is null", fn);
+    ConstLevelPtrs lp{};
+    for (int l = 0; l < levels; ++l) {
+        if ((rc = check_ptr(fn, pyr[l], "pyr[l]"))) return rc;
+        lp.p[l] = pyr[l];
+    }
+    if ((rc = check_ptr(fn, coords, "coords")) || (rc = check_ptr(fn, weight_t, "weight_t")) ||
+        (rc = check_ptr(fn, bias, "bias")) || (rc = check_ptr(fn, out, "out")))
+        return rc;
+    return hip_status(launch_lookup_conv(lp, coords, B, H * W, H, W, levels, radius, weight_t, bias, relu, out,
+                                         (hipStream_t)stream),
+                      fn);
+}
+
 int corr_convex_upsample(const float *flow, const float *mask, int N, int h, int w, float *out, void *stream) {
     static const char *fn = "corr_convex_upsample";
     g_err[0] = 0;

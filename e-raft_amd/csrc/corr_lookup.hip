@@ -40,6 +40,8 @@
 namespace corr {
 namespace {
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 constexpr int kQB = 64;  // queries per workgroup (one per lane)
 
 // Sentinel anchor for NaN / huge coordinates: every window cell is outside the map.
@@ -184,23 +186,19 @@ constexpr int lookup_threads(int S, int QB) { return (QB * S + 63) / 64 * 64; }
 
 // ABL: diagnostic ablations for tools/kbench_lookup.hip only (0 in the library): bit 0 = no
 // neighbourhood loads, bit 1 = no output stores, bit 2 = no coords load.
-template <int S, int QB, int ABL = 0>
-__global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
-    ConstLevelPtrs pyr, const float *__restrict__ coords, int B, int NQ, int H, int W, int L,
-    float *__restrict__ out) {
-    constexpr int R = (S - 1) / 2, K = S * S, NT = lookup_threads(S, QB);
+// One pyramid level of one block of QB queries (NT threads): the whole lookup of
+// lookup_kernel below.  emit(j, acc) receives output tap (i, j) of this thread's window column
+// i = tid / QB for query q = tid % QB (called only for live queries).  Shared by lookup_kernel
+// (global NCHW stores) and lookup_conv_kernel (LDS tile feeding the fused 1x1 convolution).
+template <int S, int QB, int NT, int ABL, class Emit>
+__device__ __forceinline__ void lookup_block(LookupSmem<S, QB> &sm, const float *__restrict__ P,
+                                             const float *__restrict__ coords, int b, int n0, int N,
+                                             int H, int W, int l, Emit emit) {
+    constexpr int R = (S - 1) / 2;
     using SM = LookupSmem<S, QB>;
     constexpr int WIN = SM::WIN, WSTR = SM::WSTR;
-    __shared__ SM sm;
-
-    const int N = NQ;  // query pixels per batch item (H*W, or a row slab of it)
-    const int nqb = (N + QB - 1) / QB;
-    const int b = blockIdx.x / nqb;
-    const int n0 = (blockIdx.x - b * nqb) * QB;
-    const int l = blockIdx.y;
     const int Hl = H >> l, Wl = W >> l;
     const float inv_scale = 1.0f / (float)(1 << l);
-    const float *P = pyr.p[l];
     const size_t mapsz = (size_t)Hl * Wl;
     const size_t qbase = (size_t)b * N + n0;
 
@@ -249,7 +247,6 @@ __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
     // ---- 3. outputs (i, 0..S-1) of query q ----
     const int ax = sm.ax[q], ay = sm.ay[q];
     const float *wq = &sm.win[q * WSTR];
-    float *o = out + (((size_t)b * L + l) * K + (size_t)i * S) * N + n;
     const float x0 = tx.f, ex = tx.lo, wx = tx.hi;
     if (mode == 0) {
         // regular taps: tap (i, j) has corners at neighbourhood column i, i+1 and rows j, j+1,
@@ -269,7 +266,7 @@ __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
             acc = __builtin_fmaf(c1[j], __fmul_rn(ey, wx), acc);
             acc = __builtin_fmaf(c0[j + 1], __fmul_rn(ny, ex), acc);
             acc = __builtin_fmaf(c1[j + 1], __fmul_rn(ny, wx), acc);
-            if (qok && (!(ABL & 2) || acc == 1234.5f)) o[(size_t)j * N] = acc;
+            if (qok && (!(ABL & 2) || acc == 1234.5f)) emit(j, acc);
         }
     } else if (!(mode & 1)) {
         // every corner is inside the neighbourhood (cells outside the map hold 0)
@@ -285,7 +282,7 @@ __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
             acc = __builtin_fmaf(c[1], __fmul_rn(ey, wx), acc);
             acc = __builtin_fmaf(c[WIN], __fmul_rn(ny, ex), acc);
             acc = __builtin_fmaf(c[WIN + 1], __fmul_rn(ny, wx), acc);
-            if (qok) o[(size_t)j * N] = acc;
+            if (qok) emit(j, acc);
         }
     } else {
         const float *Pq = P + (qbase + q) * mapsz;
@@ -304,9 +301,105 @@ __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
             acc = __builtin_fmaf(fetch(x1, y0), __fmul_rn(ey, wx), acc);
             acc = __builtin_fmaf(fetch(x0, y1), __fmul_rn(ny, ex), acc);
             acc = __builtin_fmaf(fetch(x1, y1), __fmul_rn(ny, wx), acc);
-            if (qok) o[(size_t)j * N] = acc;
+            if (qok) emit(j, acc);
         }
     }
+}
+
+template <int S, int QB, int ABL = 0>
+__global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
+    ConstLevelPtrs pyr, const float *__restrict__ coords, int B, int NQ, int H, int W, int L,
+    float *__restrict__ out) {
+    constexpr int K = S * S, NT = lookup_threads(S, QB);
+    __shared__ LookupSmem<S, QB> sm;
+    const int N = NQ;  // query pixels per batch item (H*W, or a row slab of it)
+    const int nqb = (N + QB - 1) / QB;
+    const int b = blockIdx.x / nqb;
+    const int n0 = (blockIdx.x - b * nqb) * QB;
+    const int l = blockIdx.y;
+    const int i = threadIdx.x / QB, n = n0 + threadIdx.x % QB;
+    float *o = out + (((size_t)b * L + l) * K + (size_t)i * S) * N + n;
+    lookup_block<S, QB, NT, ABL>(sm, pyr.p[l], coords, b, n0, N, H, W, l,
+                                 [&](int j, float acc) { o[(size_t)j * N] = acc; });
+}
+
+// Lookup fused with the consumer's 1x1 convolution (BasicMotionEncoder.convc1, update.py:68,75:
+// cor = relu(convc1(corr)), 324 -> 256 channels): a workgroup looks up 16 queries at every
+// level into an LDS tile ct[L*K][16] (lookup_block, bit-identical values), then multiplies it by
+// the transposed weight wt[L*K][O] on the fp32 MFMA (v_mfma_f32_16x16x4_f32: A = weight rows
+// = output channels, B = the tile, exact fp32 products, fp32 accumulate) and writes
+// relu(acc + bias) as [B][O][NQ].  The 324-channel lookup output never touches HBM.
+// Wave w owns output channels [64 w, 64 w + 64) (4 blocks of 16), so O = 256.
+constexpr int kConvQB = 16, kConvNT = 256, kConvO = 256;
+
+template <int S>
+__global__ __launch_bounds__(kConvNT) void lookup_conv_kernel(ConstLevelPtrs pyr, const float *__restrict__ coords,
+                                                              int B, int NQ, int H, int W, int L,
+                                                              const float *__restrict__ wt,
+                                                              const float *__restrict__ bias, int relu,
+                                                              float *__restrict__ out) {
+    constexpr int K = S * S, QB = kConvQB;
+    __shared__ LookupSmem<S, QB> sm;
+    __shared__ float ct[CORR_MAX_LEVELS * K][QB];
+    const int N = NQ;
+    const int nqb = (N + QB - 1) / QB;
+    const int b = blockIdx.x / nqb;
+    const int n0 = (blockIdx.x - b * nqb) * QB;
+    const int tid = threadIdx.x, i = tid / QB, q = tid % QB;
+    for (int l = 0; l < L; ++l) {
+        lookup_block<S, QB, kConvNT, 0>(sm, pyr.p[l], coords, b, n0, N, H, W, l,
+                                        [&](int j, float acc) { ct[l * K + i * S + j][q] = acc; });
+        __syncthreads();  // the next level reuses sm; the GEMM reads ct
+    }
+    const int KC = L * K;
+    const int lane = tid & 63, w = tid >> 6;
+    const int col = lane & 15, kr = lane >> 4;
+    const int o0 = w * 64;
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // weight rows stream from L2: batches of KB k-steps are loaded one batch ahead
+    constexpr int KB = 8;
+    const int nsteps = (KC + 3) / 4;
+    float wa[2][KB][4], cb[2][KB];
+    auto load = [&](int buf, int s0) {
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            const int k = 4 * (s0 + u) + kr;
+            const bool kok = k < KC;
+            cb[buf][u] = kok && n0 + col < N ? ct[k][col] : 0.0f;
+            const float *wr = wt + (size_t)(kok ? k : 0) * kConvO + o0 + col;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) wa[buf][u][t] = kok ? wr[16 * t] : 0.0f;
+        }
+    };
+    load(0, 0);
+    for (int s0 = 0; s0 < nsteps; s0 += 2 * KB) {
+        if (s0 + KB < nsteps) load(1, s0 + KB);
+#pragma unroll
+        for (int u = 0; u < KB; ++u)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[0][u][t], cb[0][u], acc[t], 0, 0, 0);
+        if (s0 + 2 * KB < nsteps) load(0, s0 + 2 * KB);
+        if (s0 + KB < nsteps) {
+#pragma unroll
+            for (int u = 0; u < KB; ++u)
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[1][u][t], cb[1][u], acc[t], 0, 0, 0);
+        }
+    }
+    const int n = n0 + col;
+    if (n >= N) return;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int o = o0 + 16 * t + 4 * kr + r;
+            float v = acc[t][r] + bias[o];
+            if (relu) v = fmaxf(v, 0.0f);
+            out[((size_t)b * kConvO + o) * N + n] = v;
+        }
 }
 
 template <int S>
@@ -584,6 +677,16 @@ hipError_t launch_lookup(const ConstLevelPtrs &pyr, const float *coords, int B, 
         case 7: return launch_lookup_s<15>(pyr, coords, B, NQ, H, W, levels, out, s);
         default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_lookup_conv(const ConstLevelPtrs &pyr, const float *coords, int B, int NQ, int H, int W,
+                              int levels, int radius, const float *wt, const float *bias, int relu, float *out,
+                              hipStream_t s) {
+    if (radius != 4) return hipErrorInvalidValue;  // instantiated for E-RAFT's r = 4 (K = 81)
+    const int nqb = (NQ + kConvQB - 1) / kConvQB;
+    hipLaunchKernelGGL(lookup_conv_kernel<9>, dim3(nqb * B), dim3(kConvNT), 0, s, pyr, coords, B, NQ, H, W, levels,
+                       wt, bias, relu, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_lookup_bwd(const float *coords, const float *grad_out, int B, int NQ, int H,

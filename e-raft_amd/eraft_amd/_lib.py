@@ -27,7 +27,7 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
            "corr_build_bwd_rows", "corr_build_workspace", "corr_build_ex",
            "corr_build_bwd_ex_workspace", "corr_build_bwd_ex", "corr_forward_splat_workspace",
            "corr_forward_splat", "corr_convex_upsample", "corr_voxel_grid_workspace",
-           "corr_voxel_grid")
+           "corr_voxel_grid", "corr_lookup_conv")
 
 # Build algorithms (include/corr_mi355x.h).  F16X3 is the default: fp32 features split into
 # f16 hi/lo pairs, three f16 MFMAs per product, fp32 accumulate (~1e-6 of max|C| from the
@@ -92,13 +92,14 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.corr_forward_splat_workspace.restype = sz
     lib.corr_forward_splat.argtypes = [vp, i, i, i, vp, vp, sz, vp]
     lib.corr_convex_upsample.argtypes = [vp, vp, i, i, i, vp, vp]
+    lib.corr_lookup_conv.argtypes = [vp, vp, i, i, i, i, i, vp, vp, i, vp, vp]
     lib.corr_voxel_grid_workspace.argtypes = [i, i, i, i]
     lib.corr_voxel_grid_workspace.restype = sz
     lib.corr_voxel_grid.argtypes = [vp, vp, vp, vp, i, i, i, i, i, vp, vp, sz, vp]
     for f in ("corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd",
               "corr_build_rows", "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows",
               "corr_build_ex", "corr_build_bwd_ex", "corr_forward_splat",
-              "corr_convex_upsample", "corr_voxel_grid"):
+              "corr_convex_upsample", "corr_voxel_grid", "corr_lookup_conv"):
         getattr(lib, f).restype = i
     if path is None:
         _lib = lib
@@ -260,3 +261,13 @@ def voxel_grid(x, y, t, p, out, normalize):
     with torch.cuda.device(out.device):
         _check(lib.corr_voxel_grid(*ptrs, M, C, H, W, int(bool(normalize)), o, ws.data_ptr(), ws.numel() * 4,
                                    _stream(out)))
+
+
+def lookup_conv(levels, coords, radius, weight_t, bias, out, relu=True):
+    """corr_lookup_conv: fused lookup + 1x1 conv (+ReLU) -> out [B, 256, H, W]."""
+    B, _, H, W = coords.shape
+    pp, c = _ptrs(levels, "pyr"), _dev(coords, "coords")
+    wt, bs, o = _dev(weight_t, "weight_t"), _dev(bias, "bias"), _dev(out, "out")
+    with torch.cuda.device(coords.device):
+        _check(load().corr_lookup_conv(pp, c, B, H, W, len(levels), radius, wt, bs, int(bool(relu)), o,
+                                       _stream(coords)))

@@ -167,6 +167,23 @@ class CorrBlock:
         _lib.lookup(self._state.levels, coords, self.radius, out)
         return out
 
+    def lookup_conv(self, coords, weight, bias, relu=True):
+        """Lookup fused with the motion encoder's first layer, relu(convc1(self(coords)))
+        (update.py:68,75), without materialising the lookup output.  weight: convc1.weight
+        [256, L*K, 1, 1]; bias [256].  Inference only (no autograd)."""
+        B, _, H, W = coords.shape
+        K = (2 * self.radius + 1) ** 2
+        key = (weight.data_ptr(), weight._version)
+        cached = getattr(self, "_wt_cache", None)
+        if cached is None or cached[0] != key:  # transposed once per block, not per iteration
+            wt = weight.detach().reshape(weight.shape[0], self.num_levels * K).t().contiguous().float()
+            self._wt_cache = cached = (key, wt)
+        wt = cached[1]
+        out = torch.empty((B, weight.shape[0], H, W), dtype=torch.float32, device=coords.device)
+        _lib.lookup_conv(self._state.levels, coords.detach().contiguous(), self.radius, wt,
+                         bias.detach().contiguous().float(), out, relu)
+        return out
+
     @staticmethod
     def corr(fmap1, fmap2):
         """model/corr.py:52-60: all-pairs volume [B, H, W, 1, H, W] scaled by 1/sqrt(D)."""

@@ -12,6 +12,8 @@ identical random weights, tests/test_e2e.py) and as the integration example.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -105,8 +107,9 @@ class BasicMotionEncoder(nn.Module):
         self.convf2 = nn.Conv2d(128, 64, 3, padding=1)
         self.conv = nn.Conv2d(64 + 192, 128 - 2, 3, padding=1)
 
-    def forward(self, flow, corr):
-        c = F.relu(self.convc2(F.relu(self.convc1(corr))))
+    def forward(self, flow, corr, fused=False):
+        # fused: corr already is relu(convc1(lookup)) (CorrBlock.lookup_conv, inference)
+        c = F.relu(self.convc2(corr if fused else F.relu(self.convc1(corr))))
         f = F.relu(self.convf2(F.relu(self.convf1(flow))))
         return torch.cat([F.relu(self.conv(torch.cat([c, f], dim=1))), flow], dim=1)
 
@@ -154,8 +157,8 @@ class BasicUpdateBlock(nn.Module):
         self.mask = nn.Sequential(nn.Conv2d(128, 256, 3, padding=1), nn.ReLU(inplace=True),
                                   nn.Conv2d(256, 64 * 9, 1))
 
-    def forward(self, net, inp, corr, flow):
-        motion = self.encoder(flow, corr)
+    def forward(self, net, inp, corr, flow, fused=False):
+        motion = self.encoder(flow, corr, fused)
         net = self.gru(net, torch.cat([inp, motion], dim=1))
         return net, 0.25 * self.mask(net), self.flow_head(net)
 
@@ -188,6 +191,9 @@ class ERAFT(nn.Module):
     context_dim = 128
     corr_levels = 4
     corr_radius = 4
+    # lookup fused with convc1 at inference (corr_lookup_conv) when ERAFT_AMD_FUSE_CONV=1.  Off
+    # by default: measured 1.1% slower end to end than lookup + rocBLAS convc1
+    fuse_lookup_conv = os.environ.get("ERAFT_AMD_FUSE_CONV", "0") == "1"
 
     def __init__(self, config, n_first_channels):
         super().__init__()
@@ -238,10 +244,17 @@ class ERAFT(nn.Module):
         if flow_init is not None:
             coords1 = coords1 + flow_init
         predictions = []
+        # inference on the MI355X: the lookup feeds convc1 on-chip (corr_lookup_conv)
+        fuse = (self.fuse_lookup_conv and image1.is_cuda and not torch.is_grad_enabled()
+                and self.corr_radius == 4 and hasattr(corr_fn, "lookup_conv"))
         for _ in range(iters):
             coords1 = coords1.detach()
-            corr = corr_fn(coords1)
-            net, up_mask, delta = self.update_block(net, inp, corr, coords1 - coords0)
+            if fuse:
+                enc = self.update_block.encoder
+                corr = corr_fn.lookup_conv(coords1, enc.convc1.weight, enc.convc1.bias)
+            else:
+                corr = corr_fn(coords1)
+            net, up_mask, delta = self.update_block(net, inp, corr, coords1 - coords0, fuse)
             coords1 = coords1 + delta
             predictions.append(self.image_padder.unpad(self.upsample_flow(coords1 - coords0, up_mask)))
         return coords1 - coords0, predictions

@@ -172,6 +172,18 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
 size_t corr_forward_splat_workspace(int B, int H, int W);
 
 /*
+ * Lookup fused with its consumer, BasicMotionEncoder's cor = relu(convc1(corr))
+ * (model/update.py:68,75; a 1x1 convolution L*(2r+1)^2 -> 256): the window lookup of
+ * corr_lookup into an on-chip tile, then out[b][o][h][w] = (relu?)(bias[o] +
+ * sum_c weight_t[c][o] * corr[b][c][h][w]) on the fp32 MFMA.  weight_t = convc1.weight viewed
+ * [256][L*K] and transposed to [L*K][256]; out [B][256][H][W].  radius 4 only (E-RAFT's);
+ * CORR_EUNSUPPORTED otherwise.  Inference (no gradient).
+ */
+int corr_lookup_conv(const float *const *pyr, const float *coords, int B, int H, int W,
+                     int levels, int radius, const float *weight_t, const float *bias, int relu,
+                     float *out, void *stream);
+
+/*
  * DSEC event -> voxel grid.  Replaces VoxelGrid.convert (utils/dsec_utils.py:26-64) as the DSEC
  * loader calls it (loader/loader_dsec.py:245-257): events as float32 device arrays x, y, t
  * (t in [0, 1], ascending), p in {0, 1}; out [C][H][W].  Bilinear in x and y, nearest-lower

@@ -83,3 +83,20 @@ def test_e2e_training_step_runs_through_hip_backward():
     loss.backward()
     g = model.fnet.conv1.weight.grad
     assert g is not None and torch.isfinite(g).all() and g.abs().sum() > 0
+
+
+@pytest.mark.gpu
+def test_e2e_with_fused_lookup_conv_matches_reference(monkeypatch):
+    """The same cold-start golden with the lookup fused into convc1 (corr_lookup_conv)."""
+    from eraft_amd.model import ERAFT
+    monkeypatch.setattr(ERAFT, "fuse_lookup_conv", True)
+    g = load("g_e2e_dsec")
+    seed, H, W, bins, iters = (int(v) for v in g["meta"])
+    dev = "cuda:0"
+    im1 = torch.from_numpy(prng.voxel_grid(seed, (1, bins, H, W))).to(dev)
+    im2 = torch.from_numpy(prng.voxel_grid(seed + 2, (1, bins, H, W))).to(dev)
+    model = _model(bins).to(dev)
+    with torch.no_grad():
+        low, ups = model(im1, im2, iters=iters)
+    assert _epe(low.cpu().numpy(), g["low"]) <= EPE_TOL
+    assert _epe(ups[-1][..., ::4, ::4].cpu().numpy(), g["up_sub"]) <= EPE_TOL

@@ -391,3 +391,24 @@ def test_voxel_grid_dsec_size_vs_oracle():
     a = vg.convert(ev).cpu().numpy()
     assert bit_equal(a, oracle.voxel_grid(ev_np, C, H, W, False))
     assert bit_equal(vg.convert(ev).cpu().numpy(), a)
+
+
+@pytest.mark.parametrize("B,H,W,L", [(1, 60, 80, 4), (2, 17, 23, 3)])
+def test_lookup_conv_vs_torch_reference(B, H, W, L):
+    """Fused lookup + convc1 + ReLU (corr_lookup_conv) vs the unfused reference composition
+    relu(conv2d(lookup, W, b)) evaluated in float64 from the (bit-exact) HIP lookup output:
+    |diff| <= 1e-5 of max|out|; and the same without ReLU."""
+    import torch.nn.functional as F
+    D, r = 32, 4
+    K = (2 * r + 1) ** 2
+    f1, f2 = prng.gauss(81, (B, D, H, W)), prng.gauss(82, (B, D, H, W))
+    cb = _cb()(torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV), num_levels=L, radius=r)
+    c = torch.from_numpy(prng.lookup_coords(83, B, H, W, 3.0)).to(DEV)
+    w = torch.from_numpy(prng.gauss(84, (256, L * K, 1, 1), 0.05)).to(DEV)
+    bias = torch.from_numpy(prng.gauss(85, (256,), 0.1)).to(DEV)
+    corr = cb(c).cpu().double()
+    pre = F.conv2d(corr, w.cpu().double(), bias.cpu().double())
+    for relu in (True, False):
+        ref = (torch.relu(pre) if relu else pre).numpy()
+        out = cb.lookup_conv(c, w, bias, relu=relu).cpu().numpy()
+        assert np.abs(out - ref).max() <= 1e-5 * np.abs(ref).max(), relu

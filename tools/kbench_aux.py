@@ -55,4 +55,17 @@ mask = torch.randn(1, 576, 60, 80, device=dev)
 out = torch.empty(1, 2, 480, 640, device=dev)
 res["convex_upsample_60x80"] = {"gpu_us": round(gpu_us(lambda: _lib.convex_upsample(ft, mask, out)), 1),
                                 "bytes": int(576 * 4800 * 4 + 2 * 4800 * 4 + 2 * 480 * 640 * 4)}
+# lookup fused with convc1 vs lookup + conv2d + relu (DSEC, 12 GRU iterations' worth)
+from eraft_amd import CorrBlock  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+f1 = torch.randn(1, 256, 60, 80, device=dev)
+f2 = torch.randn(1, 256, 60, 80, device=dev)
+cb = CorrBlock(f1, f2, 4, 4)
+co = (torch.stack(torch.meshgrid(torch.arange(60, device=dev), torch.arange(80, device=dev),
+                                 indexing="ij")[::-1]).float()[None] + torch.randn(1, 2, 60, 80, device=dev))
+wc = torch.randn(256, 324, 1, 1, device=dev) * 0.05
+bc = torch.randn(256, device=dev)
+res["lookup_convc1_dsec"] = {"fused_us": round(gpu_us(lambda: cb.lookup_conv(co, wc, bc)), 1),
+                             "unfused_us": round(gpu_us(lambda: F.relu(F.conv2d(cb(co), wc, bc))), 1),
+                             "lookup_only_us": round(gpu_us(lambda: cb(co)), 1)}
 print(json.dumps(res))
