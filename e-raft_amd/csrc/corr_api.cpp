@@ -242,7 +242,8 @@ int corr_lookup_conv(const float *const *pyr, const float *coords, int B, int H,
     g_err[0] = 0;
     int rc = check_dims(fn, B, H * W, H, W, levels);
     if (rc) return rc;
-    if (radius != 4) return fail(CORR_EUNSUPPORTED, "%s: built for radius 4 (got %d)", fn, radius);
+    if (radius != 4 || levels > 4)
+        return fail(CORR_EUNSUPPORTED, "%s: built for radius 4 and <= 4 levels (got %d, %d)", fn, radius, levels);
     if (!pyr) return fail(CORR_EINVAL, "%s: pyr is null", fn);
     ConstLevelPtrs lp{};
     for (int l = 0; l < levels; ++l) {

@@ -193,7 +193,7 @@ constexpr int lookup_threads(int S, int QB) { return (QB * S + 63) / 64 * 64; }
 template <int S, int QB, int NT, int ABL, class Emit>
 __device__ __forceinline__ void lookup_block(LookupSmem<S, QB> &sm, const float *__restrict__ P,
                                              const float *__restrict__ coords, int b, int n0, int N,
-                                             int H, int W, int l, Emit emit) {
+                                             int H, int W, int l, int tid, Emit emit) {
     constexpr int R = (S - 1) / 2;
     using SM = LookupSmem<S, QB>;
     constexpr int WIN = SM::WIN, WSTR = SM::WSTR;
@@ -202,7 +202,6 @@ __device__ __forceinline__ void lookup_block(LookupSmem<S, QB> &sm, const float 
     const size_t mapsz = (size_t)Hl * Wl;
     const size_t qbase = (size_t)b * N + n0;
 
-    const int tid = threadIdx.x;
     const int q = tid % QB;
     const int i = tid / QB;  // this thread's x-tap (window column); i >= S: gather only
     const bool act = i < S;
@@ -319,18 +318,20 @@ __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
     const int l = blockIdx.y;
     const int i = threadIdx.x / QB, n = n0 + threadIdx.x % QB;
     float *o = out + (((size_t)b * L + l) * K + (size_t)i * S) * N + n;
-    lookup_block<S, QB, NT, ABL>(sm, pyr.p[l], coords, b, n0, N, H, W, l,
+    lookup_block<S, QB, NT, ABL>(sm, pyr.p[l], coords, b, n0, N, H, W, l, (int)threadIdx.x,
                                  [&](int j, float acc) { o[(size_t)j * N] = acc; });
 }
 
 // Lookup fused with the consumer's 1x1 convolution (BasicMotionEncoder.convc1, update.py:68,75:
-// cor = relu(convc1(corr)), 324 -> 256 channels): a workgroup looks up 16 queries at every
-// level into an LDS tile ct[L*K][16] (lookup_block, bit-identical values), then multiplies it by
-// the transposed weight wt[L*K][O] on the fp32 MFMA (v_mfma_f32_16x16x4_f32: A = weight rows
-// = output channels, B = the tile, exact fp32 products, fp32 accumulate) and writes
-// relu(acc + bias) as [B][O][NQ].  The 324-channel lookup output never touches HBM.
-// Wave w owns output channels [64 w, 64 w + 64) (4 blocks of 16), so O = 256.
-constexpr int kConvQB = 16, kConvNT = 256, kConvO = 256;
+// cor = relu(convc1(corr)), 324 -> 256 channels).  A workgroup owns 16 queries: four groups of
+// 3 waves look them up at the four pyramid levels CONCURRENTLY (lookup_block, bit-identical
+// values) into an LDS tile ct[L*K][16]; then 8 waves multiply it by the transposed weight
+// wt[L*K][O] on the fp32 MFMA (v_mfma_f32_16x16x4_f32: A = weight rows = output channels,
+// B = the tile; exact fp32 products, fp32 accumulate; weight batches loaded one batch ahead)
+// and write relu(acc + bias) as [B][O][NQ].  The 324-channel lookup output never reaches HBM.
+// Wave w < 8 owns output channels [32 w, 32 w + 32), so O = 256; L <= 4 (groups beyond L
+// repeat the last level and discard it, keeping every barrier collective).
+constexpr int kConvQB = 16, kConvGT = 192, kConvGroups = 4, kConvNT = kConvGT * kConvGroups, kConvO = 256;
 
 template <int S>
 __global__ __launch_bounds__(kConvNT) void lookup_conv_kernel(ConstLevelPtrs pyr, const float *__restrict__ coords,
@@ -339,29 +340,33 @@ __global__ __launch_bounds__(kConvNT) void lookup_conv_kernel(ConstLevelPtrs pyr
                                                               const float *__restrict__ bias, int relu,
                                                               float *__restrict__ out) {
     constexpr int K = S * S, QB = kConvQB;
-    __shared__ LookupSmem<S, QB> sm;
-    __shared__ float ct[CORR_MAX_LEVELS * K][QB];
+    static_assert(lookup_threads(S, QB) == kConvGT, "one level per 3-wave group");
+    __shared__ LookupSmem<S, QB> sm[kConvGroups];
+    __shared__ float ct[kConvGroups * K][QB];
     const int N = NQ;
     const int nqb = (N + QB - 1) / QB;
     const int b = blockIdx.x / nqb;
     const int n0 = (blockIdx.x - b * nqb) * QB;
-    const int tid = threadIdx.x, i = tid / QB, q = tid % QB;
-    for (int l = 0; l < L; ++l) {
-        lookup_block<S, QB, kConvNT, 0>(sm, pyr.p[l], coords, b, n0, N, H, W, l,
-                                        [&](int j, float acc) { ct[l * K + i * S + j][q] = acc; });
-        __syncthreads();  // the next level reuses sm; the GEMM reads ct
-    }
+    const int tid = threadIdx.x;
+    const int g = tid / kConvGT, ltid = tid - g * kConvGT;
+    const int l = g < L ? g : L - 1;
+    const int i = ltid / QB, q = ltid % QB;
+    lookup_block<S, QB, kConvGT, 0>(sm[g], pyr.p[l], coords, b, n0, N, H, W, l, ltid, [&](int j, float acc) {
+        if (g < L) ct[g * K + i * S + j][q] = acc;
+    });
+    __syncthreads();  // the GEMM reads every level's tile
     const int KC = L * K;
     const int lane = tid & 63, w = tid >> 6;
+    if (w >= 8) return;
     const int col = lane & 15, kr = lane >> 4;
-    const int o0 = w * 64;
-    f32x4 acc[4];
+    const int o0 = w * 32;
+    f32x4 acc[2];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 2; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     // weight rows stream from L2: batches of KB k-steps are loaded one batch ahead
     constexpr int KB = 8;
     const int nsteps = (KC + 3) / 4;
-    float wa[2][KB][4], cb[2][KB];
+    float wa[2][KB][2], cb[2][KB];
     auto load = [&](int buf, int s0) {
 #pragma unroll
         for (int u = 0; u < KB; ++u) {
@@ -370,7 +375,7 @@ __global__ __launch_bounds__(kConvNT) void lookup_conv_kernel(ConstLevelPtrs pyr
             cb[buf][u] = kok && n0 + col < N ? ct[k][col] : 0.0f;
             const float *wr = wt + (size_t)(kok ? k : 0) * kConvO + o0 + col;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) wa[buf][u][t] = kok ? wr[16 * t] : 0.0f;
+            for (int t = 0; t < 2; ++t) wa[buf][u][t] = kok ? wr[16 * t] : 0.0f;
         }
     };
     load(0, 0);
@@ -379,20 +384,20 @@ __global__ __launch_bounds__(kConvNT) void lookup_conv_kernel(ConstLevelPtrs pyr
 #pragma unroll
         for (int u = 0; u < KB; ++u)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[0][u][t], cb[0][u], acc[t], 0, 0, 0);
+            for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[0][u][t], cb[0][u], acc[t], 0, 0, 0);
         if (s0 + 2 * KB < nsteps) load(0, s0 + 2 * KB);
         if (s0 + KB < nsteps) {
 #pragma unroll
             for (int u = 0; u < KB; ++u)
 #pragma unroll
-                for (int t = 0; t < 4; ++t)
+                for (int t = 0; t < 2; ++t)
                     acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[1][u][t], cb[1][u], acc[t], 0, 0, 0);
         }
     }
     const int n = n0 + col;
     if (n >= N) return;
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int o = o0 + 16 * t + 4 * kr + r;
@@ -682,7 +687,7 @@ hipError_t launch_lookup(const ConstLevelPtrs &pyr, const float *coords, int B, 
 hipError_t launch_lookup_conv(const ConstLevelPtrs &pyr, const float *coords, int B, int NQ, int H, int W,
                               int levels, int radius, const float *wt, const float *bias, int relu, float *out,
                               hipStream_t s) {
-    if (radius != 4) return hipErrorInvalidValue;  // instantiated for E-RAFT's r = 4 (K = 81)
+    if (radius != 4 || levels > kConvGroups) return hipErrorInvalidValue;  // E-RAFT: r = 4, L <= 4
     const int nqb = (NQ + kConvQB - 1) / kConvQB;
     hipLaunchKernelGGL(lookup_conv_kernel<9>, dim3(nqb * B), dim3(kConvNT), 0, s, pyr, coords, B, NQ, H, W, levels,
                        wt, bias, relu, out);

@@ -176,7 +176,7 @@ size_t corr_forward_splat_workspace(int B, int H, int W);
  * (model/update.py:68,75; a 1x1 convolution L*(2r+1)^2 -> 256): the window lookup of
  * corr_lookup into an on-chip tile, then out[b][o][h][w] = (relu?)(bias[o] +
  * sum_c weight_t[c][o] * corr[b][c][h][w]) on the fp32 MFMA.  weight_t = convc1.weight viewed
- * [256][L*K] and transposed to [L*K][256]; out [B][256][H][W].  radius 4 only (E-RAFT's);
+ * [256][L*K] and transposed to [L*K][256]; out [B][256][H][W].  radius 4, levels <= 4 (E-RAFT);
  * CORR_EUNSUPPORTED otherwise.  Inference (no gradient).
  */
 int corr_lookup_conv(const float *const *pyr, const float *coords, int B, int H, int W,
