@@ -351,7 +351,9 @@ inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct BwdWs {
     u32x4 *pkA, *pkB;
     int *exA, *exB;
-    unsigned *mxA, *mxB, *mxC;  // row max of A, row max of B (dC rows), column max of dC
+    unsigned *mxA, *mxB, *mxC, *mxA2;  // row max of F2, of dC rows, column max of dC, row max of F1
+    unsigned *mx0;                     // start of the four (contiguous, zeroed once per call)
+    size_t mx_bytes;
     float *slab;
 };
 
@@ -368,12 +370,15 @@ BwdWs carve(void *ws, int B, int D, int NQ, int N) {
     w += al256((size_t)B * D * 4);
     r.exB = (int *)w;
     w += al256((size_t)B * R * 4);
-    r.mxA = (unsigned *)w;
+    r.mx0 = r.mxA = (unsigned *)w;
     w += al256((size_t)B * D * 4);
     r.mxB = (unsigned *)w;
     w += al256((size_t)B * R * 4);
     r.mxC = (unsigned *)w;
     w += al256((size_t)B * R * 4);
+    r.mxA2 = (unsigned *)w;
+    w += al256((size_t)B * D * 4);
+    r.mx_bytes = (size_t)(w - (char *)r.mx0);
     r.slab = (float *)w;
     return r;
 }
@@ -385,15 +390,8 @@ size_t slab_floats(int B, int D, int NQ, int N) {
     return std::max(s1, s2);
 }
 
+// rmax / cmax must be zeroed by the caller (one memset covers every maximum of a call).
 hipError_t absmax(const float *X, int B, int rows, int cols, unsigned *rmax, unsigned *cmax, hipStream_t s) {
-    if (rmax) {
-        hipError_t e = hipMemsetAsync(rmax, 0, (size_t)B * rows * 4, s);
-        if (e != hipSuccess) return e;
-    }
-    if (cmax) {
-        hipError_t e = hipMemsetAsync(cmax, 0, (size_t)B * cols * 4, s);
-        if (e != hipSuccess) return e;
-    }
     hipLaunchKernelGGL(absmax_kernel, dim3((cols + 255) / 256, (rows + kRowsPer - 1) / kRowsPer, B), dim3(256), 0, s,
                        X, rows, cols, rmax, cmax);
     return hipGetLastError();
@@ -457,7 +455,7 @@ size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W) {
     const int N = H * W;
     const size_t R = std::max(NQ, N), KP = (size_t)(std::max(NQ, N) + kBK - 1) / kBK * kBK;
     return al256((size_t)B * KP * D * 4) + al256((size_t)B * KP * R * 4) + al256((size_t)B * D * 4) +
-           al256((size_t)B * R * 4) + al256((size_t)B * D * 4) + 2 * al256((size_t)B * R * 4) +
+           al256((size_t)B * R * 4) + 2 * al256((size_t)B * D * 4) + 2 * al256((size_t)B * R * 4) +
            slab_floats(B, D, NQ, N) * sizeof(float);
 }
 
@@ -471,14 +469,15 @@ hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, 
 #define CK_(x)                          \
     if ((e = (x)) != hipSuccess) return e;
     // dF1 = F2 . dC^T : A = F2 rows d (k = m), B = dC rows n (k = m)
+    CK_(hipMemsetAsync(w.mx0, 0, w.mx_bytes, s));
     CK_(absmax(grad_c, B, NQ, N, w.mxB, w.mxC, s));  // one pass: dC row and column maxima
     CK_(absmax(f2, B, D, N, w.mxA, nullptr, s));
+    CK_(absmax(f1, B, D, NQ, w.mxA2, nullptr, s));
     CK_(convert(f2, (long)D * N, N, 1, B, D, N, w.mxA, w.pkA, w.exA, s));
     CK_(convert(grad_c, (long)NQ * N, N, 1, B, NQ, N, w.mxB, w.pkB, w.exB, s));
     CK_(gemm(w, B, D, NQ, N, sD, df1, s));
     // dF2 = F1 . dC : A = F1 rows d (k = n), B = dC columns m (k = n)
-    CK_(absmax(f1, B, D, NQ, w.mxA, nullptr, s));
-    CK_(convert(f1, (long)D * NQ, NQ, 1, B, D, NQ, w.mxA, w.pkA, w.exA, s));
+    CK_(convert(f1, (long)D * NQ, NQ, 1, B, D, NQ, w.mxA2, w.pkA, w.exA, s));
     CK_(convert(grad_c, (long)NQ * N, 1, N, B, N, NQ, w.mxC, w.pkB, w.exB, s));
     CK_(gemm(w, B, D, N, NQ, sD, df2, s));
 #undef CK_
