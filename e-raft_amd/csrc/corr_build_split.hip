@@ -33,6 +33,7 @@
 //   ex[b][n] = e_n (int32).  KP = D rounded up to 16 (zero padding).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <type_traits>
 
 #include "corr_build_common.h"
@@ -181,6 +182,72 @@ __global__ __launch_bounds__(64 * kPackW) void split_pack_reg_kernel(PackArgs a)
     }
 }
 
+// Pixel-lane pack: lane = pixel, 64 consecutive pixels per workgroup of NW waves, wave w holding
+// the chunks kc = w, w + NW, ... .  Every load instruction reads one feature of 64 consecutive
+// pixels (256 contiguous bytes; the register pack's read 2 x 64 B), and a lane writes its
+// pixel's whole 64-B chunk record as four 16-B stores that together cover the wave's 4 KiB run.
+// The per-pixel max is reduced over the NW waves through LDS.  Same arithmetic as
+// split_pack_kernel, element for element (bit-identical packs).
+template <int NW, int CPT>
+__global__ __launch_bounds__(64 * NW) void split_pack_px_kernel(PackArgs a) {
+    __shared__ float red[NW][64];
+    const int z = blockIdx.z, b = blockIdx.y, tid = threadIdx.x;
+    const int NP = a.np[z], D = a.D, nkc = a.KP / kSplitBK;
+    const int n0 = blockIdx.x * 64;
+    if (n0 >= NP) return;  // the grid covers the larger of the two tensors (uniform exit)
+    const int lane = tid & 63, w = tid >> 6;
+    const int n = min(n0 + lane, NP - 1);  // clamped: unconditional loads
+    const float *src = a.f[z] + (size_t)b * D * NP + n;
+    float v[CPT][16];
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+        const int kc = w + NW * c;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int d = kc * kSplitBK + j;
+            v[c][j] = (kc < nkc && d < D) ? src[(size_t)d * NP] : 0.f;
+        }
+    }
+    float m = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) m = fmaxf(m, fabsf(v[c][j]));
+    red[w][lane] = m;
+    __syncthreads();
+    float mm = 0.f;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) mm = fmaxf(mm, red[k][lane]);
+    int s = 0;
+    if (mm > 0.f && mm <= 3.402823466e38f) {
+        int E;
+        (void)frexpf(mm, &E);  // mm < 2^E
+        s = 15 - E;            // mm * 2^s < 2^15: neither half overflows
+    }
+    const bool live = n0 + lane < NP;
+    if (w == 0 && live) a.ex[z][(size_t)b * NP + n0 + lane] = -s;
+    if (!live) return;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+        const int kc = w + NW * c;
+        if (kc >= nkc) break;
+        u32x4 *dst = a.pk[z] + (((size_t)b * nkc + kc) * NP + n0 + lane) * 4;
+#pragma unroll
+        for (int oct = 0; oct < 2; ++oct) {
+            half8 hi8, lo8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float y = ldexpf(v[c][oct * 8 + j], s);
+                const _Float16 hi = (_Float16)y;
+                hi8[j] = hi;
+                lo8[j] = __builtin_isinf(y) ? (_Float16)0.f : (_Float16)(y - (float)hi);
+            }
+            dst[2 * oct] = __builtin_bit_cast(u32x4, hi8);
+            dst[2 * oct + 1] = __builtin_bit_cast(u32x4, lo8);
+        }
+    }
+}
+
 // Chunks per wave of the register pack for this KP, 0 = use the LDS pack.
 inline int split_pack_cpt(int KP) {
     const int nkc = KP / kSplitBK;
@@ -225,6 +292,7 @@ struct SplitParams {
     int nq, npx, npy;        // query blocks, patch columns (16 px), patch rows (8*WT px)
     int eshift;              // log2(1/sqrt(D)) when that is exact, else 0
     int exact;               // 1/sqrt(D) is a power of two, folded into the exponent
+    int vec0;                // level 0 takes 16-B stores (W % 4 == 0, aligned base) even when !VEC
     float inv_s;             // 1/sqrt(D) otherwise (multiplied: within tolerance, not bitwise)
 };
 
@@ -358,7 +426,11 @@ __device__ __forceinline__ void split_epilogue(const SplitParams &p, f32x16 (&ac
                 {
                     const int Y = Y0 + 4 * half + drow;
                     const float e4[4] = {v4.x, v4.y, v4.z, v4.w};
-                    if (nlev > 0 && qok && Y < H) store_run<4, VEC>(p.lvl[0] + qrow * N + (size_t)Y * W, X0 + 4 * dc4, W, e4);
+                    if (nlev > 0 && qok && Y < H) {
+                        float *row = p.lvl[0] + qrow * N + (size_t)Y * W;
+                        if (VEC || p.vec0) store_run<4, true>(row, X0 + 4 * dc4, W, e4);
+                        else store_run<4, false>(row, X0 + 4 * dc4, W, e4);
+                    }
                 }
                 // level 1 at lanes with an even row: columns 2 dc4, 2 dc4 + 1 of L1 row 2 half + drow / 2
                 float s0 = v4.x + v4.y;
@@ -705,6 +777,31 @@ size_t build_split_workspace(int B, int D, int NQ, int H, int W) {
 
 bool build_split_supported(int D) { return split_pack_tp(split_kp(D)) > 0; }
 
+// Pixel-lane pack with NW waves per workgroup (kbench variants; D <= 16 * NW * 4).
+template <int NW>
+hipError_t launch_split_pack_px(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, void *ws,
+                                hipStream_t s) {
+    const SplitWs w = split_ws(ws, B, D, NQ, H, W);
+    PackArgs a{};
+    a.f[0] = f1, a.f[1] = f2;
+    a.pk[0] = w.pk1, a.pk[1] = w.pk2;
+    a.ex[0] = w.ex1, a.ex[1] = w.ex2;
+    a.np[0] = NQ, a.np[1] = H * W;
+    a.D = D;
+    a.KP = split_kp(D);
+    const int np = std::max(NQ, H * W);
+    const int cpt = (a.KP / kSplitBK + NW - 1) / NW;
+    const dim3 grid((np + 63) / 64, B, 2), blk(64 * NW);
+    switch (cpt) {
+        case 1: hipLaunchKernelGGL((split_pack_px_kernel<NW, 1>), grid, blk, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((split_pack_px_kernel<NW, 2>), grid, blk, 0, s, a); break;
+        case 3: hipLaunchKernelGGL((split_pack_px_kernel<NW, 3>), grid, blk, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((split_pack_px_kernel<NW, 4>), grid, blk, 0, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 // lds_pack: force the LDS-tiled pack (any D; the register pack covers D <= 512).
 hipError_t launch_split_pack(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, void *ws,
                              hipStream_t s, bool lds_pack = false) {
@@ -773,6 +870,7 @@ hipError_t launch_split_mfma_cfg(int NQ, int B, int D, int H, int W, int levels,
     const long tiles = (long)p.nq * p.npx * p.npy * B;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
     const bool vec = split_vec_ok(W, pyr, p.nlev);
+    p.vec0 = p.nlev > 0 && W % 4 == 0 && (uintptr_t)pyr.p[0] % 16 == 0;
     static bool attr_set[2] = {false, false};
     if (!attr_set[vec]) {
         hipError_t e = hipFuncSetAttribute(vec ? (const void *)corr_build_split_kernel<Cfg, true>
@@ -825,6 +923,7 @@ hipError_t launch_split_ring_cfg(int NQ, int B, int D, int H, int W, int levels,
     const size_t lds = std::max(STAGES * (size_t)Cfg::ROWS * 64, (size_t)(Cfg::NT / 64) * kEpiBytes) +
                        (size_t)Cfg::ROWS * 4;
     const bool vec = split_vec_ok(W, pyr, p.nlev);
+    p.vec0 = p.nlev > 0 && W % 4 == 0 && (uintptr_t)pyr.p[0] % 16 == 0;
     static bool attr_set[2] = {false, false};
     if (!attr_set[vec]) {
         hipError_t e = hipFuncSetAttribute(vec ? (const void *)corr_build_split_ring_kernel<Cfg, STAGES, true>
@@ -853,9 +952,42 @@ hipError_t launch_build_split_cfg(const float *f1, int NQ, const float *f2, int 
     return launch_split_mfma_cfg<Cfg>(NQ, B, D, H, W, levels, pyr, ws, s);
 }
 
+// Tile geometry per shape.  The candidates compute identical bits (every output sums the same
+// chunk sequence through the same three MFMAs and the same epilogue; only the workgroup shape
+// differs), so the choice is free.  Every wave owns a 64-query x 128-target tile in all three,
+// so the padded work — and the rounds of waves over the chip — is proportional to the wave
+// count; take the configuration with the fewest, ties to the larger workgroup (more LDS
+// operand reuse).  Measured (profiles/r01j_kbench_split.txt, MFMA kernel): DSEC 60x80 all tie
+// -> 2x2; train 36x48 B8 4x1 (82 vs 84 us); MVSEC 36x44 B16 2x1 (163 vs 170 us).
+// CORR_SPLIT_TILE=0|1|2 forces 2x2 | 4x1 | 2x1 (tests: all three must agree bit for bit).
+using SplitTall = SplitCfg<4, 1, 2, 2>;
+using SplitSmall = SplitCfg<2, 1, 2, 2>;
+
+template <class Cfg>
+long split_waves(int NQ, int B, int H, int W) {
+    return (long)((NQ + Cfg::BQ - 1) / Cfg::BQ) * ((W + 15) / 16) * ((H + Cfg::PH - 1) / Cfg::PH) * B * (Cfg::NT / 64);
+}
+
+int split_tile_choice(int NQ, int B, int H, int W) {
+    if (const char *e = std::getenv("CORR_SPLIT_TILE")) {
+        const int v = std::atoi(e);
+        if (v >= 0 && v <= 2) return v;
+    }
+    const long w[3] = {split_waves<SplitDefault>(NQ, B, H, W), split_waves<SplitTall>(NQ, B, H, W),
+                       split_waves<SplitSmall>(NQ, B, H, W)};
+    int pick = 0;
+    for (int k = 1; k < 3; ++k)
+        if (w[k] < w[pick]) pick = k;
+    return pick;
+}
+
 hipError_t launch_build_split(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, int levels,
                               const LevelPtrs &pyr, void *ws, hipStream_t s) {
-    return launch_build_split_cfg<SplitDefault>(f1, NQ, f2, B, D, H, W, levels, pyr, ws, s);
+    switch (split_tile_choice(NQ, B, H, W)) {
+        case 1: return launch_build_split_cfg<SplitTall>(f1, NQ, f2, B, D, H, W, levels, pyr, ws, s);
+        case 2: return launch_build_split_cfg<SplitSmall>(f1, NQ, f2, B, D, H, W, levels, pyr, ws, s);
+        default: return launch_build_split_cfg<SplitDefault>(f1, NQ, f2, B, D, H, W, levels, pyr, ws, s);
+    }
 }
 
 }  // namespace corr

@@ -59,6 +59,33 @@ def test_build_matches_reference(name, algo, monkeypatch):
         assert bit_equal(oracle.avg_pool2x2(gpu[l - 1]), gpu[l]), l
 
 
+@pytest.mark.parametrize("shape", [(1, 256, 60, 80), (8, 256, 36, 48), (3, 256, 36, 44), (2, 200, 17, 23),
+                                   (1, 64, 9, 130)])
+def test_split_tile_geometries_bit_identical(shape, monkeypatch):
+    """The f16x3 build picks its workgroup shape per map size (corr_build_split.hip,
+    split_tile_choice); every choice must write the same bits, and the auto pick with them."""
+    B, D, H, W = shape
+    monkeypatch.setenv("ERAFT_AMD_BUILD", "f16x3")
+    t1 = torch.from_numpy(prng.gauss(11, (B, D, H, W))).to(DEV)
+    t2 = torch.from_numpy(prng.gauss(12, (B, D, H, W))).to(DEV)
+    pyrs = []
+    for tile in ("0", "1", "2", None):
+        if tile is None:
+            monkeypatch.delenv("CORR_SPLIT_TILE", raising=False)
+        else:
+            monkeypatch.setenv("CORR_SPLIT_TILE", tile)
+        cb = _cb()(t1, t2, num_levels=4, radius=4)
+        torch.cuda.synchronize()
+        pyrs.append([p.cpu().numpy() for p in cb.corr_pyramid])
+    for k in range(1, len(pyrs)):
+        for l in range(4):
+            assert bit_equal(pyrs[0][l], pyrs[k][l]), (k, l)
+    nq = min(H * W, 300)  # oracle on the first queries only (seconds at every shape)
+    ref = oracle.corr_rows(prng.gauss(11, (B, D, H, W)), prng.gauss(12, (B, D, H, W)), 0, nq)
+    got = pyrs[0][0].reshape(B, H * W, H * W)[:, :nq]
+    assert norm_rel(got, ref) < REL_TOL
+
+
 @pytest.mark.parametrize("name", BUILD_CASES)
 def test_lookup_bitexact_on_reference_pyramid(name):
     g = load(name)

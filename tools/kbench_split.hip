@@ -104,6 +104,15 @@ int main(int argc, char **argv) {
         vs.push_back({"x3   pack only LDS", [&](float *o) {
                           return launch_split_pack(f1, (int)N, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, true);
                       }});
+        vs.push_back({"x3   pack only px4", [&](float *o) {
+                          return launch_split_pack_px<4>(f1, (int)N, f2, sh.B, sh.D, sh.H, sh.W, ws, 0);
+                      }});
+        vs.push_back({"x3   pack only px8", [&](float *o) {
+                          return launch_split_pack_px<8>(f1, (int)N, f2, sh.B, sh.D, sh.H, sh.W, ws, 0);
+                      }});
+        vs.push_back({"x3   pack only px16", [&](float *o) {
+                          return launch_split_pack_px<16>(f1, (int)N, f2, sh.B, sh.D, sh.H, sh.W, ws, 0);
+                      }});
         {  // the register pack and the LDS pack must write identical bytes
             hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f1, fe, 7u, 3.0f);
             hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f2, fe, 8u, 0.01f);
@@ -115,6 +124,15 @@ int main(int argc, char **argv) {
             CK(launch_split_pack(f1, (int)N, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, false));
             CK(hipMemcpy(h1.data(), ws, wsb, hipMemcpyDeviceToHost));
             printf("%-10s pack reg vs LDS: %s\n", sh.name, std::memcmp(h0.data(), h1.data(), wsb) ? "DIFFER" : "bit-identical");
+            for (int nw : {4, 8, 16}) {
+                CK(hipMemset(ws, 0, wsb));
+                CK(nw == 4    ? launch_split_pack_px<4>(f1, (int)N, f2, sh.B, sh.D, sh.H, sh.W, ws, 0)
+                   : nw == 8 ? launch_split_pack_px<8>(f1, (int)N, f2, sh.B, sh.D, sh.H, sh.W, ws, 0)
+                             : launch_split_pack_px<16>(f1, (int)N, f2, sh.B, sh.D, sh.H, sh.W, ws, 0));
+                CK(hipMemcpy(h1.data(), ws, wsb, hipMemcpyDeviceToHost));
+                printf("%-10s pack px%d vs LDS: %s\n", sh.name, nw,
+                       std::memcmp(h0.data(), h1.data(), wsb) ? "DIFFER" : "bit-identical");
+            }
         }
         const size_t first_mfma = vs.size();
 #define MF(name, ...)                                                                                     \
