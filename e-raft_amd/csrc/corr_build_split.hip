@@ -292,7 +292,7 @@ struct SplitParams {
     int nq, npx, npy;        // query blocks, patch columns (16 px), patch rows (8*WT px)
     int eshift;              // log2(1/sqrt(D)) when that is exact, else 0
     int exact;               // 1/sqrt(D) is a power of two, folded into the exponent
-    int vec0;                // level 0 takes 16-B stores (W % 4 == 0, aligned base) even when !VEC
+    int vec0, vec1;          // !VEC: store width of levels 0 / 1 (store_run4_mode: 2, 1 or 0)
     float inv_s;             // 1/sqrt(D) otherwise (multiplied: within tolerance, not bitwise)
 };
 
@@ -355,6 +355,19 @@ __device__ __forceinline__ void store_run(float *row, int X, int Wl, const float
 #pragma unroll
         for (int k = 0; k < NV; ++k)
             if (X + k < Wl) row[X + k] = v[k];
+    }
+}
+
+// Run of 4 at column X (a multiple of 4) with a store width picked per launch: mode 2 = one
+// 16-B store (W % 4 == 0), 1 = two 8-B stores (W even), 0 = element stores.  Uniform per level.
+__device__ __forceinline__ void store_run4_mode(float *row, int X, int Wl, const float *v, int mode) {
+    if (mode == 2) {
+        store_run<4, true>(row, X, Wl, v);
+    } else if (mode == 1) {
+        if (X < Wl) *reinterpret_cast<float2 *>(row + X) = make_float2(v[0], v[1]);
+        if (X + 2 < Wl) *reinterpret_cast<float2 *>(row + X + 2) = make_float2(v[2], v[3]);
+    } else {
+        store_run<4, false>(row, X, Wl, v);
     }
 }
 
@@ -428,8 +441,8 @@ __device__ __forceinline__ void split_epilogue(const SplitParams &p, f32x16 (&ac
                     const float e4[4] = {v4.x, v4.y, v4.z, v4.w};
                     if (nlev > 0 && qok && Y < H) {
                         float *row = p.lvl[0] + qrow * N + (size_t)Y * W;
-                        if (VEC || p.vec0) store_run<4, true>(row, X0 + 4 * dc4, W, e4);
-                        else store_run<4, false>(row, X0 + 4 * dc4, W, e4);
+                        if constexpr (VEC) store_run<4, true>(row, X0 + 4 * dc4, W, e4);
+                        else store_run4_mode(row, X0 + 4 * dc4, W, e4, p.vec0);
                     }
                 }
                 // level 1 at lanes with an even row: columns 2 dc4, 2 dc4 + 1 of L1 row 2 half + drow / 2
@@ -467,9 +480,11 @@ __device__ __forceinline__ void split_epilogue(const SplitParams &p, f32x16 (&ac
                 const float4 v4 = reinterpret_cast<const float4 *>(R1)[u];
                 const float e4[4] = {v4.x, v4.y, v4.z, v4.w};
                 const int q = q0 + qb0 + ql, Y = (Y0 >> 1) + row;
-                if (q < NQ && Y < H1)
-                    store_run<4, VEC>(p.lvl[1] + ((size_t)b * NQ + q) * (size_t)(H1 * W1) + (size_t)Y * W1,
-                                      (X0 >> 1) + 4 * c4, W1, e4);
+                if (q < NQ && Y < H1) {
+                    float *row1 = p.lvl[1] + ((size_t)b * NQ + q) * (size_t)(H1 * W1) + (size_t)Y * W1;
+                    if constexpr (VEC) store_run<4, true>(row1, (X0 >> 1) + 4 * c4, W1, e4);
+                    else store_run4_mode(row1, (X0 >> 1) + 4 * c4, W1, e4, p.vec1);
+                }
             }
         }
         if (nlev > 2) {
@@ -761,6 +776,13 @@ SplitWs split_ws(void *ws, int B, int D, int NQ, int H, int W) {
 
 // Vector (16-B / 8-B) stores in every fused level: W % 16 == 0 keeps each level's row runs
 // aligned and never straddling the right edge; level bases must be 16-B aligned.
+// Store width of one level's runs of 4 (columns X = 4k; row offsets are multiples of Wl).
+int split_store_mode(int Wl, const float *base) {
+    if (Wl % 4 == 0 && (uintptr_t)base % 16 == 0) return 2;
+    if (Wl % 2 == 0 && (uintptr_t)base % 8 == 0) return 1;
+    return 0;
+}
+
 bool split_vec_ok(int W, const LevelPtrs &pyr, int nlev) {
     if (W % 16) return false;
     for (int l = 0; l < nlev; ++l)
@@ -870,7 +892,8 @@ hipError_t launch_split_mfma_cfg(int NQ, int B, int D, int H, int W, int levels,
     const long tiles = (long)p.nq * p.npx * p.npy * B;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
     const bool vec = split_vec_ok(W, pyr, p.nlev);
-    p.vec0 = p.nlev > 0 && W % 4 == 0 && (uintptr_t)pyr.p[0] % 16 == 0;
+    p.vec0 = p.nlev > 0 ? split_store_mode(W, pyr.p[0]) : 0;
+    p.vec1 = p.nlev > 1 ? split_store_mode(W >> 1, pyr.p[1]) : 0;
     static bool attr_set[2] = {false, false};
     if (!attr_set[vec]) {
         hipError_t e = hipFuncSetAttribute(vec ? (const void *)corr_build_split_kernel<Cfg, true>
@@ -923,7 +946,8 @@ hipError_t launch_split_ring_cfg(int NQ, int B, int D, int H, int W, int levels,
     const size_t lds = std::max(STAGES * (size_t)Cfg::ROWS * 64, (size_t)(Cfg::NT / 64) * kEpiBytes) +
                        (size_t)Cfg::ROWS * 4;
     const bool vec = split_vec_ok(W, pyr, p.nlev);
-    p.vec0 = p.nlev > 0 && W % 4 == 0 && (uintptr_t)pyr.p[0] % 16 == 0;
+    p.vec0 = p.nlev > 0 ? split_store_mode(W, pyr.p[0]) : 0;
+    p.vec1 = p.nlev > 1 ? split_store_mode(W >> 1, pyr.p[1]) : 0;
     static bool attr_set[2] = {false, false};
     if (!attr_set[vec]) {
         hipError_t e = hipFuncSetAttribute(vec ? (const void *)corr_build_split_ring_kernel<Cfg, STAGES, true>

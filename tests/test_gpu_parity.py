@@ -60,7 +60,7 @@ def test_build_matches_reference(name, algo, monkeypatch):
 
 
 @pytest.mark.parametrize("shape", [(1, 256, 60, 80), (8, 256, 36, 48), (3, 256, 36, 44), (2, 200, 17, 23),
-                                   (1, 64, 9, 130)])
+                                   (1, 64, 9, 130), (2, 96, 20, 46)])
 def test_split_tile_geometries_bit_identical(shape, monkeypatch):
     """The f16x3 build picks its workgroup shape per map size (corr_build_split.hip,
     split_tile_choice); every choice must write the same bits, and the auto pick with them."""
@@ -84,6 +84,9 @@ def test_split_tile_geometries_bit_identical(shape, monkeypatch):
     ref = oracle.corr_rows(prng.gauss(11, (B, D, H, W)), prng.gauss(12, (B, D, H, W)), 0, nq)
     got = pyrs[0][0].reshape(B, H * W, H * W)[:, :nq]
     assert norm_rel(got, ref) < REL_TOL
+    # every level's store width (16-B, 8-B or element stores by W_l) writes the pooled values
+    for l in range(1, 4):
+        assert bit_equal(oracle.avg_pool2x2(pyrs[0][l - 1]), pyrs[0][l]), l
 
 
 @pytest.mark.parametrize("name", BUILD_CASES)
