@@ -980,9 +980,9 @@ hipError_t launch_build_split_cfg(const float *f1, int NQ, const float *f2, int 
 // chunk sequence through the same three MFMAs and the same epilogue; only the workgroup shape
 // differs), so the choice is free.  Every wave owns a 64-query x 128-target tile in all three,
 // so the padded work — and the rounds of waves over the chip — is proportional to the wave
-// count; take the configuration with the fewest, ties to the larger workgroup (more LDS
-// operand reuse).  Measured (profiles/r01j_kbench_split.txt, MFMA kernel): DSEC 60x80 all tie
-// -> 2x2; train 36x48 B8 4x1 (82 vs 84 us); MVSEC 36x44 B16 2x1 (163 vs 170 us).
+// count; take the configuration with the fewest, ties to 4x1, then 2x2.  Measured
+// (profiles/r01j_kbench_split.txt, r01k_tile_ab.txt): DSEC 60x80 all tie -> 4x1 (bench 6504
+// vs 6418 frame-pairs/s for 2x2); train 36x48 B8 4x1 (67 vs 69 us); MVSEC 36x44 B16 2x1.
 // CORR_SPLIT_TILE=0|1|2 forces 2x2 | 4x1 | 2x1 (tests: all three must agree bit for bit).
 using SplitTall = SplitCfg<4, 1, 2, 2>;
 using SplitSmall = SplitCfg<2, 1, 2, 2>;
@@ -999,8 +999,8 @@ int split_tile_choice(int NQ, int B, int H, int W) {
     }
     const long w[3] = {split_waves<SplitDefault>(NQ, B, H, W), split_waves<SplitTall>(NQ, B, H, W),
                        split_waves<SplitSmall>(NQ, B, H, W)};
-    int pick = 0;
-    for (int k = 1; k < 3; ++k)
+    int pick = 1;  // ties: 4x1 first (DSEC, 3 interleaved A/B runs: 72.3 vs 73.9 us for 2x2)
+    for (int k : {0, 2})
         if (w[k] < w[pick]) pick = k;
     return pick;
 }
