@@ -296,6 +296,33 @@ int corr_voxel_grid(const float *x, const float *y, const float *t, const float 
                       fn);
 }
 
+size_t corr_voxel_grid_tbilinear_workspace(int n_events, int C, int H, int W) {
+    if (n_events < 0 || C < 1 || H < 1 || W < 1) return 0;
+    return voxel_tbilinear_workspace(n_events, C, H, W);
+}
+
+int corr_voxel_grid_tbilinear(const double *events, int n_events, int C, int H, int W, int normalize, float *out,
+                              void *workspace, size_t workspace_bytes, void *stream) {
+    static const char *fn = "corr_voxel_grid_tbilinear";
+    g_err[0] = 0;
+    if (n_events < 0 || C < 1 || H < 1 || W < 1)
+        return fail(CORR_EINVAL, "%s: need n_events >= 0 and C, H, W >= 1 (got %d, %d, %d, %d)", fn, n_events, C,
+                    H, W);
+    if ((long long)n_events * 2 >= (1ll << 31) || (long long)C * H * W >= (1ll << 31))
+        return fail(CORR_EINVAL, "%s: problem too large", fn);
+    int rc;
+    if ((rc = check_ptr(fn, out, "out"))) return rc;
+    if (n_events > 0) {
+        if ((rc = check_ptr(fn, events, "events"))) return rc;
+        if ((uintptr_t)events % 8) return fail(CORR_EINVAL, "%s: events is not 8-byte aligned", fn);
+    }
+    const size_t need = voxel_tbilinear_workspace(n_events, C, H, W);
+    if (workspace_bytes < need || !workspace)
+        return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
+    return hip_status(
+        launch_voxel_grid_tbilinear(events, n_events, C, H, W, normalize, out, workspace, (hipStream_t)stream), fn);
+}
+
 size_t corr_forward_splat_workspace(int B, int H, int W) {
     if (B < 1 || H < 1 || W < 1) return 0;
     return splat_workspace(B, H, W);

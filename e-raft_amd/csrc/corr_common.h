@@ -52,6 +52,9 @@ hipError_t launch_lookup_conv(const ConstLevelPtrs &pyr, const float *coords, in
                               hipStream_t s);
 size_t splat_workspace(int B, int H, int W);
 size_t voxel_workspace(int M, int C, int H, int W);
+size_t voxel_tbilinear_workspace(int M, int C, int H, int W);
+hipError_t launch_voxel_grid_tbilinear(const double *events, int M, int C, int H, int W, int normalize, float *out,
+                                       void *ws, hipStream_t s);
 hipError_t launch_voxel_grid(const float *x, const float *y, const float *t, const float *p, int M, int C, int H,
                              int W, int normalize, float *out, void *ws, hipStream_t s);
 hipError_t launch_forward_splat(const float *flow, int B, int H, int W, float *out, void *ws, hipStream_t s);

@@ -15,6 +15,15 @@
 // Optional normalisation (:54-62) over the nonzero cells: count, sum and sum of squared
 // deviations in fp64 (fixed partitions over 512 workgroups + ordered tree: deterministic), then
 // v = (v - mean) / std in fp32 (std unbiased; v - mean when std is not > 0).
+//
+// The MVSEC representation (utils/transformers.py:18-126 EventSequenceToVoxelGrid_Pytorch, fed by
+// loader/loader_mvsec_flow.py:35) runs through the same count / scan / bucket / ordered-sum
+// pipeline with a different entry source (VoxTArgs): events [M][4] float64 (t, x, y, p) as
+// the loader hands them over (.astype('float'), :46); each event makes two entries, "left"
+// (bin floor(t_n), weight p (1 - dt)) and "right" (bin floor(t_n) + 1, weight p dt) with
+// t_n = ((C-1) (t - t_0)) / (t_{M-1} - t_0) in fp64 and dt rounded to fp32 (:77-89).  The
+// reference adds them with two index_add_ passes (:99-112), each sequential in event order on
+// CPU, so entry = side * M + event reproduces its per-cell order exactly.
 #include <cmath>
 
 #include "corr_common.h"
@@ -27,12 +36,24 @@ struct VoxEntry {
     int cell;  // -1: out of bounds
 };
 
+// DSEC (dsec_utils.py:26-64): four xy corners per event, entry = corner * M + event.
 struct VoxArgs {
     const float *x, *y, *t, *p;
     int M, C, H, W;
+    static constexpr int kSides = 4;
+    __device__ __forceinline__ VoxEntry entry(int e) const;
 };
 
-__device__ __forceinline__ VoxEntry vox_entry(const VoxArgs &a, int e) {
+// MVSEC (transformers.py:36-126): two temporal sides per event, entry = side * M + event.
+struct VoxTArgs {
+    const double *ev;  // [M][4]: t, x, y, p
+    int M, C, H, W;
+    static constexpr int kSides = 2;
+    __device__ __forceinline__ VoxEntry entry(int e) const;
+};
+
+__device__ __forceinline__ VoxEntry VoxArgs::entry(int e) const {
+    const VoxArgs &a = *this;
     const int corner = e / a.M, i = e - corner * a.M;
     const float t0 = a.t[0], dt = __fsub_rn(a.t[a.M - 1], t0);
     const float tn = __fdiv_rn(__fmul_rn((float)(a.C - 1), __fsub_rn(a.t[i], t0)), dt);
@@ -48,10 +69,41 @@ __device__ __forceinline__ VoxEntry vox_entry(const VoxArgs &a, int e) {
     return r;
 }
 
-__global__ __launch_bounds__(256) void vox_count_kernel(VoxArgs a, int *__restrict__ cnt) {
+// transformers.py:66-112, op for op: t_n in fp64 (:77, (C-1) * (t - t0) first, then / deltaT,
+// deltaT = 1 when the stamps are equal :74-75); tis = floor(t_n), dts = t_n - tis (fp64) then
+// rounded to fp32 (:85-89); pols = fp32(p), 0 -> -1 (:81-82); x, y truncated to int64 (:79-80).
+// left: valid for 0 <= tis < C; right: bin tis + 1, valid for 0 <= tis and tis + 1 < C
+// (:91-92, :106-107).  The flat index x + y W + bin W H is the reference's (:100-101); one
+// outside [0, C H W) makes index_add_ raise in the reference and is dropped here.
+__device__ __forceinline__ VoxEntry VoxTArgs::entry(int e) const {
+    const int side = e >= M ? 1 : 0, i = e - side * M;
+    const double t0 = ev[0];
+    double dT = __dsub_rn(ev[(size_t)(M - 1) * 4], t0);
+    if (dT == 0.0) dT = 1.0;
+    const double *q = ev + (size_t)i * 4;
+    const double ts = __ddiv_rn(__dmul_rn((double)(C - 1), __dsub_rn(q[0], t0)), dT);
+    const double tis = floor(ts);
+    const float dts = (float)__dsub_rn(ts, tis);
+    float pol = (float)q[3];
+    if (pol == 0.0f) pol = -1.0f;
+    VoxEntry r;
+    r.w = side ? __fmul_rn(pol, dts) : __fmul_rn(pol, __fsub_rn(1.0f, dts));
+    r.cell = -1;
+    const double bin = __dadd_rn(tis, (double)side);
+    const double lim = 2147483648.0;  // |x|, |y| < 2^31: the int64 index below cannot overflow
+    if (tis >= 0.0 && bin < (double)C && fabs(q[1]) < lim && fabs(q[2]) < lim) {
+        const long long xs = (long long)q[1], ys = (long long)q[2], HW = (long long)H * W;
+        const long long cell = xs + ys * W + (long long)bin * HW;
+        if (cell >= 0 && cell < HW * C) r.cell = (int)cell;
+    }
+    return r;
+}
+
+template <class A>
+__global__ __launch_bounds__(256) void vox_count_kernel(A a, int *__restrict__ cnt) {
     const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= 4 * a.M) return;
-    const VoxEntry v = vox_entry(a, e);
+    if (e >= A::kSides * a.M) return;
+    const VoxEntry v = a.entry(e);
     if (v.cell >= 0) atomicAdd(&cnt[v.cell], 1);
 }
 
@@ -128,16 +180,18 @@ __global__ __launch_bounds__(1024) void vox_tile_scan_kernel(const int *__restri
     }
 }
 
-__global__ __launch_bounds__(256) void vox_fill_kernel(VoxArgs a, const int *__restrict__ off, int *__restrict__ fill,
+template <class A>
+__global__ __launch_bounds__(256) void vox_fill_kernel(A a, const int *__restrict__ off, int *__restrict__ fill,
                                                        int *__restrict__ ent) {
     const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= 4 * a.M) return;
-    const VoxEntry v = vox_entry(a, e);
+    if (e >= A::kSides * a.M) return;
+    const VoxEntry v = a.entry(e);
     if (v.cell >= 0) ent[off[v.cell] + atomicAdd(&fill[v.cell], 1)] = e;
 }
 
 // One thread per cell: sort its bucket (ascending entry index = the reference's order), sum.
-__global__ __launch_bounds__(256) void vox_gather_kernel(VoxArgs a, const int *__restrict__ cnt,
+template <class A>
+__global__ __launch_bounds__(256) void vox_gather_kernel(A a, const int *__restrict__ cnt,
                                                          const int *__restrict__ off, int *__restrict__ ent,
                                                          float *__restrict__ out) {
     const int n = a.C * a.H * a.W;
@@ -155,7 +209,7 @@ __global__ __launch_bounds__(256) void vox_gather_kernel(VoxArgs a, const int *_
         b[j + 1] = v;
     }
     float s = 0.0f;
-    for (int i = 0; i < k; ++i) s = __fadd_rn(s, vox_entry(a, b[i]).w);
+    for (int i = 0; i < k; ++i) s = __fadd_rn(s, a.entry(b[i]).w);
     out[c] = s;
 }
 
@@ -243,41 +297,39 @@ __global__ __launch_bounds__(256) void vox_normalize_kernel(float *__restrict__ 
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-}  // namespace
-
-// cnt [CHW] | off [CHW] | fill [CHW] | ent [4M] | tile sums | stats [4] float | partials (fp64)
-size_t voxel_workspace(int M, int C, int H, int W) {
+// cnt [CHW] | off [CHW] | fill [CHW] | ent [entries] | tile sums | stats [4] float | partials (fp64)
+size_t voxel_ws_entries(size_t entries, int C, int H, int W) {
     const size_t n = (size_t)C * H * W, tiles = (n + kTile - 1) / kTile;
-    return 3 * al256(n * 4) + al256((size_t)4 * M * 4) + al256(tiles * 4) + 256 +
+    return 3 * al256(n * 4) + al256(entries * 4) + al256(tiles * 4) + 256 +
            al256((2 * kStatBlocks + 2) * sizeof(double));
 }
 
-hipError_t launch_voxel_grid(const float *x, const float *y, const float *t, const float *p, int M, int C, int H,
-                             int W, int normalize, float *out, void *ws, hipStream_t s) {
-    const size_t n = (size_t)C * H * W;
+template <class A>
+hipError_t launch_voxel(const A &a, int normalize, float *out, void *ws, hipStream_t s) {
+    const int C = a.C, H = a.H, W = a.W, M = a.M;
+    const size_t n = (size_t)C * H * W, entries = (size_t)A::kSides * M;
     char *w = (char *)ws;
     int *cnt = (int *)w, *off = (int *)(w + al256(n * 4)), *fill = (int *)(w + 2 * al256(n * 4));
     int *ent = (int *)(w + 3 * al256(n * 4));
     const size_t tiles = (n + kTile - 1) / kTile;
-    int *tsum = (int *)(w + 3 * al256(n * 4) + al256((size_t)4 * M * 4));
+    int *tsum = (int *)(w + 3 * al256(n * 4) + al256(entries * 4));
     float *st = (float *)((char *)tsum + al256(tiles * 4));
     double *part = (double *)((char *)st + 256);
     hipError_t e = hipMemsetAsync(cnt, 0, n * 4, s);
     if (e == hipSuccess) e = hipMemsetAsync(fill, 0, n * 4, s);
     if (e != hipSuccess) return e;
-    VoxArgs a{x, y, t, p, M, C, H, W};
-    const unsigned ge = (unsigned)((4 * (size_t)M + 255) / 256), gc = (unsigned)((n + 255) / 256);
+    const unsigned ge = (unsigned)((entries + 255) / 256), gc = (unsigned)((n + 255) / 256);
     if (M > 0) {
-        hipLaunchKernelGGL(vox_count_kernel, dim3(ge), dim3(256), 0, s, a, cnt);
+        hipLaunchKernelGGL(vox_count_kernel<A>, dim3(ge), dim3(256), 0, s, a, cnt);
         hipLaunchKernelGGL(vox_tile_sum_kernel, dim3((unsigned)tiles), dim3(1024), 0, s, cnt, (int)n, tsum);
         hipLaunchKernelGGL(vox_scan_small_kernel, dim3(1), dim3(1024), 0, s, tsum, (int)tiles);
         hipLaunchKernelGGL(vox_tile_scan_kernel, dim3((unsigned)tiles), dim3(1024), 0, s, cnt, (int)n, tsum, off);
-        hipLaunchKernelGGL(vox_fill_kernel, dim3(ge), dim3(256), 0, s, a, off, fill, ent);
+        hipLaunchKernelGGL(vox_fill_kernel<A>, dim3(ge), dim3(256), 0, s, a, off, fill, ent);
     } else {
         e = hipMemsetAsync(off, 0, n * 4, s);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(vox_gather_kernel, dim3(gc), dim3(256), 0, s, a, cnt, off, ent, out);
+    hipLaunchKernelGGL(vox_gather_kernel<A>, dim3(gc), dim3(256), 0, s, a, cnt, off, ent, out);
     if (normalize) {
         for (int pass = 0; pass < 2; ++pass) {
             hipLaunchKernelGGL(vox_stat_partial_kernel, dim3(kStatBlocks), dim3(256), 0, s, out, (int)n, pass, st, part);
@@ -286,6 +338,24 @@ hipError_t launch_voxel_grid(const float *x, const float *y, const float *t, con
         hipLaunchKernelGGL(vox_normalize_kernel, dim3(gc), dim3(256), 0, s, out, (int)n, st);
     }
     return hipGetLastError();
+}
+
+}  // namespace
+
+size_t voxel_workspace(int M, int C, int H, int W) { return voxel_ws_entries((size_t)VoxArgs::kSides * M, C, H, W); }
+
+size_t voxel_tbilinear_workspace(int M, int C, int H, int W) {
+    return voxel_ws_entries((size_t)VoxTArgs::kSides * M, C, H, W);
+}
+
+hipError_t launch_voxel_grid(const float *x, const float *y, const float *t, const float *p, int M, int C, int H,
+                             int W, int normalize, float *out, void *ws, hipStream_t s) {
+    return launch_voxel(VoxArgs{x, y, t, p, M, C, H, W}, normalize, out, ws, s);
+}
+
+hipError_t launch_voxel_grid_tbilinear(const double *events, int M, int C, int H, int W, int normalize, float *out,
+                                       void *ws, hipStream_t s) {
+    return launch_voxel(VoxTArgs{events, M, C, H, W}, normalize, out, ws, s);
 }
 
 }  // namespace corr

@@ -27,7 +27,8 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
            "corr_build_bwd_rows", "corr_build_workspace", "corr_build_ex",
            "corr_build_bwd_ex_workspace", "corr_build_bwd_ex", "corr_forward_splat_workspace",
            "corr_forward_splat", "corr_convex_upsample", "corr_voxel_grid_workspace",
-           "corr_voxel_grid", "corr_lookup_conv")
+           "corr_voxel_grid", "corr_lookup_conv", "corr_voxel_grid_tbilinear_workspace",
+           "corr_voxel_grid_tbilinear")
 
 # Build algorithms (include/corr_mi355x.h).  F16X3 is the default: fp32 features split into
 # f16 hi/lo pairs, three f16 MFMAs per product, fp32 accumulate (~1e-6 of max|C| from the
@@ -96,10 +97,14 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.corr_voxel_grid_workspace.argtypes = [i, i, i, i]
     lib.corr_voxel_grid_workspace.restype = sz
     lib.corr_voxel_grid.argtypes = [vp, vp, vp, vp, i, i, i, i, i, vp, vp, sz, vp]
+    lib.corr_voxel_grid_tbilinear_workspace.argtypes = [i, i, i, i]
+    lib.corr_voxel_grid_tbilinear_workspace.restype = sz
+    lib.corr_voxel_grid_tbilinear.argtypes = [vp, i, i, i, i, i, vp, vp, sz, vp]
     for f in ("corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd",
               "corr_build_rows", "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows",
               "corr_build_ex", "corr_build_bwd_ex", "corr_forward_splat",
-              "corr_convex_upsample", "corr_voxel_grid", "corr_lookup_conv"):
+              "corr_convex_upsample", "corr_voxel_grid", "corr_lookup_conv",
+              "corr_voxel_grid_tbilinear"):
         getattr(lib, f).restype = i
     if path is None:
         _lib = lib
@@ -261,6 +266,25 @@ def voxel_grid(x, y, t, p, out, normalize):
     with torch.cuda.device(out.device):
         _check(lib.corr_voxel_grid(*ptrs, M, C, H, W, int(bool(normalize)), o, ws.data_ptr(), ws.numel() * 4,
                                    _stream(out)))
+
+
+def voxel_grid_tbilinear(events, out, normalize):
+    """corr_voxel_grid_tbilinear: float64 device events [M, 4] (t, x, y, p) -> out [C, H, W]."""
+    C, H, W = out.shape
+    if events.dim() != 2 or events.shape[1] != 4:
+        raise ValueError(f"events must be [M, 4] (t, x, y, p) (got {tuple(events.shape)})")
+    if events.device.type != "cuda":
+        raise RuntimeError(f"events is on {events.device}: eraft_amd runs only on an MI355X (HIP) device")
+    if events.dtype != torch.float64 or not events.is_contiguous():
+        raise TypeError("events must be a contiguous float64 tensor")
+    M = events.shape[0]
+    o = _dev(out, "out")
+    lib = load()
+    n = lib.corr_voxel_grid_tbilinear_workspace(M, C, H, W)
+    ws = torch.empty(max(1, (n + 3) // 4), dtype=torch.int32, device=out.device)
+    with torch.cuda.device(out.device):
+        _check(lib.corr_voxel_grid_tbilinear(events.data_ptr() if M else 0, M, C, H, W, int(bool(normalize)), o,
+                                             ws.data_ptr(), ws.numel() * 4, _stream(out)))
 
 
 def lookup_conv(levels, coords, radius, weight_t, bias, out, relu=True):

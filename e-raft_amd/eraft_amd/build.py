@@ -22,7 +22,7 @@ HEADERS = ["corr_common.h", "corr_build_common.h", os.path.join("..", "..", "inc
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off: the lookup / pool arithmetic is specified op-by-op (each fp32 op rounds
 # once, fmaf only where the reference's ATen kernel fuses); the compiler must not contract.
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++20", "-fPIC", "-shared", "-ffp-contract=off",
          "-Wall"]
 
 

@@ -198,6 +198,23 @@ int corr_voxel_grid(const float *x, const float *y, const float *t, const float 
                     size_t workspace_bytes, void *stream);
 
 /*
+ * MVSEC event -> voxel grid.  Replaces EventSequenceToVoxelGrid_Pytorch.__call__
+ * (utils/transformers.py:36-126), the representation of loader/loader_mvsec_flow.py:35:
+ * events [n_events][4] float64 device rows (t, x, y, p), as the loader's event_sequence.features
+ * .astype('float') holds them (t ascending in practice; t_0 = row 0, t_end = the last row);
+ * out [C][H][W].  Bilinear in t: t_n = (C-1)(t - t_0)/(t_end - t_0) (fp64), each event adds
+ * p(1 - dt) at bin floor(t_n) and p dt at floor(t_n) + 1 (p = 0 -> -1, dt rounded to fp32),
+ * at flat index trunc(x) + trunc(y) W + bin H W.  The raw grid is bit-identical to the
+ * reference's two index_add_ passes (left then right, event order) — deterministic, no float
+ * atomics.  An entry whose flat index falls outside the grid is dropped (the reference raises).
+ * normalize: as corr_voxel_grid.  Workspace: corr_voxel_grid_tbilinear_workspace(...) bytes.
+ */
+size_t corr_voxel_grid_tbilinear_workspace(int n_events, int C, int H, int W);
+int corr_voxel_grid_tbilinear(const double *events, int n_events, int C, int H, int W,
+                              int normalize, float *out, void *workspace, size_t workspace_bytes,
+                              void *stream);
+
+/*
  * Convex upsampling of the 1/8-resolution flow after every GRU iteration.  Replaces
  * ERAFT.upsample_flow (model/eraft.py:75-86): softmax over the 9 taps of mask
  * [N][9*64][h][w], weighted sum of the zero-padded 3x3 neighbourhood of 8*flow [N][2][h][w]

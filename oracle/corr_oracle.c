@@ -22,6 +22,9 @@
  *                                                      oracle_corr_bwd
  *   utils/image_utils.py:10-83  forward_interpolate_pytorch / grid_sample_values
  *                         (warm-start forward splat) -> oracle_forward_splat
+ *   utils/dsec_utils.py:26-64   VoxelGrid.convert    -> oracle_voxel_grid
+ *   utils/transformers.py:36-126 EventSequenceToVoxelGrid_Pytorch
+ *                                                   -> oracle_voxel_grid_tbilinear
  *
  * Build with -ffp-contract=off: every fp32 operation below is meant to round exactly once,
  * and fmaf() is used only where the reference's ATen kernel fuses.
@@ -346,6 +349,61 @@ void oracle_voxel_grid(const float *x, const float *y, const float *t, const flo
         if (out[i] != 0.0f) q += ((double)out[i] - mean) * ((double)out[i] - mean);
     const float mf = (float)mean;
     const float sf = n > 1 ? (float)sqrt(q / (double)(n - 1)) : NAN;
+    for (long i = 0; i < CHW; ++i)
+        if (out[i] != 0.0f) out[i] = sf > 0.0f ? (out[i] - mf) / sf : out[i] - mf;
+}
+
+/*
+ * MVSEC event -> voxel grid, utils/transformers.py:36-126 (EventSequenceToVoxelGrid_Pytorch,
+ * the representation of loader/loader_mvsec_flow.py:35), events [M][4] float64 rows
+ * (t, x, y, p) as .astype('float') makes them (:46):
+ *   t_n = ((C-1) * (t - t[0])) / dT, dT = t[M-1] - t[0] or 1 when 0 (:66-77, fp64);
+ *   tis = floor(t_n), dts = fp32(t_n - tis) (:85-87); pol = fp32(p), 0 -> -1 (:81-82);
+ *   left  = pol * (1 - dts) at bin tis      for 0 <= tis < C      (:88, :91-103);
+ *   right = pol * dts       at bin tis + 1  for 0 <= tis, tis+1 < C (:89, :106-112);
+ *   flat index trunc(x) + trunc(y) * W + bin * W * H; index_add_ on CPU adds sequentially in
+ *   index order: all left entries in event order, then all right entries.  An index outside
+ *   the grid (the reference raises) is skipped.  normalize: as oracle_voxel_grid.
+ */
+void oracle_voxel_grid_tbilinear(const double *ev, long M, int C, int H, int W, int normalize, float *out) {
+    const long CHW = (long)C * H * W, HW = (long)H * W;
+    memset(out, 0, sizeof(float) * CHW);
+    if (M >= 1) {
+        const double t0 = ev[0];
+        double dT = ev[(M - 1) * 4] - t0;
+        if (dT == 0.0) dT = 1.0;
+        for (int side = 0; side < 2; ++side)
+            for (long e = 0; e < M; ++e) {
+                const double *q = ev + e * 4;
+                const double ts = ((double)(C - 1) * (q[0] - t0)) / dT;
+                const double tis = floor(ts);
+                const float dts = (float)(ts - tis);
+                float pol = (float)q[3];
+                if (pol == 0.0f) pol = -1.0f;
+                const double bin = tis + side;
+                if (!(tis >= 0.0 && bin < (double)C)) continue;
+                if (!(fabs(q[1]) < 2147483648.0 && fabs(q[2]) < 2147483648.0)) continue;
+                const long idx = (long)q[1] + (long)q[2] * W + (long)bin * HW;
+                if (idx < 0 || idx >= CHW) continue;
+                const float v = side ? pol * dts : pol * (1.0f - dts);
+                out[idx] = out[idx] + v;
+            }
+    }
+    if (!normalize) return;
+    long n = 0;
+    double s = 0.0;
+    for (long i = 0; i < CHW; ++i)
+        if (out[i] != 0.0f) {
+            s += out[i];
+            ++n;
+        }
+    if (n == 0) return;
+    const double mean = s / (double)n;
+    double qq = 0.0;
+    for (long i = 0; i < CHW; ++i)
+        if (out[i] != 0.0f) qq += ((double)out[i] - mean) * ((double)out[i] - mean);
+    const float mf = (float)mean;
+    const float sf = n > 1 ? (float)sqrt(qq / (double)(n - 1)) : NAN;
     for (long i = 0; i < CHW; ++i)
         if (out[i] != 0.0f) out[i] = sf > 0.0f ? (out[i] - mf) / sf : out[i] - mf;
 }

@@ -49,9 +49,10 @@ def _load():
         lib.oracle_corr_bwd.argtypes = [vp, vp, vp, i, i, i, vp, vp]
         lib.oracle_forward_splat.argtypes = [vp, i, i, i, vp]
         lib.oracle_voxel_grid.argtypes = [vp, vp, vp, vp, l, i, i, i, i, vp]
+        lib.oracle_voxel_grid_tbilinear.argtypes = [vp, l, i, i, i, i, vp]
         for f in ("oracle_corr_rows", "oracle_avg_pool2x2", "oracle_lookup",
                   "oracle_lookup_bwd", "oracle_pool_bwd", "oracle_corr_bwd", "oracle_forward_splat",
-                  "oracle_voxel_grid"):
+                  "oracle_voxel_grid", "oracle_voxel_grid_tbilinear"):
             getattr(lib, f).restype = None
         _lib = lib
     return _lib
@@ -185,4 +186,14 @@ def voxel_grid(ev, C, H, W, normalize) -> np.ndarray:
     out = np.empty((C, H, W), np.float32)
     rows = [np.ascontiguousarray(ev[k]) for k in range(4)]
     _load().oracle_voxel_grid(*[_p(r) for r in rows], M, C, H, W, int(bool(normalize)), _p(out))
+    return out
+
+
+def voxel_grid_tbilinear(events, C, H, W, normalize) -> np.ndarray:
+    """utils/transformers.py:36-126 EventSequenceToVoxelGrid_Pytorch: events [M, 4] float64
+    rows (t, x, y, p) -> [C, H, W] float32."""
+    ev = np.ascontiguousarray(events, dtype=np.float64)
+    M = ev.shape[0]
+    out = np.empty((C, H, W), np.float32)
+    _load().oracle_voxel_grid_tbilinear(_p(ev), M, C, H, W, int(bool(normalize)), _p(out))
     return out

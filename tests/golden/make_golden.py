@@ -179,7 +179,43 @@ def case_voxel(name, seed):
     save(name, **out)
 
 
+def case_voxel_mvsec(name, seed):
+    """MVSEC event -> voxel grid (utils/transformers.py:18-126 EventSequenceToVoxelGrid_Pytorch,
+    the representation of loader/loader_mvsec_flow.py:35), normalize=True and False.  Events
+    as the MVSEC loader holds them: [M, 4] float64 rows (t, x, y, p) with integer pixel
+    coordinates, t ascending relative microsecond stamps, p in {0, 1}; duplicated stamps, the
+    first/last bins and colliding pixels are included, and case "c" has all stamps equal
+    (deltaT = 0 -> 1).  index_add_ on CPU adds sequentially in index order, so the thread
+    count does not matter; run single-threaded anyway as main.py:2-5 does."""
+    import types
+    from utils.transformers import EventSequenceToVoxelGrid_Pytorch
+    torch.set_num_threads(1)
+    out = {}
+    for tag, M, C, H, W in (("a", 3000, 5, 12, 16), ("b", 60000, 15, 260, 346), ("c", 500, 3, 8, 8)):
+        u = prng.uniform(seed, (4, M)).astype(np.float64)
+        x = np.floor(u[0] * W)
+        y = np.floor(u[1] * H)
+        t = np.sort(u[2] * 50000.0)          # relative microseconds (loader_mvsec_flow.py:170-172)
+        t[::5] = np.floor(t[::5])             # some integer stamps
+        t[10:20] = t[10]                      # repeated stamps
+        if tag == "c":
+            t[:] = 12345.0
+        p = (u[3] > 0.5).astype(np.float64)
+        ev = np.ascontiguousarray(np.stack([t, x, y, p], axis=1))
+        seq = types.SimpleNamespace(features=ev, image_width=W, image_height=H)
+        out[f"ev_{tag}"] = ev
+        out[f"meta_{tag}"] = np.array([M, C, H, W], np.int64)
+        for norm, key in ((False, "raw"), (True, "norm")):
+            conv = EventSequenceToVoxelGrid_Pytorch(C, gpu=False, normalize=norm, forkserver=False)
+            out[f"{key}_{tag}"] = conv(seq).numpy()
+        seed += 1
+    save(name, **out)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "voxel_mvsec":
+        case_voxel_mvsec("g_voxel_mvsec", 51)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "voxel":
         case_voxel("g_voxel", 41)
         sys.exit(0)

@@ -143,6 +143,18 @@ def test_oracle_forward_splat_matches_reference_golden():
     assert bit_equal(oracle.forward_splat(e["low"]), e["flow_init"])
 
 
+def test_oracle_voxel_grid_tbilinear_matches_reference_golden():
+    """MVSEC event -> voxel grid (utils/transformers.py:36-126) restated in C: the raw grid is
+    bit-identical to the reference (left then right index_add_ passes, event order), including
+    the all-equal-stamps case (deltaT = 0 -> 1); the normalised grid within 1e-6 of max|v|."""
+    g = load("g_voxel_mvsec")
+    for t in "abc":
+        M, C, H, W = (int(v) for v in g[f"meta_{t}"])
+        assert bit_equal(oracle.voxel_grid_tbilinear(g[f"ev_{t}"], C, H, W, False), g[f"raw_{t}"]), t
+        n, ref = oracle.voxel_grid_tbilinear(g[f"ev_{t}"], C, H, W, True), g[f"norm_{t}"]
+        assert np.abs(n - ref).max() <= 1e-6 * np.abs(ref).max(), t
+
+
 def test_oracle_voxel_grid_matches_reference_golden():
     """DSEC event -> voxel grid (utils/dsec_utils.py:26-64) restated in C: the raw grid is
     bit-identical to the reference (single-threaded, as main.py:2-5 runs it); the normalised

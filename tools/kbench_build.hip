@@ -1,18 +1,23 @@
-// kbench_build.hip — A/B timing of corr_build tile geometries in ONE process, variants
-// interleaved round-robin (cdna_hip_programming.md §5.4 rule 24: cross-process / cross-device
-// variance otherwise dominates), random data.  Every variant must be bit-identical to the
-// first (same k-order) — checked on device.
+// kbench_build.hip — the f16x3 build (corr_build_split.hip) against the exact-fp32 MFMA build
+// (corr_build.hip) and the round-1 f16x3 kernel (tools/legacy/build_split_r01.hip):
+//   * accuracy: max |x - f32| / max |f32| over every pyramid level, three operand scales;
+//   * pooling: levels 1-3 bit-identical to avg_pool2d of the kernel's own level 0 (host check);
+//   * timing: interleaved rounds of every variant in one process, random data (HIP events
+//     around PER back-to-back launches; cdna_hip_programming.md §5.4 rule 24).
 //
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -o kbench_build tools/kbench_build.hip
-//   ./kbench_build [rounds]
+//   hipcc --offload-arch=gfx950 -O3 -std=c++20 -ffp-contract=off -o tools/_build/kbench_build tools/kbench_build.hip
+//   ./kbench_build [rounds] [shape]
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <string>
 #include <vector>
 
 #include "../e-raft_amd/csrc/corr_build.hip"
+#include "../e-raft_amd/csrc/corr_build_split.hip"
+#include "legacy/build_split_r01.hip"
 
 using namespace corr;
 
@@ -25,19 +30,24 @@ using namespace corr;
         }                                                                                     \
     } while (0)
 
-__global__ void fill(float *p, size_t n, unsigned seed) {
+__global__ void fill(float *p, size_t n, unsigned seed, float scale) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         unsigned x = (unsigned)i * 2654435761u ^ seed;
-        x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
-        p[i] = ((x >> 8) * (1.0f / 16777216.0f)) * 2.0f - 1.0f;
+        x ^= x >> 13;
+        x *= 0x5bd1e995u;
+        x ^= x >> 15;
+        p[i] = (((x >> 8) * (1.0f / 16777216.0f)) * 2.0f - 1.0f) * scale;
     }
 }
 
-__global__ void count_diff(const float *a, const float *b, size_t n, unsigned long long *cnt) {
-    unsigned long long c = 0;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        c += (__float_as_uint(a[i]) != __float_as_uint(b[i]));
-    if (c) atomicAdd(cnt, c);
+__global__ void maxdiff(const float *a, const float *b, size_t n, unsigned *dmax, unsigned *rmax) {
+    float d = 0.f, r = 0.f;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        d = fmaxf(d, fabsf(a[i] - b[i]));
+        r = fmaxf(r, fabsf(a[i]));
+    }
+    atomicMax(dmax, __float_as_uint(d));
+    atomicMax(rmax, __float_as_uint(r));
 }
 
 struct Shape {
@@ -47,70 +57,139 @@ struct Shape {
 
 struct Variant {
     std::string name;
-    std::function<hipError_t(float *)> launch;  // writes the pyramid rooted at the argument
+    std::function<hipError_t(float *)> launch;
+    bool has_output;
     std::vector<float> us;
 };
 
-template <class Cfg>
-static Variant make(const char *name, const Shape &sh, const float *f1, const float *f2, const size_t *off) {
-    Variant v;
-    char buf[128];
-    snprintf(buf, sizeof buf, "%-26s thr %4d LDS %6zu", name, Cfg::NT, Cfg::LDS);
-    v.name = buf;
-    v.launch = [=](float *base) {
-        LevelPtrs lp{};
-        for (int l = 0; l < 4; ++l) lp.p[l] = base + off[l];
-        return launch_build_cfg<Cfg>(f1, sh.H * sh.W, f2, sh.B, sh.D, sh.H, sh.W, 4, lp, 0);
-    };
-    return v;
+static float pool_host(float a, float b, float c, float d) {
+    volatile float t = a + b;
+    t = t + c;
+    t = t + d;
+    return t * 0.25f;
 }
 
 int main(int argc, char **argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 20;
-    constexpr int PER = 4;  // launches per timing sample
-    std::vector<Shape> shapes = {{"dsec", 1, 256, 60, 80},
-                                 {"mvsec-pad", 16, 256, 36, 44},
-                                 {"train", 8, 256, 36, 48},
-                                 {"1280x960", 1, 256, 120, 160}};
+    const char *only = argc > 2 ? argv[2] : nullptr;
+    const char *vfilter = argc > 3 ? argv[3] : nullptr;  // time only variants containing this
+    constexpr int PER = 4;
+    std::vector<Shape> shapes = {{"dsec", 1, 256, 60, 80},     {"mvsec-pad", 16, 256, 36, 44},
+                                 {"mvsec-crop", 16, 256, 32, 32}, {"train", 8, 256, 36, 48},
+                                 {"odd", 2, 200, 17, 23},      {"1280x960", 1, 256, 120, 160},
+                                 {"1920x1280", 1, 256, 160, 240}};
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (const Shape &sh : shapes) {
+        if (only && strcmp(only, "all") && strcmp(only, sh.name)) continue;
         const size_t N = (size_t)sh.H * sh.W, BN = (size_t)sh.B * N;
-        static size_t off[4];
-        size_t tot = 0;
+        size_t off[4], cnt[4], tot = 0;
         for (int l = 0; l < 4; ++l) {
             off[l] = tot;
-            tot += (BN * (sh.H >> l) * (sh.W >> l) + 3) / 4 * 4;
+            cnt[l] = BN * (sh.H >> l) * (sh.W >> l);
+            tot += (cnt[l] + 3) / 4 * 4;
         }
         const size_t fe = (size_t)sh.B * sh.D * N;
         float *f1, *f2, *ref, *out;
+        void *ws, *ws1;
+        const size_t wsb = build_split_workspace(sh.B, sh.D, (int)N, sh.H, sh.W);
+        const size_t wsb1 = r01::build_split_workspace(sh.B, sh.D, (int)N, sh.H, sh.W);
         CK(hipMalloc(&f1, fe * 4));
         CK(hipMalloc(&f2, fe * 4));
         CK(hipMalloc(&ref, tot * 4));
         CK(hipMalloc(&out, tot * 4));
-        hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f1, fe, 1u);
-        hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f2, fe, 2u);
+        CK(hipMalloc(&ws, wsb));
+        CK(hipMalloc(&ws1, wsb1));
+        auto lp_of = [&](float *base) {
+            LevelPtrs lp{};
+            for (int l = 0; l < 4; ++l) lp.p[l] = base + off[l];
+            return lp;
+        };
+        const int NQ = (int)N;
         std::vector<Variant> vs;
-        vs.push_back(make<BuildCfg<2, 2, 2, 32, 2, false, false>>("v0  BK32 o2 noPF noSKIP", sh, f1, f2, off));
-        vs.push_back(make<BuildCfg<2, 2, 2, 8, 4, true, false>>("P8  BK8 o4 PF noSKIP", sh, f1, f2, off));
-        vs.push_back(make<BuildCfg<2, 2, 2, 8, 4, true, true>>("P8S BK8 o4 PF SKIP", sh, f1, f2, off));
-        vs.push_back(make<BuildCfg<2, 2, 2, 16, 4, true, true>>("P16S BK16 o4 PF SKIP", sh, f1, f2, off));
-        vs.push_back(make<BuildCfg<2, 2, 1, 16, 5, true, true>>("J16S QT1 BK16 o5 PF SKIP", sh, f1, f2, off));
-        vs.push_back(make<BuildCfg<4, 2, 2, 16, 2, true, true>>("H16S 8w BK16 o2 PF SKIP", sh, f1, f2, off));
-        vs.push_back(make<BuildCfg<2, 2, 2, 16, 3, false, true>>("D16S BK16 o3 noPF SKIP", sh, f1, f2, off));
-        CK(vs[0].launch(ref));
-        for (auto &v : vs) {  // warm + correctness
-            CK(hipMemset(out, 0, tot * 4));
-            CK(v.launch(out));
-            CK(hipDeviceSynchronize());
-            unsigned long long *d, diff = 0;
-            CK(hipMalloc(&d, sizeof(*d)));
-            CK(hipMemset(d, 0, sizeof(*d)));
-            hipLaunchKernelGGL(count_diff, dim3(2048), dim3(256), 0, 0, ref, out, tot, d);
-            CK(hipMemcpy(&diff, d, sizeof(diff), hipMemcpyDeviceToHost));
-            CK(hipFree(d));
-            if (diff) printf("!! %s differs from v0 in %llu elements\n", v.name.c_str(), diff);
+        vs.push_back({"f32 build (corr_build.hip)", [&](float *o) {
+                          return launch_build_cfg<BuildDefault>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
+                      }, true});
+        vs.push_back({"r01 x3 pack+mfma", [&](float *o) {
+                          return r01::launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws1, 0);
+                      }, true});
+        vs.push_back({"x3 pack+mfma", [&](float *o) {
+                          return launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
+                      }, true});
+        vs.push_back({"x3 pack only", [&](float *) {
+                          return launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0);
+                      }, false});
+        vs.push_back({"x3 mfma only", [&](float *o) {
+                          return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
+                      }, false});
+        vs.push_back({"x3 mfma NOSTORE", [&](float *o) {
+                          return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), ws, 0);
+                      }, false});
+        vs.push_back({"x3 mfma L0tiled", [&](float *o) {
+                          return launch_split_mfma<4>(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
+                      }, false});
+        vs.push_back({"x3 mfma L0only", [&](float *o) {
+                          return launch_split_mfma<8>(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
+                      }, false});
+        vs.push_back({"x3 mfma L0tiled only", [&](float *o) {
+                          return launch_split_mfma<12>(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
+                      }, false});
+        vs.push_back({"x3 mfma NOSTORE noDMA", [&](float *o) {
+                          return launch_split_mfma<1>(NQ, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), ws, 0);
+                      }, false});
+        vs.push_back({"x3 mfma NOSTORE noQ", [&](float *o) {
+                          return launch_split_mfma<2>(NQ, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), ws, 0);
+                      }, false});
+        vs.push_back({"x3 mfma NOSTORE noDMA noQ", [&](float *o) {
+                          return launch_split_mfma<3>(NQ, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), ws, 0);
+                      }, false});
+        for (float sc : {1.0f, 1e-3f, 300.0f}) {
+            hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f1, fe, 1u, sc);
+            hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f2, fe, 2u, sc);
+            CK(vs[0].launch(ref));
+            for (size_t k = 1; k < vs.size(); ++k) {
+                if (!vs[k].has_output) continue;
+                CK(hipMemset(out, 0xff, tot * 4));
+                CK(vs[k].launch(out));
+                unsigned *d;
+                unsigned hv[2] = {0, 0};
+                CK(hipMalloc(&d, 8));
+                CK(hipMemset(d, 0, 8));
+                hipLaunchKernelGGL(maxdiff, dim3(2048), dim3(256), 0, 0, ref, out, tot, d, d + 1);
+                CK(hipMemcpy(hv, d, 8, hipMemcpyDeviceToHost));
+                CK(hipFree(d));
+                float dm, rm;
+                std::memcpy(&dm, &hv[0], 4);
+                std::memcpy(&rm, &hv[1], 4);
+                printf("%-10s scale %-6g %-28s max|x-f32|/max|f32| = %.3e\n", sh.name, sc, vs[k].name.c_str(), dm / rm);
+            }
+        }
+        {  // pooling of the new kernel: every level bit-identical to avg_pool2d of its own level 0
+            CK(launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), ws, 0));
+            std::vector<float> h(tot);
+            CK(hipMemcpy(h.data(), out, tot * 4, hipMemcpyDeviceToHost));
+            size_t bad = 0;
+            for (int l = 1; l < 4; ++l) {
+                const int Hp = sh.H >> (l - 1), Wp = sh.W >> (l - 1), Hl = sh.H >> l, Wl = sh.W >> l;
+                const float *P = h.data() + off[l - 1], *C = h.data() + off[l];
+                for (size_t q = 0; q < BN; ++q)
+                    for (int y = 0; y < Hl; ++y)
+                        for (int x = 0; x < Wl; ++x) {
+                            const float *a = P + q * Hp * Wp + (2 * y) * Wp + 2 * x;
+                            const float e = pool_host(a[0], a[1], a[Wp], a[Wp + 1]);
+                            const float g = C[q * Hl * Wl + y * Wl + x];
+                            if (std::memcmp(&e, &g, 4)) ++bad;
+                        }
+            }
+            printf("%-10s pooling levels 1-3 vs own level 0: %s (%zu mismatches)\n", sh.name,
+                   bad ? "DIFFER" : "bit-identical", bad);
+        }
+        if (vfilter) {
+            std::vector<Variant> keep;
+            for (auto &v : vs)
+                if (v.name.find(vfilter) != std::string::npos) keep.push_back(v);
+            vs = keep;
         }
         for (int r = 0; r < rounds; ++r)
             for (auto &v : vs) {
@@ -126,13 +205,17 @@ int main(int argc, char **argv) {
         for (auto &v : vs) {
             std::sort(v.us.begin(), v.us.end());
             const float med = v.us[v.us.size() / 2];
-            printf("%-10s %s  median %8.2f us  min %8.2f us  %6.1f TF/s\n", sh.name, v.name.c_str(), med, v.us[0],
-                   flops / (med * 1e-6) / 1e12);
+            printf("%-10s %-28s median %8.2f us  min %8.2f us  %7.1f TF/s fp32-equiv  %6.3f of 2.5 PF f16 pipe (x3)\n",
+                   sh.name, v.name.c_str(), med, v.us[0], flops / (med * 1e-6) / 1e12,
+                   3.0 * flops / (med * 1e-6) / 2.5e15);
         }
+        fflush(stdout);
         CK(hipFree(f1));
         CK(hipFree(f2));
         CK(hipFree(ref));
         CK(hipFree(out));
+        CK(hipFree(ws));
+        CK(hipFree(ws1));
     }
     return 0;
 }
