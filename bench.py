@@ -39,23 +39,28 @@ PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA (= vector)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec
 PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense BF16/F16 MFMA
 BUILD_ALGO = {0: "fp32", 1: "f16x3"}
-BUILD_KERNELS = {0: "corr_build_kernel", 1: "split_pack_reg_kernel+corr_build_split_kernel"}
+BUILD_KERNELS = {0: "corr_build_kernel", 1: "split_pack_kernel+corr_build_split_kernel"}
 BUILD_NOTE = {
-    0: "fp32 operands on v_mfma_f32_32x32x2_f32",
-    1: "fp32 product emulated on the f16 MFMA (per-pixel 2^e*(hi+lo) split, 3 MFMAs, fp32 "
-       "accumulate); achieved = algorithmic fp32 flops / (pack + MFMA kernel time) against the "
-       "fp32 MFMA peak, the executed f16 rate is in roofline_f16_pipe",
+    0: "fp32 operands on v_mfma_f32_32x32x2_f32: achieved = 2*B*N^2*D flops / build kernel time, "
+       "against the fp32 MFMA peak",
+    1: "fp32 product emulated on the f16 MFMA pipe (per-pixel 2^e*(hi+lo) split, 3 f16 MFMAs per "
+       "fp32 product, fp32 accumulate): achieved = EXECUTED f16 flops (3 * 2*B*N^2*D) / (pack + "
+       "MFMA kernel time), against the dense f16 MFMA peak; the fp32-equivalent rate is "
+       "fp32_equivalent_tflops",
 }
 
 WORKLOADS = {
     # name: (B, D, H, W, levels, radius, iters)
     "dsec": (1, 256, 60, 80, 4, 4, 12),
-    "mvsec": (16, 256, 36, 44, 4, 4, 12),
-    "hires1280": (1, 256, 120, 160, 4, 4, 12),
+    "mvsec": (16, 256, 36, 44, 4, 4, 12),        # config 3, 260x346 padded to 288x352
+    "mvsec_crop": (16, 256, 32, 32, 4, 4, 12),   # config 3, the eval's 256x256 centre crop
+    "hires1280": (1, 256, 120, 160, 4, 4, 12),   # 1280x960: the 1.47 GB volume
+    "hires1920": (1, 256, 160, 240, 4, 4, 12),   # config 5: 1920x1280, 5.9 GB volume
     # BASELINE config 4: training step, batch 8 at 288x384 crops -> CorrBlock forward AND
     # backward (grad w.r.t. both fmaps through all 12 lookups)
     "train": (8, 256, 36, 48, 4, 4, 12),
 }
+CPU_SKIP = {"hires1280", "hires1920"}  # a CPU pair takes tens of seconds and >10 GB
 TRAIN_WORKLOADS = {"train"}
 
 
@@ -116,15 +121,16 @@ def build_traffic(workload, algo):
     return None if any(x is None for x in t) else sum(t)
 
 
-def cpu_baseline(workload, budget_s, train=False):
-    """The reference op chain on torch CPU, all host cores, bounded sample.  train: plus the
-    autograd backward to both fmaps through the 12 lookups (upstream grads randn)."""
+def cpu_baseline(workload, budget_s, train=False, threads=None):
+    """The reference op chain on torch CPU, bounded sample.  threads: None = the job's host
+    cores (OMP_NUM_THREADS share), 1 = the reference eval's own setting (main.py:2-5).
+    train: plus the autograd backward to both fmaps through the 12 lookups (randn grads)."""
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     from oracle import torch_ops
 
     B, D, H, W, L, r, iters = workload
     # the GPU box exposes every host CPU but grants this job a share (OMP_NUM_THREADS)
-    cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+    cores = threads or int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
     prev = torch.get_num_threads()
     torch.set_num_threads(cores)
     g = torch.Generator().manual_seed(0)
@@ -286,6 +292,38 @@ def cpu_e2e(model, im1, im2, finit, iters, budget_s):
                       f"median {med * 1e3:.0f} ms"}
 
 
+def graph_time_ms(fn, stream, rep=10, trials=5):
+    """Median time of one call of fn: REP back-to-back calls captured in one HIP graph,
+    bracketed by HIP events on the launch stream (the graph-launch gap is amortised, so the
+    per-call figure is the kernels' own duration and agrees with rocprofv3's kernel trace)."""
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=stream):
+        for _ in range(rep):
+            fn()
+    times = []
+    for _ in range(trials):
+        a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        g.replay()
+        z.record(stream)
+        z.synchronize()
+        times.append(a.elapsed_time(z))
+    times.sort()
+    return times[len(times) // 2] / rep
+
+
+def build_roofline(algo, fl, bb, t_ms, traffic_b):
+    """The build kernel against the roofline of the pipe it runs on (see BUILD_NOTE)."""
+    executed = 3 * fl if algo == 1 else fl
+    peak = PEAK_F16_MFMA_TFLOPS if algo == 1 else PEAK_FP32_MFMA_TFLOPS
+    ach = executed / (t_ms * 1e-3) / 1e12
+    return {"bound": "mfma", "kernel": BUILD_KERNELS[algo], "achieved": round(ach, 2), "peak": peak,
+            "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic_b,
+            "avg_us": round(t_ms * 1e3, 2), "flops_per_launch": executed, "algorithmic_fp32_flops": fl,
+            "fp32_equivalent_tflops": round(fl / (t_ms * 1e-3) / 1e12, 2), "bytes_per_launch": bb,
+            "note": BUILD_NOTE[algo]}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -312,7 +350,13 @@ def main():
     wl = WORKLOADS[args.workload]
     B, D, H, W, L, r, iters = wl
     K = (2 * r + 1) ** 2
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    train = args.workload in TRAIN_WORKLOADS
+    sharded = args.sharded
+    if sharded and train:
+        raise SystemExit("--sharded times the forward path (build + lookups)")
+    # sharded: every rank draws the same pair (same seed); rank 0's fmap2 is what the broadcast
+    # carries.  replicas: each rank its own pair.
+    g = torch.Generator(device=dev).manual_seed(1234 if sharded else 1234 + rank)
     f1 = torch.randn(B, D, H, W, device=dev, generator=g)
     f2 = torch.randn(B, D, H, W, device=dev, generator=g)
     base = torch.stack(torch.meshgrid(torch.arange(H, device=dev), torch.arange(W, device=dev),
@@ -320,18 +364,8 @@ def main():
     coords = [(base + 0.5 * t * torch.randn(B, 2, H, W, device=dev, generator=g)).contiguous()
               for t in range(iters)]
 
-    # persistent buffers: pyramid + one output per lookup (as the GRU loop would consume them)
-    sharded = args.sharded
     if sharded:
-        # every rank draws the same pair (same seed); rank 0's fmap2 is what the broadcast carries
         from eraft_amd.sharded import _alloc_pyramid_rows, row_partition
-        if args.workload in TRAIN_WORKLOADS:
-            raise SystemExit("--sharded times the forward path (build + lookups)")
-        g = torch.Generator(device=dev).manual_seed(1234)
-        f1 = torch.randn(B, D, H, W, device=dev, generator=g)
-        f2 = torch.randn(B, D, H, W, device=dev, generator=g)
-        coords = [(base + 0.5 * t * torch.randn(B, 2, H, W, device=dev, generator=g)).contiguous()
-                  for t in range(iters)]
         h0, h1 = row_partition(H, world, rank)
         f1 = f1[:, :, h0:h1].contiguous()
         coords = [c[:, :, h0:h1].contiguous() for c in coords]
@@ -347,48 +381,68 @@ def main():
     def build_only():
         _lib.build(f1, f2, pyr, algo, ws)
 
-    def run_build():
-        if sharded and world > 1:
-            dist.broadcast(f2, src=0)  # RCCL over xGMI: fmap2 to every row shard
-        build_only()
+    def build_fp32():
+        _lib.build(f1, f2, pyr, _lib.BUILD_FP32, None)
 
     def run_lookups():
         for c, o in zip(coords, outs):
             _lib.lookup(pyr, c, r, o, H, W)
 
-    train = args.workload in TRAIN_WORKLOADS
     if train:
-        # backward of the 12 lookups + pyramid + product (eraft.py:128 detaches coords): one
-        # gradient pyramid accumulated by every lookup, folded once, then the two MFMA GEMMs
+        # backward of the 12 lookups + pyramid + product (eraft.py:128 detaches coords)
         gouts = [torch.randn(B, L * K, H, W, device=dev, generator=g) for _ in range(iters)]
         gpyr = _alloc_pyramid(B, H, W, L, f1, zero=True)
         gbuf = gpyr[0]._base  # the one allocation behind every level view
+        f1g = f1.clone().requires_grad_(True)
+        f2g = f2.clone().requires_grad_(True)
 
-        def run_bwd():
+        def run_bwd_kernels():  # the library calls alone, on a preallocated gradient pyramid
             gbuf.zero_()
             for c, go in zip(coords, gouts):
                 _lib.lookup_bwd(c, go, r, gpyr)
             _lib.pool_bwd(gpyr, H, W)
             return _lib.build_bwd(gpyr[0], f1, f2)
 
+        def autograd_step():  # what training runs: CorrBlock forward + loss.backward() to both fmaps
+            cb = CorrBlock(f1g, f2g, num_levels=L, radius=r)
+            outs_ = [cb(c) for c in coords]
+            torch.autograd.backward(outs_, gouts)
+            f1g.grad = None
+            f2g.grad = None
+
     stream = torch.cuda.Stream(device=dev)
+    bcast_ms = None
     with torch.cuda.stream(stream):
-        # first call through the public drop-in API (validates the same path end to end)
-        if not sharded:
-            cb = CorrBlock(f1, f2, num_levels=L, radius=r)
-            cb(coords[0])
-        run_build()
+        if not sharded:  # first call through the public drop-in API (validates the path)
+            CorrBlock(f1, f2, num_levels=L, radius=r)(coords[0])
+        build_only()
         run_lookups()
         torch.cuda.synchronize()
-        def pair():
-            run_build()
-            run_lookups()
-            if train:
-                run_bwd()
 
-        if args.eager or (sharded and world > 1):  # collectives stay out of graph capture
-            step = pair
-        else:
+        def pair():
+            if sharded and world > 1:
+                dist.broadcast(f2, src=0)  # RCCL over xGMI: fmap2 to every row shard
+            build_only()
+            run_lookups()
+
+        launch = "eager" if args.eager or (sharded and world > 1) else "hipgraph"
+        step = pair
+        if train:
+            step = autograd_step
+            try:  # the whole autograd step as one HIP graph (its allocations come from the pool)
+                for _ in range(2):
+                    autograd_step()
+                torch.cuda.synchronize()
+                if not args.eager:
+                    g_step = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g_step, stream=stream):
+                        autograd_step()
+                    step = g_step.replay
+            except Exception as exc:  # noqa: BLE001 — report and stay eager
+                print(f"train: graph capture of the autograd step failed ({exc}); eager", file=sys.stderr)
+                launch = "eager"
+                step = autograd_step
+        elif launch == "hipgraph":
             g_pair = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_pair, stream=stream):
                 pair()
@@ -398,77 +452,55 @@ def main():
             step()
         torch.cuda.synchronize()
 
-        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for k in range(args.steps):
-            ev[k][0].record(stream)
+        for _ in range(args.steps):
             step()
-            ev[k][1].record(stream)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         if world > 1:
             dist.barrier()
 
-        # Per-kernel durations on the launch stream: REP back-to-back launches of each kernel
-        # in one graph, bracketed by HIP events (amortises the graph-launch gap, so the average
-        # is the kernel's own duration and agrees with rocprofv3's kernel trace).
-        REP = 10
-        g_b, g_l = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_b, stream=stream):
-            for _ in range(REP):
-                build_only()
-        with torch.cuda.graph(g_l, stream=stream):
-            for _ in range(REP):
-                run_lookups()
-        kb, kl, kw = [], [], []
-        timed = [(g_b, kb), (g_l, kl)]
-        if train:
-            g_w = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_w, stream=stream):
-                for _ in range(REP):
-                    run_bwd()
-            timed.append((g_w, kw))
-        for _ in range(5):
-            for g, acc in timed:
+        # per-kernel durations on the launch stream (graph_time_ms)
+        build_ms = graph_time_ms(build_only, stream)
+        look_ms = graph_time_ms(run_lookups, stream) / iters
+        fp32_ms = graph_time_ms(build_fp32, stream, rep=4) if algo == _lib.BUILD_F16X3 else None
+        bwd_ms = graph_time_ms(run_bwd_kernels, stream, rep=4) if train else None
+        if sharded and world > 1:  # per-rank broadcast time (eager, events on the stream)
+            ts = []
+            for _ in range(5):
                 a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record(stream)
-                g.replay()
+                dist.broadcast(f2, src=0)
                 z.record(stream)
                 z.synchronize()
-                acc.append(a.elapsed_time(z))
-        kb.sort()
-        kl.sort()
-        kw.sort()
+                ts.append(a.elapsed_time(z))
+            bcast_ms = sorted(ts)[len(ts) // 2]
 
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    step_gpu_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
-    build_ms = kb[len(kb) // 2] / REP
-    look_ms = kl[len(kl) // 2] / (REP * iters)
 
     pairs = B * args.steps * (1 if sharded else world)
     value = pairs / elapsed
     fl = build_flops(B, D, H, W)
     lb = lookup_bytes(B, H, W, L, r)
+    bb = build_bytes(B, D, H, W, L)
     if sharded:  # per-rank kernels process the rank's slab (rank 0 owns the largest)
         frac_rows = (h1 - h0) / H
         fl *= frac_rows
         lb *= frac_rows
-    ach_tf = fl / (build_ms * 1e-3) / 1e12
-    look_gbs = lb / (look_ms * 1e-3) / 1e9
-    bb = build_bytes(B, D, H, W, L)
-    if sharded:
         lvn = sum((H >> l) * (W >> l) for l in range(L))
         bb = B * D * (h1 - h0 + H) * W * 4 + B * (h1 - h0) * W * lvn * 4
+    look_gbs = lb / (look_ms * 1e-3) / 1e9
     hbm_gbs = (bb + iters * lb) / (build_ms + iters * look_ms) / 1e6
 
     if rank == 0:
+        wl_name = args.workload
         res = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -482,48 +514,41 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (randn fmaps, coords_grid + randn flow), resident in HBM",
-            "config": {"workload": f"CorrBlock build + {iters} lookups{' + backward' if train else ''}, "
-                                   f"{args.workload} "
+            "config": {"workload": f"CorrBlock build + {iters} lookups"
+                                   f"{' + autograd backward to both fmaps' if train else ''}, {wl_name} "
                                    f"fmaps [{B},{D},{H},{W}], {L} levels, radius {r}",
-                       "global_batch": B * world, "launch": "eager" if args.eager else "hipgraph",
+                       "global_batch": B * (1 if sharded else world), "launch": launch,
                        "parallelism": (f"row-sharded x{world} (query rows of one pair per GPU, "
                                        "fmap2 RCCL broadcast)") if sharded else
                                       f"replicas x{world} (independent frame pairs per GPU)"},
             "build_algo": BUILD_ALGO[algo],
-            "roofline": {"bound": "mfma", "kernel": BUILD_KERNELS[algo],
-                         "achieved": round(ach_tf, 2), "peak": PEAK_FP32_MFMA_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(ach_tf / PEAK_FP32_MFMA_TFLOPS, 4),
-                         "traffic": build_traffic(args.workload, algo),
-                         "avg_us": round(build_ms * 1e3, 2), "flops_per_launch": fl,
-                         "bytes_per_launch": bb,
-                         "note": BUILD_NOTE[algo]},
+            "roofline": build_roofline(algo, fl, bb, build_ms, build_traffic(wl_name, algo)),
             "roofline_lookup": {"bound": "hbm", "kernel": "lookup_kernel",
                                 "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                 "frac": round(look_gbs / PEAK_HBM_GBS, 4),
-                                "traffic": traffic(args.workload, "lookup_kernel"),
+                                "traffic": traffic(wl_name, "lookup_kernel"),
                                 "avg_us": round(look_ms * 1e3, 3), "bytes_per_launch": lb},
-            **({"roofline_f16_pipe": {
-                "bound": "mfma", "executed_tflops": round(3 * ach_tf, 1), "peak": PEAK_F16_MFMA_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(3 * ach_tf / PEAK_F16_MFMA_TFLOPS, 4),
-                "note": "3 f16 MFMA products per fp32 product (hi*hi + hi*lo + lo*hi)"}}
-               if algo == _lib.BUILD_F16X3 else {}),
-            "kernel_timing": f"HIP events around {REP} back-to-back launches per graph on the "
-                             "launch stream, median of 5",
-            **({"backward": {
-                "phase": f"zero grad pyramid + {iters} lookup_bwd_kernel + pool_bwd + 2 MFMA GEMMs "
-                         "(dF1 = dC F2^T, dF2 = F1^T dC) + split-K reduce",
-                "avg_us": round(kw[len(kw) // 2] / REP * 1e3, 2),
-                "gemm_flops": 2 * fl,
-                "gemm_tflops_lower_bound": round(2 * fl / (kw[len(kw) // 2] / REP * 1e-3) / 1e12, 2),
-                "note": "whole backward phase time; per-kernel split in the rocprofv3 trace"}}
-               if train else {}),
-            "step_gpu_us": round(step_gpu_ms * 1e3, 2),
+            "kernel_timing": "HIP events around back-to-back launches in one HIP graph on the launch "
+                             "stream, median of 5",
             "hbm_gbs_algorithmic": round(hbm_gbs, 1),
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if fp32_ms is not None:  # the reference's own precision, beside the f16x3 default
+            res["build_fp32"] = build_roofline(0, fl, bb, fp32_ms, build_traffic(wl_name, 0))
+        if train:
+            res["backward_kernels"] = {
+                "phase": f"zero grad pyramid + {iters} lookup_bwd + pool_bwd + 2 split GEMMs "
+                         "(dF1 = dC F2^T, dF2 = F1^T dC), library calls alone",
+                "avg_us": round(bwd_ms * 1e3, 2), "gemm_flops": 2 * fl}
+            res["train_step_note"] = ("value times the autograd step through CorrBlock (forward, 12 "
+                                      "lookups, loss.backward() to both fmaps), as training runs it")
+        if bcast_ms is not None:
+            res["sharded_timing"] = {"broadcast_ms": round(bcast_ms, 4), "build_ms": round(build_ms, 4),
+                                     "lookup_ms": round(look_ms, 4), "rows": [h0, h1]}
+        if world == 1 and not args.no_cpu_baseline and wl_name not in CPU_SKIP:
             cb = cpu_baseline(wl, args.cpu_seconds, train)
             res["cpu_baseline"] = cb
             res["speedup_vs_cpu"] = round(value / cb["value"], 1)
+            res["cpu_baseline_1thread"] = cpu_baseline(wl, args.cpu_seconds * 0.75, train, threads=1)
         print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()

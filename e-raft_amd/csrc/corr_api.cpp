@@ -1,6 +1,8 @@
 // corr_api.cpp — the extern "C" boundary of libcorr_mi355x.so (declared in
 // include/corr_mi355x.h).  Validates arguments, records thread-local errors and forwards to
-// the gfx950 launchers.  No allocation, no synchronisation, no global mutable state.
+// the gfx950 launchers.  No allocation and no synchronisation.  Global state: the thread-local
+// error message, and per-kernel per-device "dynamic-LDS limit raised" bits (atomic, idempotent;
+// ensure_lds_limit in corr_build_common.h) — re-entrant across threads, streams and devices.
 //
 // The reference-shaped entry points (corr_build, corr_lookup, ...) are the row-slab
 // variants (corr_*_rows) with the slab = every query pixel (NQ = H*W).

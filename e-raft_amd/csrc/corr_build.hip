@@ -356,23 +356,15 @@ hipError_t launch_build_cfg(const float *f1, int NQ, const float *f2, int B, int
                      ((uintptr_t)f1 % 16 == 0) && ((uintptr_t)f2 % 16 == 0);
     const long tiles = (long)p.nq * p.npx * p.npy * B;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
-    static bool attr_set[2] = {false, false};
+    static std::atomic<unsigned long long> lds_done[2];
     if (vec) {
-        if (!attr_set[1]) {
-            hipError_t e = hipFuncSetAttribute((const void *)corr_build_kernel<Cfg, true>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
-            if (e != hipSuccess) return e;
-            attr_set[1] = true;
-        }
+        hipError_t e = ensure_lds_limit((const void *)corr_build_kernel<Cfg, true>, (int)Cfg::LDS, lds_done[1]);
+        if (e != hipSuccess) return e;
         hipLaunchKernelGGL((corr_build_kernel<Cfg, true>), dim3((unsigned)tiles), dim3(Cfg::NT),
                            Cfg::LDS, s, p);
     } else {
-        if (!attr_set[0]) {
-            hipError_t e = hipFuncSetAttribute((const void *)corr_build_kernel<Cfg, false>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)Cfg::LDS);
-            if (e != hipSuccess) return e;
-            attr_set[0] = true;
-        }
+        hipError_t e = ensure_lds_limit((const void *)corr_build_kernel<Cfg, false>, (int)Cfg::LDS, lds_done[0]);
+        if (e != hipSuccess) return e;
         hipLaunchKernelGGL((corr_build_kernel<Cfg, false>), dim3((unsigned)tiles), dim3(Cfg::NT),
                            Cfg::LDS, s, p);
     }

@@ -2,6 +2,7 @@
 // corr_build_split.hip: fp32 operands split into f16 pairs).  Internal, not part of the C-ABI.
 #pragma once
 
+#include <atomic>
 #include <cmath>
 
 #include "corr_common.h"
@@ -23,6 +24,20 @@ __device__ __forceinline__ float pool4(float a, float b, float c, float d) {
     t = t + c;
     t = t + d;
     return t * 0.25f;
+}
+
+// Raise a kernel's dynamic-LDS limit once per device: `done` holds one bit per device id, set
+// after a successful hipFuncSetAttribute (thread-safe; two threads racing both set the same
+// attribute, which is idempotent).  One `done` word per kernel instantiation.
+inline hipError_t ensure_lds_limit(const void *fn, int bytes, std::atomic<unsigned long long> &done) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (done.load(std::memory_order_acquire) & bit) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done.fetch_or(bit, std::memory_order_acq_rel);
+    return e;
 }
 
 // sqrt(D) is a power of two: x * (1/s) == x / s bit for bit.

@@ -448,18 +448,6 @@ int store_mode(int Wl, const float *base) {
     return 0;
 }
 
-// Per-device, thread-safe: raise a kernel's dynamic-LDS limit once per device.
-hipError_t ensure_lds_limit(const void *fn, int bytes, std::atomic<unsigned long long> &done) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    const unsigned long long bit = 1ull << (dev & 63);
-    if (done.load(std::memory_order_acquire) & bit) return hipSuccess;
-    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    if (e == hipSuccess) done.fetch_or(bit, std::memory_order_acq_rel);
-    return e;
-}
-
 }  // namespace
 
 size_t build_split_workspace(int B, int D, int NQ, int H, int W) {

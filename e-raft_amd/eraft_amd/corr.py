@@ -77,6 +77,8 @@ class _BuildFn(torch.autograd.Function):
         B, _, H, W = fmap1.shape
         levels = _alloc_pyramid(B, H, W, num_levels, fmap1)
         _lib.build(fmap1, fmap2, levels)
+        # the lookups read state.levels, not these outputs: no zero-filled level gradients
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(fmap1, fmap2)
         ctx.state = state
         token = fmap1.new_zeros(())  # autograd anchor: every lookup depends on it
@@ -152,12 +154,16 @@ class CorrBlock:
             _lib.build(fmap1.detach(), fmap2.detach(), self.corr_pyramid)
         self._state.levels = [p.detach() for p in self.corr_pyramid]
 
-    def __call__(self, coords):
+    def _check_coords(self, coords):
         if coords.dim() != 4 or coords.shape[1] != 2:
             raise ValueError(f"coords must be [B, 2, H, W] (got {tuple(coords.shape)})")
         B, _, H, W = coords.shape
         if B * H * W != self.corr_pyramid[0].shape[0] or (H, W) != (self._state.H, self._state.W):
             raise ValueError("coords do not match the feature maps this block was built from")
+
+    def __call__(self, coords):
+        self._check_coords(coords)
+        B, _, H, W = coords.shape
         # the reference accepts any strides (permute at corr.py:31); fp32 as in eraft.py:128
         coords = coords.detach().contiguous()
         if self._token is not None and torch.is_grad_enabled():
@@ -171,8 +177,13 @@ class CorrBlock:
         """Lookup fused with the motion encoder's first layer, relu(convc1(self(coords)))
         (update.py:68,75), without materialising the lookup output.  weight: convc1.weight
         [256, L*K, 1, 1]; bias [256].  Inference only (no autograd)."""
+        self._check_coords(coords)
         B, _, H, W = coords.shape
         K = (2 * self.radius + 1) ** 2
+        C = self.num_levels * K
+        if tuple(weight.shape) not in ((256, C, 1, 1), (256, C)) or tuple(bias.shape) != (256,):
+            raise ValueError(f"lookup_conv needs weight [256, {C}, 1, 1] and bias [256] "
+                             f"(got {tuple(weight.shape)}, {tuple(bias.shape)})")
         key = (weight.data_ptr(), weight._version)
         cached = getattr(self, "_wt_cache", None)
         if cached is None or cached[0] != key:  # transposed once per block, not per iteration

@@ -12,8 +12,13 @@ is O(N^2) (1920x1280: 5.9 GB per pair), so the build partitions the QUERY pixels
     [B, L*K, H, W] tensor when a replicated consumer needs it;
   * backward (training): every lookup's backward accumulates into the rank's gradient
     pyramid slab; the build's backward folds it and runs the two GEMMs on the slab, giving
-    the slab's dfmap1 rows (row-local, no exchange) and a PARTIAL dfmap2 (the slab's queries
-    only) -> one all-reduce (RCCL) of B*D*H*W floats per frame pair.
+    the slab's dfmap1 rows and a PARTIAL dfmap2 (the slab's queries only).  Gradient rule:
+    when every rank holds the FULL fmap1 (a replicated encoder, the default), both gradients
+    are SUM-all-reduced (RCCL, B*D*H*W floats each), so every rank ends with the single-GPU
+    dfmap1 and dfmap2 — the encoder's parameter gradients are then identical on all ranks and
+    equal to the single-GPU ones (DDP's averaging of identical values keeps them).  With
+    ``fmap1_is_slab=True`` (a row-sharded fmap1 producer) dfmap1 stays the rank's rows and only
+    dfmap2 is all-reduced.
 
 Per-query arithmetic is unchanged, so sharded results are bit-identical to one GPU.
 The compute goes through libcorr_mi355x.so's *_rows entry points (``HipRows`` below).
@@ -85,33 +90,41 @@ def _alloc_pyramid_rows(B, NQ, H, W, num_levels, like):
 
 
 class _ShardState:
-    __slots__ = ("levels", "grad_levels", "B", "NQ", "H", "W", "backend", "group")
+    __slots__ = ("levels", "grad_levels", "B", "NQ", "H", "W", "backend", "group", "h0", "h1", "full1")
 
 
 class _ShardBuildFn(torch.autograd.Function):
-    """Build of the rank's slab; backward = pool fold + slab GEMMs + all-reduce of dfmap2."""
+    """Build of the rank's slab; backward = pool fold + slab GEMMs + all-reduce of dfmap2 (and,
+    when fmap1 is the full replicated map, of the zero-padded dfmap1)."""
 
     @staticmethod
-    def forward(ctx, f1_rows, f2, num_levels, st):
+    def forward(ctx, f1, f2, num_levels, st):
+        f1_rows = f1[:, :, st.h0:st.h1].contiguous() if st.full1 else f1
         st.levels = st.backend.build(f1_rows, f2, num_levels) if st.NQ > 0 else None
         ctx.save_for_backward(f1_rows, f2)
-        ctx.st, ctx.num_levels = st, num_levels
-        return f1_rows.new_zeros(())  # autograd anchor of the lookups
+        ctx.st, ctx.num_levels, ctx.f1_shape = st, num_levels, tuple(f1.shape)
+        return f1.new_zeros(())  # autograd anchor of the lookups
 
     @staticmethod
     def backward(ctx, _):
         f1_rows, f2 = ctx.saved_tensors
         st = ctx.st
         gl, st.grad_levels = st.grad_levels, None
-        if gl is None:  # no lookup reached the loss on this rank
+        if gl is None and st.NQ > 0:  # no lookup reached the loss on this rank
             gl = st.backend.zero_pyramid(st.B, st.NQ, st.H, st.W, ctx.num_levels, f2)
         if st.NQ > 0:
             st.backend.pool_bwd(gl, st.H, st.W)
             df1, df2 = st.backend.build_bwd(gl[0], f1_rows, f2)
-        else:  # a rank without rows still joins the all-reduce
+        else:  # a rank without rows still joins the all-reduces
             df1, df2 = torch.zeros_like(f1_rows), torch.zeros_like(f2)
+        if st.full1:
+            full = df1.new_zeros(ctx.f1_shape)
+            full[:, :, st.h0:st.h1] = df1
+            df1 = full
         if dist.get_world_size(st.group) > 1:
             dist.all_reduce(df2, group=st.group)
+            if st.full1:
+                dist.all_reduce(df1, group=st.group)
         return df1, df2, None, None
 
 
@@ -162,17 +175,15 @@ class RowShardedCorrBlock:
         self.fmap2 = fmap2
         self._token = None
         if torch.is_grad_enabled() and (f1.requires_grad or fmap2.requires_grad):
-            # training: autograd through the slab; dfmap2 is all-reduced over `group`
+            # training: autograd through the slab; gradients all-reduced over `group` (module doc)
             st = _ShardState()
             st.B, st.NQ, st.H, st.W = B, (self.h1 - self.h0) * W, H, W
             st.backend, st.group, st.grad_levels, st.levels = backend, group, None, None
+            st.h0, st.h1, st.full1 = self.h0, self.h1, not fmap1_is_slab
             self._st = st
-            if self.h1 > self.h0:
-                self._token = _ShardBuildFn.apply(f1.contiguous(), fmap2, num_levels, st)
-                self.corr_pyramid = st.levels
-            else:
-                self._token = _ShardBuildFn.apply(f1, fmap2, num_levels, st)
-                self.corr_pyramid = None
+            src1 = fmap1 if st.full1 else f1.contiguous()
+            self._token = _ShardBuildFn.apply(src1, fmap2, num_levels, st)
+            self.corr_pyramid = st.levels if self.h1 > self.h0 else None
             return
         self.corr_pyramid = (backend.build(f1.contiguous(), fmap2, num_levels)
                              if self.h1 > self.h0 else None)

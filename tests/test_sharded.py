@@ -175,13 +175,73 @@ def test_row_sharded_training_grads(world, shape):
     cl = [prng.lookup_coords(10 + t, B, H, W, 3.0) for t in range(T)]
     gl = [prng.gauss(20 + t, (B, L * K, H, W)) for t in range(T)]
     rdf1, rdf2 = oracle.fmap_grads(f1, f2, cl, gl, L, r)
-    df1 = np.zeros_like(rdf1)
     for rank, h0, h1, g1, g2 in res:
-        assert not np.any(g1[:, :, :h0]) and not np.any(g1[:, :, h1:])  # row-local dfmap1
-        df1[:, :, h0:h1] = g1[:, :, h0:h1]
-        # every rank holds the all-reduced dfmap2
+        # full replicated fmap1: every rank holds the all-reduced (single-GPU) dfmap1 and dfmap2
+        assert np.abs(g1 - rdf1).max() <= 1e-5 * np.abs(rdf1).max()
         assert np.abs(g2 - rdf2).max() <= 1e-5 * np.abs(rdf2).max()
-    assert np.abs(df1 - rdf1).max() <= 1e-5 * np.abs(rdf1).max()
+
+
+def _encoder_worker(rank, world, port, shape, q):
+    """A shared (replicated) encoder produces both fmaps; after backward through the sharded
+    block every rank's parameter gradients must equal the single-GPU ones."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from eraft_amd.sharded import RowShardedCorrBlock, row_partition
+
+        B, D, H, W, L, r, T = shape
+        enc = _encoder(D)
+        im1, im2 = (torch.from_numpy(prng.gauss(s, (B, 3, H, W))) for s in (31, 32))
+        f1, f2 = enc(im1), enc(im2)
+        h0, h1 = row_partition(H, world, rank)
+        OracleRows.h0 = h0
+        blk = RowShardedCorrBlock(f1, f2, L, r, backend=OracleRows, broadcast=False)
+        loss = 0
+        for t in range(T):
+            c = torch.from_numpy(prng.lookup_coords(10 + t, B, H, W, 3.0))
+            g = torch.from_numpy(prng.gauss(20 + t, (B, L * (2 * r + 1) ** 2, H, W)))
+            loss = loss + (blk(c) * g[:, :, h0:h1]).sum()
+        loss.backward()
+        q.put((rank, [p.grad.numpy().copy() for p in enc.parameters()]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _encoder(D):
+    torch.manual_seed(5)
+    return torch.nn.Sequential(torch.nn.Conv2d(3, D, 3, padding=1), torch.nn.Tanh())
+
+
+def test_row_sharded_encoder_param_grads():
+    """with fmap1 and fmap2 from one shared encoder, the sharded backward gives every
+    rank the single-GPU parameter gradients (dfmap1 and dfmap2 both SUM-all-reduced)."""
+    from oracle import torch_ops
+    world, shape = 2, (1, 6, 10, 12, 3, 2, 2)
+    B, D, H, W, L, r, T = shape
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_encoder_worker, args=(g, world, port, shape, q)) for g in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    enc = _encoder(D)
+    im1, im2 = (torch.from_numpy(prng.gauss(s, (B, 3, H, W))) for s in (31, 32))
+    lv = torch_ops.cpu_build(enc(im1), enc(im2), L)
+    loss = 0
+    for t in range(T):
+        c = torch.from_numpy(prng.lookup_coords(10 + t, B, H, W, 3.0))
+        g = torch.from_numpy(prng.gauss(20 + t, (B, L * (2 * r + 1) ** 2, H, W)))
+        loss = loss + (torch_ops.cpu_lookup(lv, c, r) * g).sum()
+    loss.backward()
+    ref = [p.grad.numpy() for p in enc.parameters()]
+    for rank, grads in res:
+        for a, b in zip(grads, ref):
+            assert np.abs(a - b).max() <= 1e-5 * np.abs(b).max(), rank
 
 
 def test_row_partition_covers_rows():
