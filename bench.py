@@ -396,7 +396,10 @@ def main():
         f1g = f1.clone().requires_grad_(True)
         f2g = f2.clone().requires_grad_(True)
 
-        def run_bwd_kernels():  # the library calls alone, on a preallocated gradient pyramid
+        def run_bwd_kernels():  # corr_backward alone: all lookup backwards + fold + GEMMs
+            return _lib.backward(coords, gouts, r, gpyr, f1, f2)
+
+        def run_bwd_staged():  # round-1 sequence: zero + lookup_bwd per lookup + pool_bwd + GEMMs
             gbuf.zero_()
             for c, go in zip(coords, gouts):
                 _lib.lookup_bwd(c, go, r, gpyr)
@@ -468,6 +471,7 @@ def main():
         look_ms = graph_time_ms(run_lookups, stream) / iters
         fp32_ms = graph_time_ms(build_fp32, stream, rep=4) if algo == _lib.BUILD_F16X3 else None
         bwd_ms = graph_time_ms(run_bwd_kernels, stream, rep=4) if train else None
+        bwd_staged_ms = graph_time_ms(run_bwd_staged, stream, rep=4) if train else None
         if sharded and world > 1:  # per-rank broadcast time (eager, events on the stream)
             ts = []
             for _ in range(5):
@@ -536,9 +540,11 @@ def main():
             res["build_fp32"] = build_roofline(0, fl, bb, fp32_ms, build_traffic(wl_name, 0))
         if train:
             res["backward_kernels"] = {
-                "phase": f"zero grad pyramid + {iters} lookup_bwd + pool_bwd + 2 split GEMMs "
-                         "(dF1 = dC F2^T, dF2 = F1^T dC), library calls alone",
-                "avg_us": round(bwd_ms * 1e3, 2), "gemm_flops": 2 * fl}
+                "phase": f"corr_backward: {iters} lookup backwards in one launch + pool fold with dC "
+                         "row/column maxima + 2 split GEMMs (dF1 = dC F2^T, dF2 = F1^T dC), library call alone",
+                "avg_us": round(bwd_ms * 1e3, 2), "gemm_flops": 2 * fl,
+                "staged_avg_us": round(bwd_staged_ms * 1e3, 2),
+                "staged_phase": f"zero + {iters} lookup_bwd + pool_bwd + absmax + GEMMs (round-1 sequence)"}
             res["train_step_note"] = ("value times the autograd step through CorrBlock (forward, 12 "
                                       "lookups, loss.backward() to both fmaps), as training runs it")
         if bcast_ms is not None:

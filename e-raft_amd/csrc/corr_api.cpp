@@ -238,6 +238,67 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
                       fn);
 }
 
+int corr_lookup_bwd_multi(const float *const *coords_rows, const float *const *grad_out_rows, int T, int B, int NQ,
+                          int H, int W, int levels, int radius, float *const *grad_pyr, void *stream) {
+    static const char *fn = "corr_lookup_bwd_multi";
+    g_err[0] = 0;
+    int rc = check_dims(fn, B, NQ, H, W, levels);
+    if (rc || (rc = check_radius(fn, radius))) return rc;
+    if (T < 0) return fail(CORR_EINVAL, "%s: T must be >= 0 (got %d)", fn, T);
+    if (T > 0 && (!coords_rows || !grad_out_rows)) return fail(CORR_EINVAL, "%s: coords / grad_out arrays are NULL", fn);
+    for (int t = 0; t < T; ++t)
+        if ((rc = check_ptr(fn, coords_rows[t], "coords[t]")) || (rc = check_ptr(fn, grad_out_rows[t], "grad_out[t]")))
+            return rc;
+    LevelPtrs lp{};
+    if ((rc = check_levels(fn, grad_pyr, levels, "grad_pyr", lp.p))) return rc;
+    return hip_status(launch_lookup_bwd_multi(coords_rows, grad_out_rows, T, B, NQ, H, W, levels, radius, lp,
+                                              (hipStream_t)stream),
+                      fn);
+}
+
+int corr_pool_fold(float *const *grad_pyr, int B, int NQ, int H, int W, int levels, void *stream) {
+    static const char *fn = "corr_pool_fold";
+    g_err[0] = 0;
+    int rc = check_dims(fn, B, NQ, H, W, levels);
+    if (rc) return rc;
+    LevelPtrs lp{};
+    if ((rc = check_levels(fn, grad_pyr, levels, "grad_pyr", lp.p))) return rc;
+    return hip_status(launch_pool_fold(lp, B, NQ, H, W, levels, nullptr, 1, (hipStream_t)stream), fn);
+}
+
+size_t corr_backward_workspace(int algo, int B, int D, int NQ, int H, int W) {
+    return corr_build_bwd_ex_workspace(algo, B, D, NQ, H, W);
+}
+
+int corr_backward(int algo, const float *const *coords_rows, const float *const *grad_out_rows, int T,
+                  const float *fmap1_rows, int NQ, const float *fmap2, int B, int D, int H, int W, int levels,
+                  int radius, float *const *grad_pyr, float *dfmap1_rows, float *dfmap2, void *workspace,
+                  size_t workspace_bytes, void *stream) {
+    static const char *fn = "corr_backward";
+    g_err[0] = 0;
+    if (algo != CORR_BUILD_FP32 && algo != CORR_BUILD_F16X3)
+        return fail(CORR_EUNSUPPORTED, "%s: unknown algorithm %d", fn, algo);
+    int rc = check_dims(fn, B, NQ, H, W, levels);
+    if (rc || (rc = check_radius(fn, radius))) return rc;
+    if (D < 1) return fail(CORR_EINVAL, "%s: D must be >= 1 (got %d)", fn, D);
+    if (T < 0) return fail(CORR_EINVAL, "%s: T must be >= 0 (got %d)", fn, T);
+    if (T > 0 && (!coords_rows || !grad_out_rows)) return fail(CORR_EINVAL, "%s: coords / grad_out arrays are NULL", fn);
+    for (int t = 0; t < T; ++t)
+        if ((rc = check_ptr(fn, coords_rows[t], "coords[t]")) || (rc = check_ptr(fn, grad_out_rows[t], "grad_out[t]")))
+            return rc;
+    if ((rc = check_ptr(fn, fmap1_rows, "fmap1")) || (rc = check_ptr(fn, fmap2, "fmap2")) ||
+        (rc = check_ptr(fn, dfmap1_rows, "dfmap1")) || (rc = check_ptr(fn, dfmap2, "dfmap2")))
+        return rc;
+    const size_t need = corr_build_bwd_ex_workspace(algo, B, D, NQ, H, W);
+    if (workspace_bytes < need || (need && !workspace))
+        return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
+    LevelPtrs lp{};
+    if ((rc = check_levels(fn, grad_pyr, levels, "grad_pyr", lp.p))) return rc;
+    return hip_status(launch_backward(algo, coords_rows, grad_out_rows, T, fmap1_rows, NQ, fmap2, B, D, H, W, levels,
+                                      radius, lp, dfmap1_rows, dfmap2, workspace, (hipStream_t)stream),
+                      fn);
+}
+
 int corr_lookup_conv(const float *const *pyr, const float *coords, int B, int H, int W, int levels, int radius,
                      const float *weight_t, const float *bias, int relu, float *out, void *stream) {
     static const char *fn = "corr_lookup_conv";

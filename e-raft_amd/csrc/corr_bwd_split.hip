@@ -109,6 +109,156 @@ __global__ __launch_bounds__(256) void rowmax2_kernel(RowMaxArgs a) {
     if (lane == 0) a.rmax[t][(size_t)b * a.rows + r] = m > 0.f ? __float_as_uint(m) : 0u;
 }
 
+// avg_pool2d backward of the whole pyramid folded into level 0 IN PLACE, with the |max| of every
+// row and column of the result (autograd of model/corr.py:25-27; replaces corr_pool_bwd's
+// level-by-level passes + absmax_kernel's extra read of dC).  Per level-0 cell (y, x):
+//   G'_{L-1} = G_{L-1};  G'_{l}(p_l) = G_l(p_l) + G'_{l+1}(p_{l+1}) * 0.25 where p_{l+1} = p_l / 2
+//   lies in the pooled region (y_l < 2 H_{l+1}, x_l < 2 W_{l+1}) — exactly corr_pool_bwd's
+//   sequence of fine += coarse * 0.25, recomputed per cell (bit-identical).
+// Workgroup: kFoldQ query rows of one batch item x a chunk of columns; thread = kFoldU units of 4
+// consecutive level-0 cells (vec: W % 4 == 0 and 16-byte aligned levels -> one float4 of level 0,
+// one float2 of level 1 and one value of each coarser level per unit; otherwise per-cell loads).
+// Column maxima stay in registers over the rows (one atomicMax per column per workgroup); row
+// maxima are wave-reduced into LDS.  rmax is written (this block owns its rows); cmax must be
+// zeroed; both hold float bits (atomicMax on non-negative floats is exact).  NaN is dropped as
+// fmaxf drops it (absmax_kernel's convention).
+constexpr int kFoldQ = 32;
+constexpr int kFoldU = 2;
+constexpr int kFoldChunk = 256 * 4 * kFoldU;  // level-0 cells per column chunk
+
+struct FoldArgs {
+    float *g[CORR_MAX_LEVELS];
+    int L, NQ, H, W, vec;
+    unsigned *rmax, *cmax;  // [B][NQ], [B][H*W]; may be null
+};
+
+// Offset of cell (y, x)'s level-l ancestor in its query map, and the mask of levels l whose
+// cell receives from level l + 1.
+__device__ __forceinline__ void fold_cell_geom(int y, int x, int H, int W, int L, int (&off)[CORR_MAX_LEVELS],
+                                               unsigned &rc) {
+    rc = 0;
+#pragma unroll
+    for (int l = 0; l < CORR_MAX_LEVELS; ++l) {
+        const int Hl = H >> l, Wl = W >> l, yl = y >> l, xl = x >> l;
+        off[l] = yl * Wl + xl;
+        if (l + 1 < L && yl < 2 * (Hl >> 1) && xl < 2 * (Wl >> 1)) rc |= 1u << l;
+    }
+}
+
+// The fold of one cell from its per-level values, coarsest first (corr_pool_bwd's order).
+__device__ __forceinline__ float fold_cell(const float (&v)[CORR_MAX_LEVELS], unsigned rc, int L) {
+    float up = 0.f;
+    bool have = false;
+#pragma unroll
+    for (int l = CORR_MAX_LEVELS - 1; l >= 0; --l) {
+        if (l >= L) continue;
+        float gv = v[l];
+        if (have) gv = gv + up * 0.25f;  // fine += coarse * 0.25
+        up = gv;
+        have = l > 0 && ((rc >> (l - 1)) & 1u);
+    }
+    return up;
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void pool_fold_max_kernel(FoldArgs a) {
+    __shared__ unsigned rm[kFoldQ];
+    const int nqb = (a.NQ + kFoldQ - 1) / kFoldQ;
+    const int b = blockIdx.x / nqb, q0 = (blockIdx.x - b * nqb) * kFoldQ;
+    const int nq = min(kFoldQ, a.NQ - q0);
+    const int H = a.H, W = a.W, N = H * W, L = a.L;
+    const int tid = threadIdx.x, lane = tid & 63;
+    size_t msz[CORR_MAX_LEVELS];
+#pragma unroll
+    for (int l = 0; l < CORR_MAX_LEVELS; ++l) msz[l] = (size_t)(H >> l) * (W >> l);
+    if (tid < kFoldQ) rm[tid] = 0u;
+    __syncthreads();
+    for (int m0 = 0; m0 < N; m0 += kFoldChunk) {
+        // VEC: a unit's 4 cells share y and every level >= 2 ancestor; W % 4 == 0 so levels 0 and 1
+        // always receive in x, and the unit's receive mask is its first cell's.
+        int off[kFoldU][CORR_MAX_LEVELS];
+        unsigned rc[kFoldU];
+        bool live[kFoldU];
+#pragma unroll
+        for (int u = 0; u < kFoldU; ++u) {
+            const int m = m0 + 4 * (tid + 256 * u);
+            live[u] = m < N;
+            const int y = live[u] ? m / W : 0;
+            if (VEC) fold_cell_geom(y, m - y * W, H, W, L, off[u], rc[u]);
+        }
+        float cm[kFoldU][4];
+#pragma unroll
+        for (int u = 0; u < kFoldU; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cm[u][j] = 0.f;
+        for (int qq = 0; qq < nq; ++qq) {
+            const size_t qrow = (size_t)b * a.NQ + q0 + qq;
+            float rmx = 0.f;
+#pragma unroll
+            for (int u = 0; u < kFoldU; ++u) {
+                if (!live[u]) continue;
+                const int mu = m0 + 4 * (tid + 256 * u);
+                float res[4];
+                if (VEC) {
+                    float v[4][CORR_MAX_LEVELS];
+                    const float4 t0 = *reinterpret_cast<const float4 *>(a.g[0] + qrow * msz[0] + off[u][0]);
+                    v[0][0] = t0.x, v[1][0] = t0.y, v[2][0] = t0.z, v[3][0] = t0.w;
+                    if (L > 1) {
+                        const float2 t1 = *reinterpret_cast<const float2 *>(a.g[1] + qrow * msz[1] + off[u][1]);
+                        v[0][1] = v[1][1] = t1.x;
+                        v[2][1] = v[3][1] = t1.y;
+                    }
+#pragma unroll
+                    for (int l = 2; l < CORR_MAX_LEVELS; ++l)
+                        if (l < L) v[0][l] = v[1][l] = v[2][l] = v[3][l] = a.g[l][qrow * msz[l] + off[u][l]];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) res[j] = fold_cell(v[j], rc[u], L);
+                    *reinterpret_cast<float4 *>(a.g[0] + qrow * msz[0] + off[u][0]) =
+                        make_float4(res[0], res[1], res[2], res[3]);
+                } else {
+                    int mv = mu;
+                    asm volatile("" : "+v"(mv));  // recompute the geometry per row (hoisted it costs 160 VGPRs)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int m = mv + j;
+                        res[j] = 0.f;
+                        if (m >= N) continue;
+                        const int y = m / W;
+                        int o[CORR_MAX_LEVELS];
+                        unsigned r;
+                        fold_cell_geom(y, m - y * W, H, W, L, o, r);
+                        float v[CORR_MAX_LEVELS];
+#pragma unroll
+                        for (int l = 0; l < CORR_MAX_LEVELS; ++l) v[l] = l < L ? a.g[l][qrow * msz[l] + o[l]] : 0.f;
+                        res[j] = fold_cell(v, r, L);
+                        a.g[0][qrow * msz[0] + m] = res[j];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float av = fabsf(res[j]);
+                    cm[u][j] = fmaxf(cm[u][j], av);
+                    rmx = fmaxf(rmx, av);
+                }
+            }
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) rmx = fmaxf(rmx, __shfl_xor(rmx, o));
+            if (lane == 0 && rmx > 0.f) atomicMax(&rm[qq], __float_as_uint(rmx));
+        }
+        if (a.cmax) {
+#pragma unroll
+            for (int u = 0; u < kFoldU; ++u)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int m = m0 + 4 * (tid + 256 * u) + j;
+                    if (m < N && cm[u][j] > 0.f) atomicMax(&a.cmax[(size_t)b * N + m], __float_as_uint(cm[u][j]));
+                }
+        }
+    }
+    __syncthreads();
+    if (a.rmax && tid < nq) a.rmax[(size_t)b * a.NQ + q0 + tid] = rm[tid];
+}
+
 // Exponent of a row from its max (as split_pack_kernel): max * 2^s < 2^15.
 __device__ __forceinline__ int split_shift(float mm) {
     int s = 0;
@@ -509,18 +659,15 @@ size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W) {
            slab_floats(B, D, NQ, N) * sizeof(float);
 }
 
-// grad_c [B][NQ][N]; f1 [B][D][NQ]; f2 [B][D][N].
-hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, const float *f2, int B, int D, int H,
-                                  int W, float *df1, float *df2, void *ws, hipStream_t s) {
+// The GEMMs once dC's row maxima (w.mxB) and column maxima (w.mxC) are in the workspace.
+hipError_t bwd_split_gemms(const float *grad_c, const float *f1, int NQ, const float *f2, int B, int D, int H, int W,
+                           float *df1, float *df2, const BwdWs &w, hipStream_t s) {
     const int N = H * W;
     const float sD = std::sqrt((float)D);
-    const BwdWs w = carve(ws, B, D, NQ, N);
     hipError_t e;
 #define CK_(x)                          \
     if ((e = (x)) != hipSuccess) return e;
     // dF1 = F2 . dC^T : A = F2 rows d (k = m), B = dC rows n (k = m)
-    CK_(hipMemsetAsync(w.mx0, 0, w.mx_bytes, s));
-    CK_(absmax(grad_c, B, NQ, N, w.mxB, w.mxC, s));  // one pass: dC row and column maxima
     CK_(rowmax2(f2, N, w.mxA, f1, NQ, w.mxA2, B, D, s));
     CK_(convert(f2, (long)D * N, N, 1, B, D, N, w.mxA, w.pkA, w.exA, s));
     CK_(convert(grad_c, (long)NQ * N, N, 1, B, NQ, N, w.mxB, w.pkB, w.exB, s));
@@ -531,6 +678,73 @@ hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, 
     CK_(gemm(w, B, D, N, NQ, sD, df2, s));
 #undef CK_
     return hipSuccess;
+}
+
+// grad_c [B][NQ][N]; f1 [B][D][NQ]; f2 [B][D][N].
+hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, const float *f2, int B, int D, int H,
+                                  int W, float *df1, float *df2, void *ws, hipStream_t s) {
+    const int N = H * W;
+    const BwdWs w = carve(ws, B, D, NQ, N);
+    hipError_t e = hipMemsetAsync(w.mx0, 0, w.mx_bytes, s);
+    if (e == hipSuccess) e = absmax(grad_c, B, NQ, N, w.mxB, w.mxC, s);  // one pass: dC row and column maxima
+    if (e != hipSuccess) return e;
+    return bwd_split_gemms(grad_c, f1, NQ, f2, B, D, H, W, df1, df2, w, s);
+}
+
+// The pool-backward fold of a gradient pyramid into level 0 (in place); with `ws` (an F16X3
+// backward workspace) its row / column maxima land where bwd_split_gemms reads them.
+hipError_t launch_pool_fold(const LevelPtrs &gpyr, int B, int NQ, int H, int W, int levels, void *ws, int D,
+                            hipStream_t s) {
+    FoldArgs a{};
+    for (int l = 0; l < levels; ++l) a.g[l] = gpyr.p[l];
+    a.L = levels, a.NQ = NQ, a.H = H, a.W = W;
+    a.vec = W % 4 == 0 && ((uintptr_t)gpyr.p[0] & 15) == 0 && (levels < 2 || ((uintptr_t)gpyr.p[1] & 7) == 0);
+    if (ws) {
+        const BwdWs w = carve(ws, B, D, NQ, H * W);
+        hipError_t e = hipMemsetAsync(w.mx0, 0, w.mx_bytes, s);
+        if (e != hipSuccess) return e;
+        a.rmax = w.mxB, a.cmax = w.mxC;
+    }
+    const int nqb = (NQ + kFoldQ - 1) / kFoldQ;
+    if (a.vec)
+        hipLaunchKernelGGL(pool_fold_max_kernel<true>, dim3((unsigned)(nqb * B)), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(pool_fold_max_kernel<false>, dim3((unsigned)(nqb * B)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// The whole backward of one build and its T lookups (corr_backward): multi-lookup gradient
+// assembly into gpyr (overwritten), the fold with dC's maxima, then the two GEMMs.
+hipError_t launch_backward(int algo, const float *const *coords, const float *const *grad_out, int T,
+                           const float *f1, int NQ, const float *f2, int B, int D, int H, int W, int levels, int radius,
+                           const LevelPtrs &gpyr, float *df1, float *df2, void *ws, hipStream_t s) {
+    hipError_t e;
+    {  // fused: all lookups + the fold in one launch, dC and its maxima straight out of LDS
+        unsigned *rmax = nullptr, *cmax = nullptr;
+        BwdWs w{};
+        if (algo == CORR_BUILD_F16X3) {
+            w = carve(ws, B, D, NQ, H * W);
+            if ((e = hipMemsetAsync(w.mx0, 0, w.mx_bytes, s)) != hipSuccess) return e;
+            rmax = w.mxB, cmax = w.mxC;
+        }
+        e = launch_lookup_bwd_fold(coords, grad_out, T, B, NQ, H, W, levels, radius, gpyr.p[0], rmax, cmax, s);
+        if (e == hipSuccess) {
+            if (algo == CORR_BUILD_F16X3) return bwd_split_gemms(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, w, s);
+            return launch_build_bwd(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, (float *)ws, s);
+        }
+        if (e != hipErrorNotSupported) return e;
+        (void)hipGetLastError();
+    }
+    e = launch_lookup_bwd_multi(coords, grad_out, T, B, NQ, H, W, levels, radius, gpyr, s);
+    if (e != hipSuccess) return e;
+    if (algo == CORR_BUILD_F16X3) {
+        e = launch_pool_fold(gpyr, B, NQ, H, W, levels, ws, D, s);
+        if (e != hipSuccess) return e;
+        return bwd_split_gemms(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, carve(ws, B, D, NQ, H * W), s);
+    }
+    e = launch_pool_fold(gpyr, B, NQ, H, W, levels, nullptr, D, s);
+    if (e != hipSuccess) return e;
+    return launch_build_bwd(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, (float *)ws, s);
 }
 
 }  // namespace corr

@@ -37,6 +37,16 @@ hipError_t launch_lookup_bwd(const float *coords, const float *grad_out, int B, 
                              int W, int levels, int radius, const LevelPtrs &gpyr, hipStream_t s);
 hipError_t launch_pool_bwd(const LevelPtrs &gpyr, long BN, int H, int W, int levels,
                            hipStream_t s);
+hipError_t launch_lookup_bwd_multi(const float *const *coords, const float *const *grad_out, int T, int B, int NQ,
+                                   int H, int W, int levels, int radius, const LevelPtrs &gpyr, hipStream_t s);
+hipError_t launch_lookup_bwd_fold(const float *const *coords, const float *const *grad_out, int T, int B, int NQ,
+                                  int H, int W, int levels, int radius, float *dc, unsigned *rmax, unsigned *cmax,
+                                  hipStream_t s);
+hipError_t launch_pool_fold(const LevelPtrs &gpyr, int B, int NQ, int H, int W, int levels, void *ws, int D,
+                            hipStream_t s);
+hipError_t launch_backward(int algo, const float *const *coords, const float *const *grad_out, int T,
+                           const float *f1, int NQ, const float *f2, int B, int D, int H, int W, int levels, int radius,
+                           const LevelPtrs &gpyr, float *df1, float *df2, void *ws, hipStream_t s);
 // The f16-split build (corr_build_split.hip): pack kernel + f16 MFMA kernel, operands in `ws`.
 size_t build_split_workspace(int B, int D, int NQ, int H, int W);
 bool build_split_supported(int D);

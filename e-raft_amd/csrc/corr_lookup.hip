@@ -33,8 +33,12 @@
 // to its own map only, so there are no atomics and results are deterministic.  Irregular
 // workgroups fall back to a sequential per-query scatter in the same order.
 #include <cmath>
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <type_traits>
 
+#include "corr_build_common.h"
 #include "corr_common.h"
 
 namespace corr {
@@ -435,11 +439,20 @@ constexpr int kBwdQB = 64;  // queries per workgroup (32: 4 workgroups per CU bu
 // tap index), which reduces to the same four terms, in the same order, for regular taps.
 // Workgroups where some corner falls outside the (S+2)^2 neighbourhood (|coords| near 2^20)
 // take the sequential per-query scatter (wave 0, lane = query) of the previous design.
+// T lookups' (coords, upstream gradient) pairs of one build, processed in order by one launch
+// (corr_lookup_bwd_multi / corr_backward): zero = the workgroup first zeroes its queries' maps of
+// its level, so the gradient pyramid needs no separate memset and every lookup's RMW hits cells
+// this workgroup wrote moments before (L2-resident).  The single-lookup entry is T = 1, zero = 0.
+constexpr int kMaxLookups = 32;
+struct BwdLookups {
+    const float *coords[kMaxLookups];
+    const float *grad[kMaxLookups];
+    int T, zero;
+};
+
 template <int S, int BQ>
-__global__ __launch_bounds__(lookup_bwd_threads(S, BQ)) void lookup_bwd_kernel(const float *__restrict__ coords,
-                                                                           const float *__restrict__ grad_out,
-                                                                           int B, int NQ, int H, int W, int L,
-                                                                           LevelPtrs gpyr) {
+__global__ __launch_bounds__(lookup_bwd_threads(S, BQ)) void lookup_bwd_kernel(BwdLookups lk, int B, int NQ, int H,
+                                                                           int W, int L, LevelPtrs gpyr) {
     constexpr int R = (S - 1) / 2, K = S * S, NT = lookup_bwd_threads(S, BQ);
     using SM = LookupBwdSmem<S, BQ>;
     constexpr int WIN = SM::WIN, WS = WIN * WIN, WSTR = SM::WSTR;
@@ -462,6 +475,24 @@ __global__ __launch_bounds__(lookup_bwd_threads(S, BQ)) void lookup_bwd_kernel(c
     const int t = tid / BQ;  // tap in phase 1, neighbourhood column in phase 2
     const int n = n0 + q;
     const bool qok = n < N;
+
+    if (lk.zero) {  // this workgroup's query maps of level l (contiguous), before the first lookup
+        const size_t cells = (size_t)min(BQ, N - n0) * mapsz;
+        float *Z = G + qbase * mapsz;
+        for (size_t i = tid; i < cells; i += NT) Z[i] = 0.0f;
+        __syncthreads();
+    }
+    for (int lt = 0; lt < lk.T; ++lt) {
+    // constant-index selects (s_cselect): a dynamic index into the by-value table would copy it
+    // to scratch
+    const float *__restrict__ coords = lk.coords[0];
+    const float *__restrict__ grad_out = lk.grad[0];
+#pragma unroll
+    for (int k = 1; k < kMaxLookups; ++k)
+        if (k == lt) {
+            coords = lk.coords[k];
+            grad_out = lk.grad[k];
+        }
 
     // ---- 1. taps and the upstream gradient tile ----
     Axis a{}, c{};
@@ -555,6 +586,9 @@ __global__ __launch_bounds__(lookup_bwd_threads(S, BQ)) void lookup_bwd_kernel(c
         }
         __syncthreads();
         // ---- 3. coalesced read-modify-write of the query's cells ----
+        int tidv = tid;
+        asm volatile("" : "+v"(tidv));  // opaque per lookup: keeps the cell-index math out of the
+                                        // loop preheader (hoisted, it held ~120 VGPRs and spilled)
         auto rmw = [&](auto cc_tag) {
             constexpr int CC = decltype(cc_tag)::value;
             constexpr int CELLS = BQ * CC * CC;
@@ -564,7 +598,7 @@ __global__ __launch_bounds__(lookup_bwd_threads(S, BQ)) void lookup_bwd_kernel(c
             bool live[PER];
 #pragma unroll
             for (int u = 0; u < PER; ++u) {
-                const int item = tid + NT * u;
+                const int item = tidv + NT * u;
                 const int qq = item / (CC * CC);
                 const int e = item - qq * (CC * CC);
                 const int cy = e / CC, cx2 = e - cy * CC;
@@ -582,7 +616,8 @@ __global__ __launch_bounds__(lookup_bwd_threads(S, BQ)) void lookup_bwd_kernel(c
             rmw(std::integral_constant<int, C>{});
         else
             rmw(std::integral_constant<int, WIN>{});
-        return;
+        __syncthreads();  // the next lookup reuses the LDS and re-reads these cells
+        continue;
     }
 
     // ---- 2c. uncovered workgroup: sequential per-query scatter (wave 0, lane = query) ----
@@ -627,6 +662,299 @@ __global__ __launch_bounds__(lookup_bwd_threads(S, BQ)) void lookup_bwd_kernel(c
             *d = *d + sm.win[qq * WSTR + e];
         }
     }
+    __syncthreads();
+    }  // lookups
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused backward of one build's T lookups + the avg-pool backward (corr_backward's fast path).
+// A workgroup owns BQ query pixels and ALL (<= 4) levels of their gradient maps, resident in LDS
+// for the whole launch: zeroed, then every lookup's window sums are added in lookup order (the
+// same per-cell values as lookup_bwd_kernel: s = the cell's contributions of one lookup in the
+// reference's scatter order, then M = M + s), then the maps are folded coarse-to-fine into
+// level 0 (pool_fold_max_kernel's per-cell recurrence) and ONLY dC = level 0 is written, with
+// its row maxima (written) and column maxima (atomicMax).  The coarse levels never reach HBM and
+// no cell is read-modify-written in HBM: traffic = the upstream gradients + coords + dC.
+// Thread (q, l, cx) = query, level, neighbourhood column — phase 1 (cx < S: tap cx of both
+// axes + the upstream gradients of x-tap cx -> LDS) and phase 2 (its column's cells, added to
+// the LDS map; each cell of a query's window has one owner thread per lookup, so no atomics).
+// Every (query, level) picks its own form: closed form (regular taps), contiguous hit ranges
+// (irregular), or — when a corner leaves the (S+2)^2 neighbourhood — the sequential scatter,
+// run by the group's cx = 0 thread into a zeroed window scratch (cells outside the window
+// directly into the map), exactly as lookup_bwd_kernel's 2c path.
+constexpr int kFusedLv = 4;  // level slots per workgroup
+
+constexpr int fused_threads(int S, int BQ) { return (BQ * kFusedLv * (S + 2) + 63) / 64 * 64; }
+
+struct FusedOut {
+    float *dc;              // [B * NQ][H * W]
+    unsigned *rmax, *cmax;  // [B][NQ] (written), [B][H * W] (atomicMax; zeroed by the caller); may be null
+    int B, NQ, H, W, L;
+    int moff[kFusedLv], msz[kFusedLv];  // LDS float offset of level l's maps, cells per map
+    int aux;                            // LDS float offset of the per-lookup staging
+};
+
+__device__ __forceinline__ void pick_lookup(const BwdLookups &lk, int lt, const float *&c, const float *&g) {
+    c = lk.coords[0];
+    g = lk.grad[0];
+#pragma unroll
+    for (int k = 1; k < kMaxLookups; ++k)
+        if (k == lt) {
+            c = lk.coords[k];
+            g = lk.grad[k];
+        }
+}
+
+// Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2).  Renumber them so
+// every XCD gets a contiguous range: neighbouring query groups — which share the 128-B lines of
+// the upstream gradients and coords — then read those lines through one L2 instead of eight.
+// A bijection on [0, n) for any n.
+__device__ __forceinline__ int xcd_contiguous(int bid, int n) {
+    constexpr int kXcd = 8;
+    const int q = n / kXcd, r = n % kXcd;
+    const int x = bid % kXcd, k = bid / kXcd;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
+// LDS-only workgroup barrier: __syncthreads() also waits for every outstanding global load
+// (vmcnt(0)), which would expose the prefetch of the next lookup.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int S, int BQ>
+__global__ __launch_bounds__(fused_threads(S, BQ)) void lookup_bwd_fold_kernel(BwdLookups lk, FusedOut o) {
+    constexpr int R = (S - 1) / 2, K = S * S, C = S + 1, WIN = S + 2, WSTR = (WIN * WIN) | 1;
+    constexpr int NT = fused_threads(S, BQ);
+    extern __shared__ float fsm[];
+    float *TX = fsm + o.aux;                   // [lv][3][S][BQ]
+    float *TY = TX + kFusedLv * 3 * S * BQ;    // [lv][3][S][BQ]
+    float *GG = TY + kFusedLv * 3 * S * BQ;    // [lv][K][BQ]
+    float *WB = GG + kFusedLv * K * BQ;        // [lv][BQ][WSTR]
+    int *AX = reinterpret_cast<int *>(WB + kFusedLv * BQ * WSTR);  // [lv][BQ]
+    int *AY = AX + kFusedLv * BQ;
+    unsigned *RM = reinterpret_cast<unsigned *>(AY + kFusedLv * BQ);  // [BQ]
+    int *UF = reinterpret_cast<int *>(RM + BQ);                       // [2] "some group uncovered" per lookup parity
+
+    const int NQ = o.NQ, H = o.H, W = o.W, L = o.L, N = H * W;
+    const int nqb = (NQ + BQ - 1) / BQ;
+    const int blk = xcd_contiguous(blockIdx.x, gridDim.x);
+    const int b = blk / nqb, n0 = (blk - b * nqb) * BQ;
+    const int tid = threadIdx.x;
+    const int q = tid % BQ, lt = tid / BQ, l = lt / WIN, cx = lt - l * WIN;
+    const bool act = l < L;
+    const int n = n0 + q;
+    const bool qok = n < NQ;
+    const int lc = act ? l : 0;
+    const int Hl = H >> lc, Wl = W >> lc;
+    const float inv_scale = 1.0f / (float)(1 << lc);
+    const int msz = o.msz[lc];
+    float *M = fsm + o.moff[lc] + q * msz;  // this thread's (query, level) map
+    auto tx = [&](int c, int t) -> float & { return TX[((lc * 3 + c) * S + t) * BQ + q]; };
+    auto ty = [&](int c, int t) -> float & { return TY[((lc * 3 + c) * S + t) * BQ + q]; };
+    auto gg = [&](int k) -> float & { return GG[(lc * K + k) * BQ + q]; };
+
+    {  // zero every map (all levels, all queries of the workgroup)
+        const int total = o.aux;
+        for (int i = tid; i < total; i += NT) fsm[i] = 0.0f;
+        if (tid < BQ) RM[tid] = 0u;
+        if (tid < 2) UF[tid] = 0;
+    }
+    __syncthreads();
+
+    // the next lookup's coords and upstream gradients are loaded one lookup ahead (registers),
+    // so their latency hides behind the current lookup's LDS work.  Every thread loads (clamped,
+    // always-valid addresses) and non-loaders drop the values at use: no branch around the loads,
+    // so no copy at a control-flow join forces the compiler to wait for them.
+    const bool loader = act && cx < S && qok;
+    const int cxl = min(cx, S - 1), nl = min(n, NQ - 1);
+    float pcx, pcy, pv[S];
+    auto prefetch = [&](int t) {
+        const float *coords, *grad_out;
+        pick_lookup(lk, t, coords, grad_out);
+        pcx = coords[((size_t)b * 2 + 0) * NQ + nl];
+        pcy = coords[((size_t)b * 2 + 1) * NQ + nl];
+        const float *g = grad_out + (((size_t)b * L + lc) * K + (size_t)cxl * S) * NQ + nl;
+#pragma unroll
+        for (int u = 0; u < S; ++u) pv[u] = g[(size_t)u * NQ];
+    };
+    prefetch(0);
+
+    for (int t = 0; t < lk.T; ++t) {
+        // ---- 1. taps of x/y tap cx and the upstream gradients of x-tap cx ----
+        const float cxv = loader ? pcx : 0.0f, cyv = loader ? pcy : 0.0f;
+        float v[S];
+#pragma unroll
+        for (int u = 0; u < S; ++u) v[u] = loader ? pv[u] : 0.0f;
+        prefetch(min(t + 1, lk.T - 1));
+        if (act && cx < S) {
+            const Axis a = tap_axis(cxv, inv_scale, cx, R, Wl);
+            const Axis c = tap_axis(cyv, inv_scale, cx, R, Hl);
+            tx(0, cx) = a.f, tx(1, cx) = a.lo, tx(2, cx) = a.hi;
+            ty(0, cx) = c.f, ty(1, cx) = c.lo, ty(2, cx) = c.hi;
+            if (cx == 0) {
+                AX[lc * BQ + q] = anchor_of(a.f);
+                AY[lc * BQ + q] = anchor_of(c.f);
+            }
+#pragma unroll
+            for (int u = 0; u < S; ++u) gg(cx * S + u) = v[u];
+        }
+        lds_barrier();
+        // ---- 2. this column's cells of the (query, level) window, added to the LDS map ----
+        bool unc = false;
+        if (act && qok) {
+            const float fx0 = tx(0, 0), fy0 = ty(0, 0);
+            const bool far = anchor_of(fx0) == kFarAnchor || anchor_of(fy0) == kFarAnchor;
+            unc = !window_covers<S>(fx0, tx(0, S - 1), fy0, ty(0, S - 1));
+            bool reg = true;
+#pragma unroll
+            for (int i = 0; i < S; ++i) reg = reg && tx(0, i) - fx0 == (float)i && ty(0, i) - fy0 == (float)i;
+            const int X = AX[lc * BQ + q] + cx, Y0 = AY[lc * BQ + q];
+            if (!unc && !far && X >= 0 && X < Wl) {
+                if (reg) {
+                    if (cx < C) {
+                        float wlo = 0.f, whi = 0.f;
+                        if (cx < S) wlo = tx(1, cx);
+                        if (cx >= 1) whi = tx(2, cx - 1);
+                        float ylo[S], yhi[S], gp[S], gc[S];
+#pragma unroll
+                        for (int j = 0; j < S; ++j) {
+                            ylo[j] = ty(1, j);
+                            yhi[j] = ty(2, j);
+                            gp[j] = cx >= 1 ? gg((cx - 1) * S + j) : 0.f;
+                            gc[j] = cx < S ? gg(cx * S + j) : 0.f;
+                        }
+#pragma unroll
+                        for (int cy = 0; cy < C; ++cy) {
+                            float s = 0.0f;
+                            if (cx >= 1 && cy >= 1) s = s + __fmul_rn(gp[cy - 1], __fmul_rn(yhi[cy - 1], whi));  // se
+                            if (cx >= 1 && cy < S) s = s + __fmul_rn(gp[cy], __fmul_rn(ylo[cy], whi));           // ne
+                            if (cx < S && cy >= 1) s = s + __fmul_rn(gc[cy - 1], __fmul_rn(yhi[cy - 1], wlo));   // sw
+                            if (cx < S && cy < S) s = s + __fmul_rn(gc[cy], __fmul_rn(ylo[cy], wlo));            // nw
+                            const int Y = Y0 + cy;
+                            if (Y >= 0 && Y < Hl) M[Y * Wl + X] = M[Y * Wl + X] + s;
+                        }
+                    }
+                } else {
+                    float dy[S];
+#pragma unroll
+                    for (int j = 0; j < S; ++j) dy[j] = ty(0, j) - fy0;
+                    int i0 = 0, i1 = 0;
+#pragma unroll
+                    for (int i = 0; i < S; ++i) {
+                        const float d = tx(0, i) - fx0;
+                        i0 += d < (float)(cx - 1);
+                        i1 += d <= (float)cx;
+                    }
+                    for (int cy = 0; cy < WIN; ++cy) {
+                        int j0 = 0, j1 = 0;
+#pragma unroll
+                        for (int j = 0; j < S; ++j) {
+                            j0 += dy[j] < (float)(cy - 1);
+                            j1 += dy[j] <= (float)cy;
+                        }
+                        float s = 0.0f;
+                        for (int i = i0; i < i1; ++i) {
+                            const float wx = (tx(0, i) - fx0 == (float)cx) ? tx(1, i) : tx(2, i);
+                            for (int j = j0; j < j1; ++j) {
+                                const float wy = (ty(0, j) - fy0 == (float)cy) ? ty(1, j) : ty(2, j);
+                                s = s + __fmul_rn(gg(i * S + j), __fmul_rn(wy, wx));
+                            }
+                        }
+                        const int Y = Y0 + cy;
+                        if (Y >= 0 && Y < Hl) M[Y * Wl + X] = M[Y * Wl + X] + s;
+                    }
+                }
+            }
+        }
+        // ---- 2c. groups whose corners leave the neighbourhood: sequential scatter ----
+        if (unc) UF[t & 1] = 1;
+        if (tid == 0) UF[(t & 1) ^ 1] = 0;  // last read before the previous lookup's closing barrier
+        lds_barrier();
+        if (UF[t & 1]) {
+            float *wq = WB + (lc * BQ + q) * WSTR;
+            if (unc)
+                for (int e = cx; e < WSTR; e += WIN) wq[e] = 0.0f;
+            lds_barrier();
+            const int ax = AX[lc * BQ + q], ay = AY[lc * BQ + q];
+            if (unc && cx == 0) {
+                auto scatter = [&](float xf, float yf, float v) {
+                    if (!in_map(xf, yf, Wl, Hl)) return;
+                    const int xi = (int)xf, yi = (int)yf;
+                    const unsigned ux = (unsigned)(xi - ax), uy = (unsigned)(yi - ay);
+                    if (ux < (unsigned)WIN && uy < (unsigned)WIN)
+                        wq[uy * WIN + ux] += v;
+                    else
+                        M[yi * Wl + xi] += v;  // outside the neighbourhood: disjoint cells
+                };
+                for (int ii = 0; ii < S; ++ii) {
+                    const float x0 = tx(0, ii), x1 = __fadd_rn(x0, 1.0f);
+                    const float ex = tx(1, ii), wx = tx(2, ii);
+                    for (int j = 0; j < S; ++j) {
+                        const float gv = gg(ii * S + j);
+                        const float y0 = ty(0, j), y1 = __fadd_rn(y0, 1.0f);
+                        const float ey = ty(1, j), ny = ty(2, j);
+                        scatter(x0, y0, __fmul_rn(gv, __fmul_rn(ey, ex)));
+                        scatter(x1, y0, __fmul_rn(gv, __fmul_rn(ey, wx)));
+                        scatter(x0, y1, __fmul_rn(gv, __fmul_rn(ny, ex)));
+                        scatter(x1, y1, __fmul_rn(gv, __fmul_rn(ny, wx)));
+                    }
+                }
+            }
+            lds_barrier();
+            if (unc) {
+                const int X = ax + cx;
+                for (int ry = 0; ry < WIN; ++ry) {
+                    const int Y = ay + ry;
+                    if (X >= 0 && X < Wl && Y >= 0 && Y < Hl) M[Y * Wl + X] = M[Y * Wl + X] + wq[ry * WIN + cx];
+                }
+            }
+        }
+        lds_barrier();  // the next lookup reuses the staging
+    }
+
+    // ---- 3. fold into level 0, write dC with its row / column maxima ----
+    float rq[BQ];
+#pragma unroll
+    for (int k = 0; k < BQ; ++k) rq[k] = 0.f;
+    for (int m = tid; m < N; m += NT) {
+        const int y = m / W, x = m - y * W;
+        float cm = 0.f;
+        int off[kFusedLv];
+        unsigned rc = 0;
+#pragma unroll
+        for (int v = 0; v < kFusedLv; ++v) {
+            const int Hv = H >> v, Wv = W >> v, yv = y >> v, xv = x >> v;
+            off[v] = o.moff[v < L ? v : 0] + yv * Wv + xv;
+            if (v + 1 < L && yv < 2 * (Hv >> 1) && xv < 2 * (Wv >> 1)) rc |= 1u << v;
+        }
+#pragma unroll
+        for (int k = 0; k < BQ; ++k) {
+            if (n0 + k >= NQ) break;
+            float up = 0.f;
+            bool have = false;
+#pragma unroll
+            for (int v = kFusedLv - 1; v >= 0; --v) {
+                if (v >= L) continue;
+                float gv = fsm[off[v] + k * o.msz[v]];
+                if (have) gv = gv + up * 0.25f;  // fine += coarse * 0.25 (corr_pool_bwd order)
+                up = gv;
+                have = v > 0 && ((rc >> (v - 1)) & 1u);
+            }
+            o.dc[((size_t)b * NQ + n0 + k) * N + m] = up;
+            const float av = fabsf(up);
+            cm = fmaxf(cm, av);
+            rq[k] = fmaxf(rq[k], av);
+        }
+        if (o.cmax && cm > 0.f) atomicMax(&o.cmax[(size_t)b * N + m], __float_as_uint(cm));
+    }
+#pragma unroll
+    for (int k = 0; k < BQ; ++k) {
+        float r = rq[k];
+#pragma unroll
+        for (int sh = 32; sh >= 1; sh >>= 1) r = fmaxf(r, __shfl_xor(r, sh));
+        if ((tid & 63) == 0 && r > 0.f) atomicMax(&RM[k], __float_as_uint(r));
+    }
+    __syncthreads();
+    if (o.rmax && tid < BQ && n0 + tid < NQ) o.rmax[(size_t)b * NQ + n0 + tid] = RM[tid];
 }
 
 // avg_pool2d backward, one level: fine[q][y][x] += coarse[q][y/2][x/2] * 0.25 on the pooled
@@ -660,12 +988,27 @@ hipError_t launch_lookup_s(const ConstLevelPtrs &pyr, const float *coords, int B
 }
 
 template <int S>
-hipError_t launch_lookup_bwd_s(const float *coords, const float *grad_out, int B, int NQ, int H,
-                               int W, int L, const LevelPtrs &gpyr, hipStream_t s) {
+hipError_t launch_lookup_bwd_s(const BwdLookups &lk, int B, int NQ, int H, int W, int L, const LevelPtrs &gpyr,
+                               hipStream_t s) {
     const int nqb = (NQ + kBwdQB - 1) / kBwdQB;
     hipLaunchKernelGGL((lookup_bwd_kernel<S, kBwdQB>), dim3(nqb * B, L), dim3(lookup_bwd_threads(S, kBwdQB)), 0, s,
-                       coords, grad_out, B, NQ, H, W, L, gpyr);
+                       lk, B, NQ, H, W, L, gpyr);
     return hipGetLastError();
+}
+
+hipError_t launch_lookup_bwd_lk(const BwdLookups &lk, int B, int NQ, int H, int W, int levels, int radius,
+                                const LevelPtrs &gpyr, hipStream_t s) {
+    switch (radius) {
+        case 0: return launch_lookup_bwd_s<1>(lk, B, NQ, H, W, levels, gpyr, s);
+        case 1: return launch_lookup_bwd_s<3>(lk, B, NQ, H, W, levels, gpyr, s);
+        case 2: return launch_lookup_bwd_s<5>(lk, B, NQ, H, W, levels, gpyr, s);
+        case 3: return launch_lookup_bwd_s<7>(lk, B, NQ, H, W, levels, gpyr, s);
+        case 4: return launch_lookup_bwd_s<9>(lk, B, NQ, H, W, levels, gpyr, s);
+        case 5: return launch_lookup_bwd_s<11>(lk, B, NQ, H, W, levels, gpyr, s);
+        case 6: return launch_lookup_bwd_s<13>(lk, B, NQ, H, W, levels, gpyr, s);
+        case 7: return launch_lookup_bwd_s<15>(lk, B, NQ, H, W, levels, gpyr, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 }  // namespace
@@ -697,17 +1040,31 @@ hipError_t launch_lookup_conv(const ConstLevelPtrs &pyr, const float *coords, in
 
 hipError_t launch_lookup_bwd(const float *coords, const float *grad_out, int B, int NQ, int H,
                              int W, int levels, int radius, const LevelPtrs &gpyr, hipStream_t s) {
-    switch (radius) {
-        case 0: return launch_lookup_bwd_s<1>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
-        case 1: return launch_lookup_bwd_s<3>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
-        case 2: return launch_lookup_bwd_s<5>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
-        case 3: return launch_lookup_bwd_s<7>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
-        case 4: return launch_lookup_bwd_s<9>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
-        case 5: return launch_lookup_bwd_s<11>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
-        case 6: return launch_lookup_bwd_s<13>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
-        case 7: return launch_lookup_bwd_s<15>(coords, grad_out, B, NQ, H, W, levels, gpyr, s);
-        default: return hipErrorInvalidValue;
+    BwdLookups lk{};
+    lk.coords[0] = coords;
+    lk.grad[0] = grad_out;
+    lk.T = 1;
+    lk.zero = 0;
+    return launch_lookup_bwd_lk(lk, B, NQ, H, W, levels, radius, gpyr, s);
+}
+
+// T lookups in order into a gradient pyramid that this call OVERWRITES (zero-initialised by the
+// kernel itself); more than kMaxLookups lookups go in chunks (the later chunks accumulate).
+hipError_t launch_lookup_bwd_multi(const float *const *coords, const float *const *grad_out, int T, int B, int NQ,
+                                   int H, int W, int levels, int radius, const LevelPtrs &gpyr, hipStream_t s) {
+    for (int t0 = 0; t0 < T || t0 == 0; t0 += kMaxLookups) {
+        BwdLookups lk{};
+        lk.T = std::min(kMaxLookups, T - t0);
+        lk.zero = t0 == 0;
+        for (int k = 0; k < lk.T; ++k) {
+            lk.coords[k] = coords[t0 + k];
+            lk.grad[k] = grad_out[t0 + k];
+        }
+        hipError_t e = launch_lookup_bwd_lk(lk, B, NQ, H, W, levels, radius, gpyr, s);
+        if (e != hipSuccess) return e;
+        if (T == 0) break;
     }
+    return hipSuccess;
 }
 
 hipError_t launch_pool_bwd(const LevelPtrs &gpyr, long BN, int H, int W, int levels,
@@ -729,4 +1086,81 @@ hipError_t launch_pool_bwd(const LevelPtrs &gpyr, long BN, int H, int W, int lev
     return hipSuccess;
 }
 
+// corr_backward's fused path: the workgroup size BQ (queries) is the first of 4 / 2 / 1 whose LDS
+// image fits 160 KiB (8 only when forced); hipErrorNotSupported when none does (or levels > 4, T > kMaxLookups) —
+// the caller then takes the staged path.
+namespace {
+size_t fused_lds_bytes(int S, int BQ, int H, int W, int levels, FusedOut *o) {
+    const int WIN = S + 2, WSTR = (WIN * WIN) | 1, K = S * S;
+    size_t maps = 0;
+    for (int l = 0; l < kFusedLv; ++l) {
+        const int msz = l < levels ? (H >> l) * (W >> l) : 0;
+        if (o) o->moff[l] = (int)maps, o->msz[l] = msz;
+        maps += (size_t)BQ * msz;
+    }
+    if (o) o->aux = (int)maps;
+    const size_t aux = (size_t)kFusedLv * (6 * S * BQ + K * BQ + BQ * WSTR + 2 * BQ) + BQ + 2;
+    return (maps + aux) * 4;
+}
+
+template <int S, int BQ>
+hipError_t launch_fused_sb(const BwdLookups &lk, FusedOut o, int bytes, hipStream_t s) {
+    static std::atomic<unsigned long long> done{0};
+    hipError_t e = ensure_lds_limit((const void *)lookup_bwd_fold_kernel<S, BQ>, bytes, done);
+    if (e != hipSuccess) return e;
+    const int nqb = (o.NQ + BQ - 1) / BQ;
+    hipLaunchKernelGGL((lookup_bwd_fold_kernel<S, BQ>), dim3((unsigned)(nqb * o.B)), dim3(fused_threads(S, BQ)),
+                       bytes, s, lk, o);
+    return hipGetLastError();
+}
+
+template <int S>
+hipError_t launch_fused_s(const BwdLookups &lk, FusedOut o, hipStream_t s) {
+    static const int force = [] {
+        const char *v = std::getenv("CORR_BWD_FUSED_BQ");  // tuning override: 8, 4, 2 or 1
+        return v ? std::atoi(v) : 0;
+    }();
+    constexpr size_t kLds = 160 * 1024;
+    for (int bq : {4, 2, 1, 8}) {  // 4 measured fastest at train (573 vs 683 us for 8, 586 for 2)
+        if (force && bq != force) continue;
+        const size_t bytes = fused_lds_bytes(S, bq, o.H, o.W, o.L, &o);
+        if (bytes > kLds) continue;
+        switch (bq) {
+            case 8: return launch_fused_sb<S, 8>(lk, o, (int)bytes, s);
+            case 4: return launch_fused_sb<S, 4>(lk, o, (int)bytes, s);
+            case 2: return launch_fused_sb<S, 2>(lk, o, (int)bytes, s);
+            default: return launch_fused_sb<S, 1>(lk, o, (int)bytes, s);
+        }
+    }
+    return hipErrorNotSupported;
+}
+}  // namespace
+
+hipError_t launch_lookup_bwd_fold(const float *const *coords, const float *const *grad_out, int T, int B, int NQ,
+                                  int H, int W, int levels, int radius, float *dc, unsigned *rmax, unsigned *cmax,
+                                  hipStream_t s) {
+    if (T < 1 || T > kMaxLookups || levels < 1 || levels > kFusedLv) return hipErrorNotSupported;
+    BwdLookups lk{};
+    lk.T = T;
+    for (int k = 0; k < T; ++k) {
+        lk.coords[k] = coords[k];
+        lk.grad[k] = grad_out[k];
+    }
+    FusedOut o{};
+    o.dc = dc, o.rmax = rmax, o.cmax = cmax;
+    o.B = B, o.NQ = NQ, o.H = H, o.W = W, o.L = levels;
+    switch (radius) {
+        case 0: return launch_fused_s<1>(lk, o, s);
+        case 1: return launch_fused_s<3>(lk, o, s);
+        case 2: return launch_fused_s<5>(lk, o, s);
+        case 3: return launch_fused_s<7>(lk, o, s);
+        case 4: return launch_fused_s<9>(lk, o, s);
+        case 5: return launch_fused_s<11>(lk, o, s);
+        case 6: return launch_fused_s<13>(lk, o, s);
+        case 7: return launch_fused_s<15>(lk, o, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 }  // namespace corr
+

@@ -28,7 +28,8 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
            "corr_build_bwd_ex_workspace", "corr_build_bwd_ex", "corr_forward_splat_workspace",
            "corr_forward_splat", "corr_convex_upsample", "corr_voxel_grid_workspace",
            "corr_voxel_grid", "corr_lookup_conv", "corr_voxel_grid_tbilinear_workspace",
-           "corr_voxel_grid_tbilinear")
+           "corr_voxel_grid_tbilinear", "corr_lookup_bwd_multi", "corr_pool_fold", "corr_backward_workspace",
+           "corr_backward")
 
 # Build algorithms (include/corr_mi355x.h).  F16X3 is the default: fp32 features split into
 # f16 hi/lo pairs, three f16 MFMAs per product, fp32 accumulate (~1e-6 of max|C| from the
@@ -100,11 +101,17 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.corr_voxel_grid_tbilinear_workspace.argtypes = [i, i, i, i]
     lib.corr_voxel_grid_tbilinear_workspace.restype = sz
     lib.corr_voxel_grid_tbilinear.argtypes = [vp, i, i, i, i, i, vp, vp, sz, vp]
+    lib.corr_lookup_bwd_multi.argtypes = [vp, vp, i, i, i, i, i, i, i, vp, vp]
+    lib.corr_pool_fold.argtypes = [vp, i, i, i, i, i, vp]
+    lib.corr_backward_workspace.argtypes = [i, i, i, i, i, i]
+    lib.corr_backward_workspace.restype = sz
+    lib.corr_backward.argtypes = [i, vp, vp, i, vp, i, vp, i, i, i, i, i, i, vp, vp, vp, vp, sz, vp]
     for f in ("corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd",
               "corr_build_rows", "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows",
               "corr_build_ex", "corr_build_bwd_ex", "corr_forward_splat",
               "corr_convex_upsample", "corr_voxel_grid", "corr_lookup_conv",
-              "corr_voxel_grid_tbilinear"):
+              "corr_voxel_grid_tbilinear", "corr_lookup_bwd_multi", "corr_pool_fold", "corr_backward_workspace",
+           "corr_backward"):
         getattr(lib, f).restype = i
     if path is None:
         _lib = lib
@@ -225,6 +232,54 @@ def build_bwd(grad_c, fmap1, fmap2, algo=None):
                                      D, H, W, df1.data_ptr(), df2.data_ptr(), ws.data_ptr(),
                                      ws.numel() * 4, _stream(fmap1)))
     return df1, df2
+
+
+def lookup_bwd_multi(coords_list, grad_list, radius, grad_levels, H=None, W=None):
+    """corr_lookup_bwd_multi: the lookups' input-gradients, in order, into grad_levels, which it
+    OVERWRITES (no zeroing needed)."""
+    c0 = coords_list[0]
+    B = c0.shape[0]
+    H = c0.shape[2] if H is None else H
+    W = c0.shape[3] if W is None else W
+    cp, gp = _ptrs(coords_list, "coords"), _ptrs(grad_list, "grad_out")
+    with torch.cuda.device(c0.device):
+        _check(load().corr_lookup_bwd_multi(cp, gp, len(coords_list), B, _nq(c0), H, W, len(grad_levels), radius,
+                                            _ptrs(grad_levels, "grad_pyr"), _stream(c0)))
+
+
+def pool_fold(grad_levels, B, H, W):
+    """corr_pool_fold: the pool-backward chain folded into grad_levels[0] in one pass."""
+    NQ = grad_levels[0].shape[0] // B
+    with torch.cuda.device(grad_levels[0].device):
+        _check(load().corr_pool_fold(_ptrs(grad_levels, "grad_pyr"), B, NQ, H, W, len(grad_levels),
+                                     _stream(grad_levels[0])))
+
+
+def backward(coords_list, grad_list, radius, grad_levels, fmap1, fmap2, algo=None):
+    """corr_backward: (dfmap1, dfmap2) of one build and its lookups (all at once, in order).
+    grad_levels: scratch gradient pyramid (overwritten; level 0 ends as dLoss/dcorr)."""
+    algo = default_algo() if algo is None else algo
+    B, D, H, W = fmap2.shape
+    lib = load()
+    NQ = _nq(fmap1)
+    ws_bytes = lib.corr_backward_workspace(algo, B, D, NQ, H, W)
+    if ws_bytes == ctypes.c_size_t(-1).value:
+        raise CorrError(CORR_EUNSUPPORTED, f"unknown backward algorithm {algo}")
+    df1 = torch.empty_like(fmap1)
+    df2 = torch.empty_like(fmap2)
+    ws = torch.empty(max(1, (ws_bytes + 3) // 4), dtype=torch.float32, device=fmap1.device)
+    cp, gp = _ptrs(coords_list, "coords"), _ptrs(grad_list, "grad_out")
+    with torch.cuda.device(fmap1.device):
+        _check(lib.corr_backward(algo, cp, gp, len(coords_list), _dev(fmap1, "fmap1"), NQ, _dev(fmap2, "fmap2"), B, D,
+                                 H, W, len(grad_levels), radius, _ptrs(grad_levels, "grad_pyr"), df1.data_ptr(),
+                                 df2.data_ptr(), ws.data_ptr(), ws.numel() * 4, _stream(fmap1)))
+    return df1, df2
+
+
+def fused_backward() -> bool:
+    """ERAFT_AMD_FUSED_BWD=0 selects the per-lookup backward (lookup_bwd per call + pool_bwd +
+    build_bwd) instead of corr_backward at the build's backward."""
+    return os.environ.get("ERAFT_AMD_FUSED_BWD", "1") != "0"
 
 
 def forward_splat(flow, out):

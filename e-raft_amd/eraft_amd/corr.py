@@ -14,8 +14,10 @@ CPU or eager fallback — CPU tensors raise.
 Autograd (training, BASELINE config 4): gradients flow to fmap1 / fmap2 only (coords are
 detached by the caller, eraft.py:128, and the reference never needs d/dcoords).  Instead of
 materialising a dense pyramid gradient per lookup as torch autograd does, every lookup's
-backward accumulates into ONE gradient pyramid owned by this block; the build's backward
-then folds it (avg-pool backward) and runs the two MFMA GEMMs once.
+backward only STASHES its (coords, upstream gradient); the build's backward then runs
+corr_backward once: all lookups' input-gradients into one gradient pyramid in one launch, the
+avg-pool backward folded into level 0 in one pass, and the two MFMA GEMMs.
+(ERAFT_AMD_FUSED_BWD=0: the per-lookup path — a kernel per lookup backward, then the fold.)
 """
 from __future__ import annotations
 
@@ -63,12 +65,13 @@ def _validate_fmaps(fmap1, fmap2, num_levels):
 class _State:
     """Per-block state shared by the build and lookup autograd nodes."""
 
-    __slots__ = ("levels", "grad_levels", "H", "W")
+    __slots__ = ("levels", "grad_levels", "H", "W", "radius", "stash")
 
-    def __init__(self, H, W):
+    def __init__(self, H, W, radius):
         self.levels = None
-        self.grad_levels = None
-        self.H, self.W = H, W
+        self.grad_levels = None  # per-lookup path: the accumulated gradient pyramid
+        self.stash = []          # fused path: (coords, grad_out) of every lookup backward
+        self.H, self.W, self.radius = H, W, radius
 
 
 class _BuildFn(torch.autograd.Function):
@@ -88,8 +91,23 @@ class _BuildFn(torch.autograd.Function):
     def backward(ctx, *grads):
         fmap1, fmap2 = ctx.saved_tensors
         st = ctx.state
-        gl = st.grad_levels
         direct = grads[:-1]
+        stash, st.stash = st.stash, []
+        if st.grad_levels is None and not any(g is not None for g in direct):
+            if not stash:
+                return None, None, None, None
+            # fused: every lookup's backward + the fold + the GEMMs in corr_backward
+            B, _, H, W = fmap1.shape
+            gl = _alloc_pyramid(B, H, W, len(direct), fmap1)  # scratch, overwritten
+            df1, df2 = _lib.backward([c for c, _ in stash], [g for _, g in stash], st.radius, gl, fmap1, fmap2)
+            return df1, df2, None, None
+        gl = st.grad_levels
+        if stash:  # direct gradients reached corr_pyramid: run the stashed lookups' backward too
+            if gl is None:
+                B, _, H, W = fmap1.shape
+                gl = _alloc_pyramid(B, H, W, len(direct), fmap1, zero=True)
+            for c, g in stash:
+                _lib.lookup_bwd(c, g, st.radius, gl)
         if any(g is not None for g in direct):
             # gradients that reached corr_pyramid outside the lookups
             if gl is None:
@@ -123,10 +141,13 @@ class _LookupFn(torch.autograd.Function):
     def backward(ctx, grad_out):
         (coords,) = ctx.saved_tensors
         st = ctx.state
-        if st.grad_levels is None:
-            B, _, H, W = coords.shape
-            st.grad_levels = _alloc_pyramid(B, H, W, len(st.levels), coords, zero=True)
-        _lib.lookup_bwd(coords, grad_out.contiguous(), ctx.radius, st.grad_levels)
+        if _lib.fused_backward():
+            st.stash.append((coords, grad_out.contiguous()))  # run by the build's backward
+        else:
+            if st.grad_levels is None:
+                B, _, H, W = coords.shape
+                st.grad_levels = _alloc_pyramid(B, H, W, len(st.levels), coords, zero=True)
+            _lib.lookup_bwd(coords, grad_out.contiguous(), ctx.radius, st.grad_levels)
         return None, torch.zeros((), dtype=torch.float32, device=coords.device), None, None
 
 
@@ -142,7 +163,7 @@ class CorrBlock:
         fmap1 = fmap1.contiguous()
         fmap2 = fmap2.contiguous()
         _, _, H, W = fmap1.shape
-        self._state = _State(H, W)
+        self._state = _State(H, W, radius)
         self._token = None
         if torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad):
             outs = _BuildFn.apply(fmap1, fmap2, num_levels, self._state)

@@ -162,6 +162,30 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
                       float *dfmap2, void *workspace, size_t workspace_bytes, void *stream);
 
 /*
+ * The backward of one build and all its lookups in three launches (autograd of model/corr.py:
+ * 25-27, 45, 58-60 for the whole GRU loop at once; coords carry no gradient, eraft.py:128).
+ * coords_rows / grad_out_rows: HOST arrays of T device pointers, the lookups' coords and upstream
+ * gradients ([B][2][NQ], [B][levels*K][NQ]), accumulated in this order.
+ *   corr_lookup_bwd_multi: the T lookups' input-gradients into grad_pyr, which it OVERWRITES
+ *     (zero-initialised inside the kernel: no memset; each workgroup's RMWs stay L2-resident).
+ *     Per cell G = ((0 + S_0) + S_1) + ... with S_t lookup t's scatter-order sum: bit-identical to
+ *     zeroing grad_pyr and calling corr_lookup_bwd_rows for t = 0..T-1.
+ *   corr_pool_fold: the avg_pool2d backward of every level folded into level 0 in place (one pass;
+ *     bit-identical to corr_pool_bwd): afterwards grad_pyr[0] = dLoss/dcorr.
+ *   corr_backward: both, then the two GEMMs of corr_build_bwd_ex (the fold also produces dC's row
+ *     and column maxima for the F16X3 packs); grad_pyr is scratch (overwritten, left = dC), the
+ *     outputs dfmap1_rows / dfmap2 as corr_build_bwd_ex.  Workspace: corr_backward_workspace.
+ */
+int corr_lookup_bwd_multi(const float *const *coords_rows, const float *const *grad_out_rows, int T, int B,
+                          int NQ, int H, int W, int levels, int radius, float *const *grad_pyr, void *stream);
+int corr_pool_fold(float *const *grad_pyr, int B, int NQ, int H, int W, int levels, void *stream);
+size_t corr_backward_workspace(int algo, int B, int D, int NQ, int H, int W);
+int corr_backward(int algo, const float *const *coords_rows, const float *const *grad_out_rows, int T,
+                  const float *fmap1_rows, int NQ, const float *fmap2, int B, int D, int H, int W, int levels,
+                  int radius, float *const *grad_pyr, float *dfmap1_rows, float *dfmap2, void *workspace,
+                  size_t workspace_bytes, void *stream);
+
+/*
  * Warm-start forward splat.  Replaces forward_interpolate_pytorch (utils/image_utils.py:52-83)
  * with grid_sample_values (:10-50): flow [B][2][H][W] -> out [B][2][H][W], every source pixel
  * splatted to its floor / ceil neighbours with bilinear weights, out = sum(z w) / (sum(w) +

@@ -267,6 +267,99 @@ def test_lookup_bwd_bitexact_vs_oracle(B, D, H, W, L, r, kind):
         assert bit_equal(gl[l].cpu().numpy(), ref[l]), l
 
 
+def _bwd_case(T, B, H, W, L, r, seed):
+    """T lookups' coords (mixed regular / pixel-grid / far taps) and upstream gradients."""
+    K = (2 * r + 1) ** 2
+    cs, gs = [], []
+    for t in range(T):
+        c = prng.lookup_coords(seed + t, B, H, W, 0.7 * t)
+        if t % 3 == 1:  # integer grid: the general range-gather path
+            ys, xs = np.meshgrid(np.arange(H, dtype=np.float32), np.arange(W, dtype=np.float32), indexing="ij")
+            c[:, 0], c[:, 1] = xs, ys
+        if t % 5 == 2:  # far taps: the sequential scatter path
+            c[0, 0, 1, :2] = [1048000.5, -3.25]
+        c[0, :, 0, t % W] = np.float32(np.nan)
+        cs.append(torch.from_numpy(c).to(DEV))
+        gs.append(torch.from_numpy(prng.gauss(seed + 100 + t, (B, L * K, H, W))).to(DEV))
+    return cs, gs
+
+
+@pytest.mark.parametrize("T", [0, 1, 3, 12, 40])
+@pytest.mark.parametrize("B,H,W,L,r", [(2, 18, 24, 4, 4), (1, 17, 23, 3, 3)])
+def test_lookup_bwd_multi_and_fold_bitexact(T, B, H, W, L, r):
+    """corr_lookup_bwd_multi (all lookups in one launch, chunks of 32, overwriting the pyramid)
+    == zero + corr_lookup_bwd per lookup, bit for bit; corr_pool_fold's level 0 == corr_pool_bwd's."""
+    from eraft_amd import _lib
+    from eraft_amd.corr import _alloc_pyramid
+    like = torch.empty(1, device=DEV)
+    cs, gs = _bwd_case(T, B, H, W, L, r, 700)
+    ref = _alloc_pyramid(B, H, W, L, like, zero=True)
+    for c, g in zip(cs, gs):
+        _lib.lookup_bwd(c, g, r, ref)
+    got = _alloc_pyramid(B, H, W, L, like)
+    for p in got:
+        p.fill_(float("nan"))  # the multi-lookup kernel must overwrite every cell
+    if T:
+        _lib.lookup_bwd_multi(cs, gs, r, got)
+    else:
+        _lib.lookup_bwd_multi([torch.zeros(B, 2, H, W, device=DEV)], [torch.zeros(B, L * (2 * r + 1) ** 2, H, W,
+                              device=DEV)], r, got)
+    for l in range(L):
+        assert bit_equal(got[l].cpu().numpy(), ref[l].cpu().numpy()), l
+    _lib.pool_bwd(ref, H, W)
+    _lib.pool_fold(got, B, H, W)
+    assert bit_equal(got[0].cpu().numpy(), ref[0].cpu().numpy())
+
+
+@pytest.mark.parametrize("algo", ["f16x3", "fp32"])
+@pytest.mark.parametrize("B,D,H,W,L,r,T", [(2, 32, 18, 24, 4, 4, 5), (1, 20, 17, 23, 3, 3, 2), (8, 64, 36, 48, 4, 4, 12),
+                                           (1, 16, 12, 16, 4, 4, 33), (1, 16, 60, 80, 4, 4, 3),
+                                           (1, 16, 64, 96, 5, 2, 2), (1, 8, 120, 160, 4, 4, 2)])
+def test_corr_backward_matches_staged_path(algo, B, D, H, W, L, r, T):
+    """corr_backward is bit-identical to the staged path (lookup_bwd per lookup, pool_bwd,
+    build_bwd with its own absmax).  Covers the fused LDS-resident kernel at workgroup sizes
+    8 (18x24, 36x48), 4 (60x80), 1 (120x160) queries, and the multi-lookup + fold fallback
+    (33 lookups > one launch's table; 5 levels)."""
+    from eraft_amd import _lib
+    from eraft_amd.corr import _alloc_pyramid
+    f1 = torch.from_numpy(prng.gauss(61, (B, D, H, W))).to(DEV)
+    f2 = torch.from_numpy(prng.gauss(62, (B, D, H, W))).to(DEV)
+    cs, gs = _bwd_case(T, B, H, W, L, r, 800)
+    ref = _alloc_pyramid(B, H, W, L, f1, zero=True)
+    for c, g in zip(cs, gs):
+        _lib.lookup_bwd(c, g, r, ref)
+    _lib.pool_bwd(ref, H, W)
+    r1, r2 = _lib.build_bwd(ref[0].reshape(B * H * W, H * W), f1, f2, _lib._ALGOS[algo])
+    got = _alloc_pyramid(B, H, W, L, f1)
+    g1, g2 = _lib.backward(cs, gs, r, got, f1, f2, _lib._ALGOS[algo])
+    assert bit_equal(got[0].cpu().numpy(), ref[0].cpu().numpy())
+    assert bit_equal(g1.cpu().numpy(), r1.cpu().numpy())
+    assert bit_equal(g2.cpu().numpy(), r2.cpu().numpy())
+
+
+def test_autograd_fused_backward_equals_per_lookup(monkeypatch):
+    """CorrBlock autograd: the stash + corr_backward path and ERAFT_AMD_FUSED_BWD=0's per-lookup
+    path give bit-identical fmap gradients, also when a direct pyramid gradient is present."""
+    B, D, H, W, L, r = 2, 32, 24, 32, 4, 4
+    f1n, f2n = prng.gauss(71, (B, D, H, W)), prng.gauss(72, (B, D, H, W))
+    cs, gs = _bwd_case(6, B, H, W, L, r, 900)
+    res = {}
+    for mode in ("1", "0"):
+        for direct in (False, True):
+            monkeypatch.setenv("ERAFT_AMD_FUSED_BWD", mode)
+            t1 = torch.from_numpy(f1n).to(DEV).requires_grad_(True)
+            t2 = torch.from_numpy(f2n).to(DEV).requires_grad_(True)
+            cb = _cb()(t1, t2, L, r)
+            loss = sum((cb(c) * g).sum() for c, g in zip(cs, gs))
+            if direct:
+                loss = loss + cb.corr_pyramid[2].square().sum()
+            loss.backward()
+            res[mode, direct] = (t1.grad.cpu().numpy(), t2.grad.cpu().numpy())
+    for direct in (False, True):
+        for a, b in zip(res["1", direct], res["0", direct]):
+            assert bit_equal(a, b), direct
+
+
 @pytest.mark.parametrize("B,D,H,W", [(1, 256, 60, 80), (2, 32, 18, 24), (1, 20, 17, 23), (8, 16, 12, 16)])
 @pytest.mark.parametrize("algo", ["f16x3", "fp32"])
 @pytest.mark.parametrize("spread", [False, True])
