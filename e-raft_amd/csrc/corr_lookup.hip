@@ -45,6 +45,7 @@ namespace corr {
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kQB = 64;  // queries per workgroup (one per lane)
 
@@ -675,35 +676,35 @@ __global__ __launch_bounds__(lookup_bwd_threads(S, BQ)) void lookup_bwd_kernel(B
 // level 0 (pool_fold_max_kernel's per-cell recurrence) and ONLY dC = level 0 is written, with
 // its row maxima (written) and column maxima (atomicMax).  The coarse levels never reach HBM and
 // no cell is read-modify-written in HBM: traffic = the upstream gradients + coords + dC.
-// Thread (q, l, cx) = query, level, neighbourhood column — phase 1 (cx < S: tap cx of both
-// axes + the upstream gradients of x-tap cx -> LDS) and phase 2 (its column's cells, added to
-// the LDS map; each cell of a query's window has one owner thread per lookup, so no atomics).
-// Every (query, level) picks its own form: closed form (regular taps), contiguous hit ranges
-// (irregular), or — when a corner leaves the (S+2)^2 neighbourhood — the sequential scatter,
-// run by the group's cx = 0 thread into a zeroed window scratch (cells outside the window
-// directly into the map), exactly as lookup_bwd_kernel's 2c path.
-constexpr int kFusedLv = 4;  // level slots per workgroup
+// Wave w = level w; lane = (query q, neighbourhood column cx) with SLOTS = pow2 >= S + 2 lanes
+// per query, so BQ = 64 / SLOTS queries (4 at r = 4).  A wave touches only its own level's maps
+// and staging, so the lookup loop has NO workgroup barrier: each wave streams through the T
+// lookups on its own (the next lookup's loads in flight), and the workgroup meets once, before
+// the fold.  Per lookup: lanes cx < S compute tap cx of both axes and stage it with the upstream
+// gradients of x-tap cx (wave-private LDS); then lane cx produces its column's cells — closed
+// form (regular taps), contiguous hit ranges (irregular), or, when a corner leaves the (S+2)^2
+// neighbourhood, lookup_bwd_kernel's sequential scatter into a zeroed window scratch — and adds
+// them to the map (branchless: out-of-map cells go to a per-lane dump slot).
+constexpr int kFusedLv = 4;  // level slots (= waves) per workgroup
 
-constexpr int fused_threads(int S, int BQ) { return (BQ * kFusedLv * (S + 2) + 63) / 64 * 64; }
+constexpr int fused_slots(int S) { return S + 2 <= 4 ? 4 : S + 2 <= 8 ? 8 : S + 2 <= 16 ? 16 : 32; }
 
 struct FusedOut {
     float *dc;              // [B * NQ][H * W]
     unsigned *rmax, *cmax;  // [B][NQ] (written), [B][H * W] (atomicMax; zeroed by the caller); may be null
     int B, NQ, H, W, L;
     int moff[kFusedLv], msz[kFusedLv];  // LDS float offset of level l's maps, cells per map
-    int aux;                            // LDS float offset of the per-lookup staging
+    int aux;                            // LDS float offset of the per-wave staging
 };
 
-__device__ __forceinline__ void pick_lookup(const BwdLookups &lk, int lt, const float *&c, const float *&g) {
-    c = lk.coords[0];
-    g = lk.grad[0];
-#pragma unroll
-    for (int k = 1; k < kMaxLookups; ++k)
-        if (k == lt) {
-            c = lk.coords[k];
-            g = lk.grad[k];
-        }
-}
+// Per-wave staging (floats): taps TX/TY [3][S][BQ], gradients [K][BQ], anchors [2][BQ], dump
+// slots [64].
+template <int S>
+struct FusedStage {
+    static constexpr int SLOTS = fused_slots(S), BQ = 64 / SLOTS, K = S * S, WIN = S + 2;
+    static constexpr int TX = 0, TY = TX + 3 * S * BQ, GG = TY + 3 * S * BQ, AX = GG + K * BQ, AY = AX + BQ,
+                         DUMP = AY + BQ, SIZE = DUMP + 64;
+};
 
 // Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2).  Renumber them so
 // every XCD gets a contiguous range: neighbouring query groups — which share the 128-B lines of
@@ -716,174 +717,190 @@ __device__ __forceinline__ int xcd_contiguous(int bid, int n) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
 
-// LDS-only workgroup barrier: __syncthreads() also waits for every outstanding global load
-// (vmcnt(0)), which would expose the prefetch of the next lookup.
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// Orders this wave's LDS traffic (LDS executes one wave's operations in issue order; the asm
+// also keeps the compiler from moving LDS accesses across it).
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-template <int S, int BQ>
-__global__ __launch_bounds__(fused_threads(S, BQ)) void lookup_bwd_fold_kernel(BwdLookups lk, FusedOut o) {
-    constexpr int R = (S - 1) / 2, K = S * S, C = S + 1, WIN = S + 2, WSTR = (WIN * WIN) | 1;
-    constexpr int NT = fused_threads(S, BQ);
+// The lookup table is the kernel's FIRST argument: read entry t straight from the kernarg
+// segment (one scalar load) — indexing the by-value copy with a runtime t makes the compiler
+// either spill the table to scratch or emit a 32-way branch tree.
+__device__ __forceinline__ void kernarg_lookup(int t, const float *&c, const float *&g) {
+    typedef const BwdLookups __attribute__((address_space(4))) *KPtr;
+    const KPtr kp = (KPtr)__builtin_amdgcn_kernarg_segment_ptr();
+    c = kp->coords[t];
+    g = kp->grad[t];
+}
+
+template <int S>
+__global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLookups lk, FusedOut o) {
+    using ST = FusedStage<S>;
+    constexpr int R = (S - 1) / 2, K = S * S, C = S + 1, WIN = ST::WIN;
+    constexpr int SLOTS = ST::SLOTS, BQ = ST::BQ, NT = 64 * kFusedLv;
     extern __shared__ float fsm[];
-    float *TX = fsm + o.aux;                   // [lv][3][S][BQ]
-    float *TY = TX + kFusedLv * 3 * S * BQ;    // [lv][3][S][BQ]
-    float *GG = TY + kFusedLv * 3 * S * BQ;    // [lv][K][BQ]
-    float *WB = GG + kFusedLv * K * BQ;        // [lv][BQ][WSTR]
-    int *AX = reinterpret_cast<int *>(WB + kFusedLv * BQ * WSTR);  // [lv][BQ]
-    int *AY = AX + kFusedLv * BQ;
-    unsigned *RM = reinterpret_cast<unsigned *>(AY + kFusedLv * BQ);  // [BQ]
-    int *UF = reinterpret_cast<int *>(RM + BQ);                       // [2] "some group uncovered" per lookup parity
 
     const int NQ = o.NQ, H = o.H, W = o.W, L = o.L, N = H * W;
     const int nqb = (NQ + BQ - 1) / BQ;
     const int blk = xcd_contiguous(blockIdx.x, gridDim.x);
     const int b = blk / nqb, n0 = (blk - b * nqb) * BQ;
-    const int tid = threadIdx.x;
-    const int q = tid % BQ, lt = tid / BQ, l = lt / WIN, cx = lt - l * WIN;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int l = tid >> 6;  // wave = level
+    const int q = lane / SLOTS, cx = lane - q * SLOTS;
     const bool act = l < L;
     const int n = n0 + q;
     const bool qok = n < NQ;
     const int lc = act ? l : 0;
     const int Hl = H >> lc, Wl = W >> lc;
     const float inv_scale = 1.0f / (float)(1 << lc);
-    const int msz = o.msz[lc];
-    float *M = fsm + o.moff[lc] + q * msz;  // this thread's (query, level) map
-    auto tx = [&](int c, int t) -> float & { return TX[((lc * 3 + c) * S + t) * BQ + q]; };
-    auto ty = [&](int c, int t) -> float & { return TY[((lc * 3 + c) * S + t) * BQ + q]; };
-    auto gg = [&](int k) -> float & { return GG[(lc * K + k) * BQ + q]; };
+    float *st = fsm + o.aux + lc * ST::SIZE;  // this wave's staging
+    const int mbase = o.moff[lc] + q * o.msz[lc];
+    const int dump = o.aux + lc * ST::SIZE + ST::DUMP + lane;
+    auto tx = [&](int c, int t) -> float & { return st[ST::TX + (c * S + t) * BQ + q]; };
+    auto ty = [&](int c, int t) -> float & { return st[ST::TY + (c * S + t) * BQ + q]; };
+    auto gg = [&](int k) -> float & { return st[ST::GG + k * BQ + q]; };
+    unsigned *RM = reinterpret_cast<unsigned *>(fsm + o.aux + kFusedLv * ST::SIZE);  // [BQ]
 
-    {  // zero every map (all levels, all queries of the workgroup)
-        const int total = o.aux;
-        for (int i = tid; i < total; i += NT) fsm[i] = 0.0f;
-        if (tid < BQ) RM[tid] = 0u;
-        if (tid < 2) UF[tid] = 0;
-    }
+    for (int i = tid; i < o.aux; i += NT) fsm[i] = 0.0f;  // every map of the workgroup
+    if (tid < BQ) RM[tid] = 0u;
     __syncthreads();
 
-    // the next lookup's coords and upstream gradients are loaded one lookup ahead (registers),
-    // so their latency hides behind the current lookup's LDS work.  Every thread loads (clamped,
-    // always-valid addresses) and non-loaders drop the values at use: no branch around the loads,
-    // so no copy at a control-flow join forces the compiler to wait for them.
+    // the next lookup's coords and upstream gradients are loaded one lookup ahead (registers).
+    // Every lane loads (clamped, always-valid addresses) and non-loaders drop the values at use:
+    // no branch around the loads, so no copy at a control-flow join makes the compiler wait.
     const bool loader = act && cx < S && qok;
     const int cxl = min(cx, S - 1), nl = min(n, NQ - 1);
     float pcx, pcy, pv[S];
     auto prefetch = [&](int t) {
         const float *coords, *grad_out;
-        pick_lookup(lk, t, coords, grad_out);
+        kernarg_lookup(t, coords, grad_out);
         pcx = coords[((size_t)b * 2 + 0) * NQ + nl];
         pcy = coords[((size_t)b * 2 + 1) * NQ + nl];
         const float *g = grad_out + (((size_t)b * L + lc) * K + (size_t)cxl * S) * NQ + nl;
 #pragma unroll
         for (int u = 0; u < S; ++u) pv[u] = g[(size_t)u * NQ];
     };
-    prefetch(0);
+    if (act) prefetch(0);
 
-    for (int t = 0; t < lk.T; ++t) {
-        // ---- 1. taps of x/y tap cx and the upstream gradients of x-tap cx ----
+    for (int t = 0; act && t < lk.T; ++t) {  // waves of absent levels (l >= L) only join the fold
+        // ---- 1. tap cx of both axes and the upstream gradients of x-tap cx -> staging ----
         const float cxv = loader ? pcx : 0.0f, cyv = loader ? pcy : 0.0f;
         float v[S];
 #pragma unroll
         for (int u = 0; u < S; ++u) v[u] = loader ? pv[u] : 0.0f;
         prefetch(min(t + 1, lk.T - 1));
-        if (act && cx < S) {
-            const Axis a = tap_axis(cxv, inv_scale, cx, R, Wl);
-            const Axis c = tap_axis(cyv, inv_scale, cx, R, Hl);
+        const Axis a = tap_axis(cxv, inv_scale, cxl, R, Wl);
+        const Axis c = tap_axis(cyv, inv_scale, cxl, R, Hl);
+        if (cx < S) {
             tx(0, cx) = a.f, tx(1, cx) = a.lo, tx(2, cx) = a.hi;
             ty(0, cx) = c.f, ty(1, cx) = c.lo, ty(2, cx) = c.hi;
-            if (cx == 0) {
-                AX[lc * BQ + q] = anchor_of(a.f);
-                AY[lc * BQ + q] = anchor_of(c.f);
-            }
 #pragma unroll
             for (int u = 0; u < S; ++u) gg(cx * S + u) = v[u];
+            if (cx == 0) {
+                reinterpret_cast<int *>(st)[ST::AX + q] = anchor_of(a.f);
+                reinterpret_cast<int *>(st)[ST::AY + q] = anchor_of(c.f);
+            }
         }
-        lds_barrier();
-        // ---- 2. this column's cells of the (query, level) window, added to the LDS map ----
-        bool unc = false;
-        if (act && qok) {
-            const float fx0 = tx(0, 0), fy0 = ty(0, 0);
-            const bool far = anchor_of(fx0) == kFarAnchor || anchor_of(fy0) == kFarAnchor;
-            unc = !window_covers<S>(fx0, tx(0, S - 1), fy0, ty(0, S - 1));
-            bool reg = true;
+        wave_lds_sync();
+        // ---- 2. the (query, level) group's form, decided per group ----
+        const float fx0 = tx(0, 0), fy0 = ty(0, 0);
+        const bool bad = cx < S && !(a.f - fx0 == (float)cx && c.f - fy0 == (float)cx);
+        const unsigned long long gmask = (SLOTS == 64 ? ~0ull : ((1ull << SLOTS) - 1)) << (q * SLOTS);
+        const bool irregular = (__ballot(bad) & gmask) != 0;
+        const bool far = anchor_of(fx0) == kFarAnchor || anchor_of(fy0) == kFarAnchor;
+        const bool unc = qok && !window_covers<S>(fx0, tx(0, S - 1), fy0, ty(0, S - 1));
+        const int ax = reinterpret_cast<int *>(st)[ST::AX + q], ay = reinterpret_cast<int *>(st)[ST::AY + q];
+        const int X = ax + cx;
+        const bool colok = qok && !unc && !far && cx < WIN && X >= 0 && X < Wl;
+        // cell (cx, cy) of the window -> its map address, or the lane's dump slot when the cell
+        // is outside the map / the column is not this lane's to write
+        const int ayv = colok ? ay : -(1 << 30);
+        const int rowbase = mbase + ay * Wl + X;
+        auto cell_at = [&](int cy) { return (unsigned)(ayv + cy) < (unsigned)Hl ? rowbase + cy * Wl : dump; };
+        if (!irregular) {
+            // closed form.  Absent terms (window edges) carry zero weights and gradients: adding
+            // +-0 to a sum that started at +0 leaves it unchanged, so every cell sums its 4 terms
+            // in the reference's order (se, ne, sw, nw) with the same bits.  Arrays are indexed
+            // by y-tap j + 1 with zero sentinels at j = -1 and j = S, and two cells (cy, cy + 1)
+            // go through each packed-fp32 instruction (v_pk_mul_f32 / v_pk_add_f32, IEEE per lane).
+            const float wlo = cx < S ? tx(1, cx) : 0.f;
+            const float whi = cx >= 1 && cx <= S ? tx(2, cx - 1) : 0.f;
+            const bool hp = cx >= 1 && cx <= S, hc = cx < S;  // x-tap cx - 1 / cx exists
+            auto yv = [&](int c, int j) { return j >= 0 && j < S ? ty(c, j) : 0.f; };
+            auto gpv = [&](int j) { return hp && j >= 0 && j < S ? gg((cx - 1) * S + j) : 0.f; };
+            auto gcv = [&](int j) { return hc && j >= 0 && j < S ? gg(cx * S + j) : 0.f; };
+            const f32x2 WH = f32x2{whi, whi}, WL = f32x2{wlo, wlo};
+            float sv[C + 1];
 #pragma unroll
-            for (int i = 0; i < S; ++i) reg = reg && tx(0, i) - fx0 == (float)i && ty(0, i) - fy0 == (float)i;
-            const int X = AX[lc * BQ + q] + cx, Y0 = AY[lc * BQ + q];
-            if (!unc && !far && X >= 0 && X < Wl) {
-                if (reg) {
-                    if (cx < C) {
-                        float wlo = 0.f, whi = 0.f;
-                        if (cx < S) wlo = tx(1, cx);
-                        if (cx >= 1) whi = tx(2, cx - 1);
-                        float ylo[S], yhi[S], gp[S], gc[S];
+            for (int cy = 0; cy < C; cy += 2) {  // cells cy, cy + 1; se / sw use y-tap cy - 1, ne / nw cy
+                const f32x2 yhi = f32x2{yv(2, cy - 1), yv(2, cy)}, ylo = f32x2{yv(1, cy), yv(1, cy + 1)};
+                const f32x2 gpm = f32x2{gpv(cy - 1), gpv(cy)}, gp0 = f32x2{gpv(cy), gpv(cy + 1)};
+                const f32x2 gcm = f32x2{gcv(cy - 1), gcv(cy)}, gc0 = f32x2{gcv(cy), gcv(cy + 1)};
+                f32x2 acc = f32x2{0.f, 0.f} + gpm * (yhi * WH);  // se
+                acc = acc + gp0 * (ylo * WH);                    // ne
+                acc = acc + gcm * (yhi * WL);                    // sw
+                acc = acc + gc0 * (ylo * WL);                    // nw
+                sv[cy] = acc.x;
+                sv[cy + 1] = acc.y;
+            }
+            float old[C];
+            int at[C];
 #pragma unroll
-                        for (int j = 0; j < S; ++j) {
-                            ylo[j] = ty(1, j);
-                            yhi[j] = ty(2, j);
-                            gp[j] = cx >= 1 ? gg((cx - 1) * S + j) : 0.f;
-                            gc[j] = cx < S ? gg(cx * S + j) : 0.f;
-                        }
+            for (int cy = 0; cy < C; ++cy) at[cy] = cx < C ? cell_at(cy) : dump;
 #pragma unroll
-                        for (int cy = 0; cy < C; ++cy) {
-                            float s = 0.0f;
-                            if (cx >= 1 && cy >= 1) s = s + __fmul_rn(gp[cy - 1], __fmul_rn(yhi[cy - 1], whi));  // se
-                            if (cx >= 1 && cy < S) s = s + __fmul_rn(gp[cy], __fmul_rn(ylo[cy], whi));           // ne
-                            if (cx < S && cy >= 1) s = s + __fmul_rn(gc[cy - 1], __fmul_rn(yhi[cy - 1], wlo));   // sw
-                            if (cx < S && cy < S) s = s + __fmul_rn(gc[cy], __fmul_rn(ylo[cy], wlo));            // nw
-                            const int Y = Y0 + cy;
-                            if (Y >= 0 && Y < Hl) M[Y * Wl + X] = M[Y * Wl + X] + s;
-                        }
-                    }
-                } else {
-                    float dy[S];
+            for (int cy = 0; cy < C; ++cy) old[cy] = fsm[at[cy]];  // all reads, then all writes
 #pragma unroll
-                    for (int j = 0; j < S; ++j) dy[j] = ty(0, j) - fy0;
-                    int i0 = 0, i1 = 0;
+            for (int cy = 0; cy < C; ++cy) fsm[at[cy]] = old[cy] + sv[cy];
+        } else {
+            float dy[S];
 #pragma unroll
-                    for (int i = 0; i < S; ++i) {
-                        const float d = tx(0, i) - fx0;
-                        i0 += d < (float)(cx - 1);
-                        i1 += d <= (float)cx;
-                    }
-                    for (int cy = 0; cy < WIN; ++cy) {
-                        int j0 = 0, j1 = 0;
+            for (int j = 0; j < S; ++j) dy[j] = ty(0, j) - fy0;
+            int i0 = 0, i1 = 0;
 #pragma unroll
-                        for (int j = 0; j < S; ++j) {
-                            j0 += dy[j] < (float)(cy - 1);
-                            j1 += dy[j] <= (float)cy;
-                        }
-                        float s = 0.0f;
-                        for (int i = i0; i < i1; ++i) {
-                            const float wx = (tx(0, i) - fx0 == (float)cx) ? tx(1, i) : tx(2, i);
-                            for (int j = j0; j < j1; ++j) {
-                                const float wy = (ty(0, j) - fy0 == (float)cy) ? ty(1, j) : ty(2, j);
-                                s = s + __fmul_rn(gg(i * S + j), __fmul_rn(wy, wx));
-                            }
-                        }
-                        const int Y = Y0 + cy;
-                        if (Y >= 0 && Y < Hl) M[Y * Wl + X] = M[Y * Wl + X] + s;
-                    }
+            for (int i = 0; i < S; ++i) {
+                const float d = tx(0, i) - fx0;
+                i0 += d < (float)(cx - 1);
+                i1 += d <= (float)cx;
+            }
+            for (int cy = 0; cy < WIN; ++cy) {
+                int j0 = 0, j1 = 0;
+#pragma unroll
+                for (int j = 0; j < S; ++j) {
+                    j0 += dy[j] < (float)(cy - 1);
+                    j1 += dy[j] <= (float)cy;
                 }
+                float sv = 0.0f;
+                if (colok)
+                    for (int i = i0; i < i1; ++i) {
+                        const float wx = (tx(0, i) - fx0 == (float)cx) ? tx(1, i) : tx(2, i);
+                        for (int j = j0; j < j1; ++j) {
+                            const float wy = (ty(0, j) - fy0 == (float)cy) ? ty(1, j) : ty(2, j);
+                            sv = sv + __fmul_rn(gg(i * S + j), __fmul_rn(wy, wx));
+                        }
+                    }
+                const int at = cell_at(cy);
+                fsm[at] = fsm[at] + sv;
             }
         }
         // ---- 2c. groups whose corners leave the neighbourhood: sequential scatter ----
-        if (unc) UF[t & 1] = 1;
-        if (tid == 0) UF[(t & 1) ^ 1] = 0;  // last read before the previous lookup's closing barrier
-        lds_barrier();
-        if (UF[t & 1]) {
-            float *wq = WB + (lc * BQ + q) * WSTR;
-            if (unc)
-                for (int e = cx; e < WSTR; e += WIN) wq[e] = 0.0f;
-            lds_barrier();
-            const int ax = AX[lc * BQ + q], ay = AY[lc * BQ + q];
+        // The group's in-map window cells are saved to registers and zeroed, so they serve as the
+        // zeroed window scratch; afterwards cell = saved + scatter sum (lookup_bwd_kernel's order).
+        if (__ballot(unc)) {
+            float *Mq = fsm + mbase;
+            const bool mine = unc && cx < WIN && X >= 0 && X < Wl;
+            float keep[WIN];
+#pragma unroll
+            for (int ry = 0; ry < WIN; ++ry) {
+                const int Y = ay + ry;
+                keep[ry] = 0.f;
+                if (mine && Y >= 0 && Y < Hl) {
+                    keep[ry] = Mq[Y * Wl + X];
+                    Mq[Y * Wl + X] = 0.0f;
+                }
+            }
+            wave_lds_sync();
             if (unc && cx == 0) {
-                auto scatter = [&](float xf, float yf, float v) {
+                auto scatter = [&](float xf, float yf, float val) {
                     if (!in_map(xf, yf, Wl, Hl)) return;
-                    const int xi = (int)xf, yi = (int)yf;
-                    const unsigned ux = (unsigned)(xi - ax), uy = (unsigned)(yi - ay);
-                    if (ux < (unsigned)WIN && uy < (unsigned)WIN)
-                        wq[uy * WIN + ux] += v;
-                    else
-                        M[yi * Wl + xi] += v;  // outside the neighbourhood: disjoint cells
+                    Mq[(int)yf * Wl + (int)xf] += val;  // window cells: the zeroed scratch
                 };
                 for (int ii = 0; ii < S; ++ii) {
                     const float x0 = tx(0, ii), x1 = __fadd_rn(x0, 1.0f);
@@ -899,59 +916,115 @@ __global__ __launch_bounds__(fused_threads(S, BQ)) void lookup_bwd_fold_kernel(B
                     }
                 }
             }
-            lds_barrier();
-            if (unc) {
-                const int X = ax + cx;
-                for (int ry = 0; ry < WIN; ++ry) {
-                    const int Y = ay + ry;
-                    if (X >= 0 && X < Wl && Y >= 0 && Y < Hl) M[Y * Wl + X] = M[Y * Wl + X] + wq[ry * WIN + cx];
-                }
+            wave_lds_sync();
+#pragma unroll
+            for (int ry = 0; ry < WIN; ++ry) {
+                const int Y = ay + ry;
+                if (mine && Y >= 0 && Y < Hl) Mq[Y * Wl + X] = keep[ry] + Mq[Y * Wl + X];
             }
         }
-        lds_barrier();  // the next lookup reuses the staging
+        wave_lds_sync();  // the next lookup rewrites the staging
     }
+    __syncthreads();
 
     // ---- 3. fold into level 0, write dC with its row / column maxima ----
     float rq[BQ];
 #pragma unroll
     for (int k = 0; k < BQ; ++k) rq[k] = 0.f;
-    for (int m = tid; m < N; m += NT) {
-        const int y = m / W, x = m - y * W;
-        float cm = 0.f;
-        int off[kFusedLv];
-        unsigned rc = 0;
+    if (W % 4 == 0 && ((uintptr_t)o.dc & 15) == 0) {
+        // 4 consecutive cells of one row per thread: one 16-B LDS read of level 0, one 8-B read of
+        // level 1 (W/2 even, so its 2 cells are 8-B aligned), one value of each coarser level
+        // (shared by the 4 cells), one 16-B store of dC
+        for (int u = tid; u < N / 4; u += NT) {
+            const int m = 4 * u, y = m / W, x = m - y * W;
+            int off[kFusedLv];
+            unsigned rc = 0;
 #pragma unroll
-        for (int v = 0; v < kFusedLv; ++v) {
-            const int Hv = H >> v, Wv = W >> v, yv = y >> v, xv = x >> v;
-            off[v] = o.moff[v < L ? v : 0] + yv * Wv + xv;
-            if (v + 1 < L && yv < 2 * (Hv >> 1) && xv < 2 * (Wv >> 1)) rc |= 1u << v;
-        }
-#pragma unroll
-        for (int k = 0; k < BQ; ++k) {
-            if (n0 + k >= NQ) break;
-            float up = 0.f;
-            bool have = false;
-#pragma unroll
-            for (int v = kFusedLv - 1; v >= 0; --v) {
-                if (v >= L) continue;
-                float gv = fsm[off[v] + k * o.msz[v]];
-                if (have) gv = gv + up * 0.25f;  // fine += coarse * 0.25 (corr_pool_bwd order)
-                up = gv;
-                have = v > 0 && ((rc >> (v - 1)) & 1u);
+            for (int v = 0; v < kFusedLv; ++v) {
+                const int Hv = H >> v, Wv = W >> v, yv = y >> v, xv = x >> v;
+                off[v] = o.moff[v < L ? v : 0] + yv * Wv + xv;
+                if (v + 1 < L && yv < 2 * (Hv >> 1) && xv < 2 * (Wv >> 1)) rc |= 1u << v;
             }
-            o.dc[((size_t)b * NQ + n0 + k) * N + m] = up;
-            const float av = fabsf(up);
-            cm = fmaxf(cm, av);
-            rq[k] = fmaxf(rq[k], av);
+            float cm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < BQ; ++k) {
+                if (n0 + k >= NQ) continue;
+                float lv[kFusedLv][4];
+                const float4 t0 = *reinterpret_cast<const float4 *>(fsm + off[0] + k * o.msz[0]);
+                lv[0][0] = t0.x, lv[0][1] = t0.y, lv[0][2] = t0.z, lv[0][3] = t0.w;
+                if (L > 1) {
+                    const float2 t1 = *reinterpret_cast<const float2 *>(fsm + off[1] + k * o.msz[1]);
+                    lv[1][0] = lv[1][1] = t1.x;
+                    lv[1][2] = lv[1][3] = t1.y;
+                }
+#pragma unroll
+                for (int v = 2; v < kFusedLv; ++v)
+                    if (v < L) lv[v][0] = lv[v][1] = lv[v][2] = lv[v][3] = fsm[off[v] + k * o.msz[v]];
+                float res[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float up = 0.f;
+                    bool have = false;
+#pragma unroll
+                    for (int v = kFusedLv - 1; v >= 0; --v) {
+                        if (v >= L) continue;
+                        float gv = lv[v][j];
+                        if (have) gv = gv + up * 0.25f;  // fine += coarse * 0.25 (corr_pool_bwd order)
+                        up = gv;
+                        have = v > 0 && ((rc >> (v - 1)) & 1u);
+                    }
+                    res[j] = up;
+                    const float av = fabsf(up);
+                    cm[j] = fmaxf(cm[j], av);
+                    rq[k] = fmaxf(rq[k], av);
+                }
+                *reinterpret_cast<float4 *>(o.dc + ((size_t)b * NQ + n0 + k) * N + m) =
+                    make_float4(res[0], res[1], res[2], res[3]);
+            }
+            if (o.cmax)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (cm[j] > 0.f) atomicMax(&o.cmax[(size_t)b * N + m + j], __float_as_uint(cm[j]));
         }
-        if (o.cmax && cm > 0.f) atomicMax(&o.cmax[(size_t)b * N + m], __float_as_uint(cm));
+    } else {
+        for (int m = tid; m < N; m += NT) {
+            const int y = m / W, x = m - y * W;
+            float cm = 0.f;
+            int off[kFusedLv];
+            unsigned rc = 0;
+#pragma unroll
+            for (int v = 0; v < kFusedLv; ++v) {
+                const int Hv = H >> v, Wv = W >> v, yv = y >> v, xv = x >> v;
+                off[v] = o.moff[v < L ? v : 0] + yv * Wv + xv;
+                if (v + 1 < L && yv < 2 * (Hv >> 1) && xv < 2 * (Wv >> 1)) rc |= 1u << v;
+            }
+#pragma unroll
+            for (int k = 0; k < BQ; ++k) {
+                if (n0 + k >= NQ) continue;
+                float up = 0.f;
+                bool have = false;
+#pragma unroll
+                for (int v = kFusedLv - 1; v >= 0; --v) {
+                    if (v >= L) continue;
+                    float gv = fsm[off[v] + k * o.msz[v]];
+                    if (have) gv = gv + up * 0.25f;
+                    up = gv;
+                    have = v > 0 && ((rc >> (v - 1)) & 1u);
+                }
+                o.dc[((size_t)b * NQ + n0 + k) * N + m] = up;
+                const float av = fabsf(up);
+                cm = fmaxf(cm, av);
+                rq[k] = fmaxf(rq[k], av);
+            }
+            if (o.cmax && cm > 0.f) atomicMax(&o.cmax[(size_t)b * N + m], __float_as_uint(cm));
+        }
     }
 #pragma unroll
     for (int k = 0; k < BQ; ++k) {
         float r = rq[k];
 #pragma unroll
         for (int sh = 32; sh >= 1; sh >>= 1) r = fmaxf(r, __shfl_xor(r, sh));
-        if ((tid & 63) == 0 && r > 0.f) atomicMax(&RM[k], __float_as_uint(r));
+        if (lane == 0 && r > 0.f) atomicMax(&RM[k], __float_as_uint(r));
     }
     __syncthreads();
     if (o.rmax && tid < BQ && n0 + tid < NQ) o.rmax[(size_t)b * NQ + n0 + tid] = RM[tid];
@@ -1086,53 +1159,33 @@ hipError_t launch_pool_bwd(const LevelPtrs &gpyr, long BN, int H, int W, int lev
     return hipSuccess;
 }
 
-// corr_backward's fused path: the workgroup size BQ (queries) is the first of 4 / 2 / 1 whose LDS
-// image fits 160 KiB (8 only when forced); hipErrorNotSupported when none does (or levels > 4, T > kMaxLookups) —
+// corr_backward's fused path: hipErrorNotSupported when the workgroup's LDS image (BQ queries'
+// maps at every level + per-wave staging) exceeds 160 KiB, or levels > 4, or T > kMaxLookups —
 // the caller then takes the staged path.
 namespace {
-size_t fused_lds_bytes(int S, int BQ, int H, int W, int levels, FusedOut *o) {
-    const int WIN = S + 2, WSTR = (WIN * WIN) | 1, K = S * S;
+template <int S>
+size_t fused_lds_bytes(int H, int W, int levels, FusedOut *o) {
+    using ST = FusedStage<S>;
     size_t maps = 0;
     for (int l = 0; l < kFusedLv; ++l) {
         const int msz = l < levels ? (H >> l) * (W >> l) : 0;
         if (o) o->moff[l] = (int)maps, o->msz[l] = msz;
-        maps += (size_t)BQ * msz;
+        maps += (size_t)ST::BQ * msz;
     }
     if (o) o->aux = (int)maps;
-    const size_t aux = (size_t)kFusedLv * (6 * S * BQ + K * BQ + BQ * WSTR + 2 * BQ) + BQ + 2;
-    return (maps + aux) * 4;
-}
-
-template <int S, int BQ>
-hipError_t launch_fused_sb(const BwdLookups &lk, FusedOut o, int bytes, hipStream_t s) {
-    static std::atomic<unsigned long long> done{0};
-    hipError_t e = ensure_lds_limit((const void *)lookup_bwd_fold_kernel<S, BQ>, bytes, done);
-    if (e != hipSuccess) return e;
-    const int nqb = (o.NQ + BQ - 1) / BQ;
-    hipLaunchKernelGGL((lookup_bwd_fold_kernel<S, BQ>), dim3((unsigned)(nqb * o.B)), dim3(fused_threads(S, BQ)),
-                       bytes, s, lk, o);
-    return hipGetLastError();
+    return (maps + (size_t)kFusedLv * ST::SIZE + ST::BQ) * 4;
 }
 
 template <int S>
 hipError_t launch_fused_s(const BwdLookups &lk, FusedOut o, hipStream_t s) {
-    static const int force = [] {
-        const char *v = std::getenv("CORR_BWD_FUSED_BQ");  // tuning override: 8, 4, 2 or 1
-        return v ? std::atoi(v) : 0;
-    }();
-    constexpr size_t kLds = 160 * 1024;
-    for (int bq : {4, 2, 1, 8}) {  // 4 measured fastest at train (573 vs 683 us for 8, 586 for 2)
-        if (force && bq != force) continue;
-        const size_t bytes = fused_lds_bytes(S, bq, o.H, o.W, o.L, &o);
-        if (bytes > kLds) continue;
-        switch (bq) {
-            case 8: return launch_fused_sb<S, 8>(lk, o, (int)bytes, s);
-            case 4: return launch_fused_sb<S, 4>(lk, o, (int)bytes, s);
-            case 2: return launch_fused_sb<S, 2>(lk, o, (int)bytes, s);
-            default: return launch_fused_sb<S, 1>(lk, o, (int)bytes, s);
-        }
-    }
-    return hipErrorNotSupported;
+    const size_t bytes = fused_lds_bytes<S>(o.H, o.W, o.L, &o);
+    if (bytes > 160 * 1024) return hipErrorNotSupported;
+    static std::atomic<unsigned long long> done{0};
+    hipError_t e = ensure_lds_limit((const void *)lookup_bwd_fold_kernel<S>, (int)bytes, done);
+    if (e != hipSuccess) return e;
+    const int nqb = (o.NQ + FusedStage<S>::BQ - 1) / FusedStage<S>::BQ;
+    hipLaunchKernelGGL(lookup_bwd_fold_kernel<S>, dim3((unsigned)(nqb * o.B)), dim3(64 * kFusedLv), bytes, s, lk, o);
+    return hipGetLastError();
 }
 }  // namespace
 
