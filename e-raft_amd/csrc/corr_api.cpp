@@ -266,8 +266,9 @@ int corr_pool_fold(float *const *grad_pyr, int B, int NQ, int H, int W, int leve
     return hip_status(launch_pool_fold(lp, B, NQ, H, W, levels, nullptr, 1, (hipStream_t)stream), fn);
 }
 
-size_t corr_backward_workspace(int algo, int B, int D, int NQ, int H, int W) {
-    return corr_build_bwd_ex_workspace(algo, B, D, NQ, H, W);
+size_t corr_backward_workspace(int algo, int B, int D, int NQ, int H, int W, int radius) {
+    if (B < 1 || D < 1 || NQ < 1 || H < 1 || W < 1 || radius < 0) return 0;
+    return backward_workspace(algo, B, D, NQ, H, W, radius);
 }
 
 int corr_backward(int algo, const float *const *coords_rows, const float *const *grad_out_rows, int T,
@@ -289,7 +290,7 @@ int corr_backward(int algo, const float *const *coords_rows, const float *const 
     if ((rc = check_ptr(fn, fmap1_rows, "fmap1")) || (rc = check_ptr(fn, fmap2, "fmap2")) ||
         (rc = check_ptr(fn, dfmap1_rows, "dfmap1")) || (rc = check_ptr(fn, dfmap2, "dfmap2")))
         return rc;
-    const size_t need = corr_build_bwd_ex_workspace(algo, B, D, NQ, H, W);
+    const size_t need = corr_backward_workspace(algo, B, D, NQ, H, W, radius);
     if (workspace_bytes < need || (need && !workspace))
         return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
     LevelPtrs lp{};

@@ -259,6 +259,38 @@ __global__ __launch_bounds__(256) void pool_fold_max_kernel(FoldArgs a) {
     if (a.rmax && tid < nq) a.rmax[(size_t)b * a.NQ + q0 + tid] = rm[tid];
 }
 
+// Column maxima of dC from the fused backward's per-workgroup partials: cmax[b][m] = max over
+// groups g of part[b][g][m] (float bits; fmaxf drops NaN as absmax_kernel does).  Block: 64
+// columns x 4 slices of the groups (lane = column: coalesced 256-B rows), 8 loads in flight per
+// thread, the slices combined through LDS.
+constexpr int kCmCols = 64, kCmSlices = 4;
+
+__global__ __launch_bounds__(kCmCols *kCmSlices) void colmax_reduce_kernel(const float *__restrict__ part, int G, int N,
+                                                                         unsigned *__restrict__ cmax) {
+    __shared__ float red[kCmSlices][kCmCols];
+    const int b = blockIdx.y, c = threadIdx.x % kCmCols, sl = threadIdx.x / kCmCols;
+    const int m = blockIdx.x * kCmCols + c;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (m < N) {
+        const float *p = part + (size_t)b * G * N + m;
+        int g = sl;
+        for (; g + 7 * kCmSlices < G; g += 8 * kCmSlices)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a[u] = fmaxf(a[u], p[(size_t)(g + u * kCmSlices) * N]);
+        for (; g < G; g += kCmSlices) a[0] = fmaxf(a[0], p[(size_t)g * N]);
+    }
+#pragma unroll
+    for (int u = 1; u < 8; ++u) a[0] = fmaxf(a[0], a[u]);
+    red[sl][c] = a[0];
+    __syncthreads();
+    if (sl == 0 && m < N) {
+        float r = red[0][c];
+#pragma unroll
+        for (int k = 1; k < kCmSlices; ++k) r = fmaxf(r, red[k][c]);
+        cmax[(size_t)b * N + m] = __float_as_uint(r);
+    }
+}
+
 // Exponent of a row from its max (as split_pack_kernel): max * 2^s < 2^15.
 __device__ __forceinline__ int split_shift(float mm) {
     int s = 0;
@@ -691,6 +723,15 @@ hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, 
     return bwd_split_gemms(grad_c, f1, NQ, f2, B, D, H, W, df1, df2, w, s);
 }
 
+// corr_backward's workspace: the backward GEMMs' plus, for F16X3, the fused path's per-workgroup
+// column maxima ([B][groups][H*W] floats, 256-B aligned after the GEMM workspace).
+size_t backward_workspace(int algo, int B, int D, int NQ, int H, int W, int radius) {
+    if (algo == CORR_BUILD_FP32) return build_bwd_workspace(B, D, NQ, H, W);
+    if (algo != CORR_BUILD_F16X3) return (size_t)-1;
+    const size_t base = (build_bwd_split_workspace(B, D, NQ, H, W) + 255) / 256 * 256;
+    return base + (size_t)B * std::max(1, lookup_bwd_fold_groups(NQ, radius)) * H * W * sizeof(float);
+}
+
 // The pool-backward fold of a gradient pyramid into level 0 (in place); with `ws` (an F16X3
 // backward workspace) its row / column maxima land where bwd_split_gemms reads them.
 hipError_t launch_pool_fold(const LevelPtrs &gpyr, int B, int NQ, int H, int W, int levels, void *ws, int D,
@@ -719,17 +760,27 @@ hipError_t launch_backward(int algo, const float *const *coords, const float *co
                            const float *f1, int NQ, const float *f2, int B, int D, int H, int W, int levels, int radius,
                            const LevelPtrs &gpyr, float *df1, float *df2, void *ws, hipStream_t s) {
     hipError_t e;
-    {  // fused: all lookups + the fold in one launch, dC and its maxima straight out of LDS
+    {  // fused: all lookups + the fold in one launch, dC and its row maxima straight out of LDS,
+       // the column maxima as per-workgroup partials reduced by colmax_reduce_kernel
         unsigned *rmax = nullptr, *cmax = nullptr;
+        float *cpart = nullptr;
         BwdWs w{};
+        const int N = H * W, G = lookup_bwd_fold_groups(NQ, radius);
         if (algo == CORR_BUILD_F16X3) {
-            w = carve(ws, B, D, NQ, H * W);
+            w = carve(ws, B, D, NQ, N);
             if ((e = hipMemsetAsync(w.mx0, 0, w.mx_bytes, s)) != hipSuccess) return e;
             rmax = w.mxB, cmax = w.mxC;
+            cpart = reinterpret_cast<float *>(static_cast<char *>(ws) +
+                                              (build_bwd_split_workspace(B, D, NQ, H, W) + 255) / 256 * 256);
         }
-        e = launch_lookup_bwd_fold(coords, grad_out, T, B, NQ, H, W, levels, radius, gpyr.p[0], rmax, cmax, s);
+        e = launch_lookup_bwd_fold(coords, grad_out, T, B, NQ, H, W, levels, radius, gpyr.p[0], rmax, cmax, cpart, s);
         if (e == hipSuccess) {
-            if (algo == CORR_BUILD_F16X3) return bwd_split_gemms(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, w, s);
+            if (algo == CORR_BUILD_F16X3) {
+                hipLaunchKernelGGL(colmax_reduce_kernel, dim3((unsigned)((N + kCmCols - 1) / kCmCols), (unsigned)B),
+                                   dim3(kCmCols * kCmSlices), 0, s, cpart, G, N, cmax);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+                return bwd_split_gemms(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, w, s);
+            }
             return launch_build_bwd(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, (float *)ws, s);
         }
         if (e != hipErrorNotSupported) return e;

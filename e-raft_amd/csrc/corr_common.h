@@ -39,9 +39,11 @@ hipError_t launch_pool_bwd(const LevelPtrs &gpyr, long BN, int H, int W, int lev
                            hipStream_t s);
 hipError_t launch_lookup_bwd_multi(const float *const *coords, const float *const *grad_out, int T, int B, int NQ,
                                    int H, int W, int levels, int radius, const LevelPtrs &gpyr, hipStream_t s);
+int lookup_bwd_fold_groups(int NQ, int radius);
 hipError_t launch_lookup_bwd_fold(const float *const *coords, const float *const *grad_out, int T, int B, int NQ,
                                   int H, int W, int levels, int radius, float *dc, unsigned *rmax, unsigned *cmax,
-                                  hipStream_t s);
+                                  float *cpart, hipStream_t s);
+size_t backward_workspace(int algo, int B, int D, int NQ, int H, int W, int radius);
 hipError_t launch_pool_fold(const LevelPtrs &gpyr, int B, int NQ, int H, int W, int levels, void *ws, int D,
                             hipStream_t s);
 hipError_t launch_backward(int algo, const float *const *coords, const float *const *grad_out, int T,

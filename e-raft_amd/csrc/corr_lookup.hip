@@ -692,8 +692,10 @@ constexpr int fused_slots(int S) { return S + 2 <= 4 ? 4 : S + 2 <= 8 ? 8 : S + 
 struct FusedOut {
     float *dc;              // [B * NQ][H * W]
     unsigned *rmax, *cmax;  // [B][NQ] (written), [B][H * W] (atomicMax; zeroed by the caller); may be null
+    float *cpart;           // [B][groups][H * W]: per-workgroup column maxima instead of cmax atomics
     int B, NQ, H, W, L;
     int moff[kFusedLv], msz[kFusedLv];  // LDS float offset of level l's maps, cells per map
+    int qstr[kFusedLv];                 // LDS floats between two queries' maps (bank-staggered)
     int aux;                            // LDS float offset of the per-wave staging
 };
 
@@ -752,7 +754,7 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     const int Hl = H >> lc, Wl = W >> lc;
     const float inv_scale = 1.0f / (float)(1 << lc);
     float *st = fsm + o.aux + lc * ST::SIZE;  // this wave's staging
-    const int mbase = o.moff[lc] + q * o.msz[lc];
+    const int mbase = o.moff[lc] + q * o.qstr[lc];
     const int dump = o.aux + lc * ST::SIZE + ST::DUMP + lane;
     auto tx = [&](int c, int t) -> float & { return st[ST::TX + (c * S + t) * BQ + q]; };
     auto ty = [&](int c, int t) -> float & { return st[ST::TY + (c * S + t) * BQ + q]; };
@@ -931,7 +933,7 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     float rq[BQ];
 #pragma unroll
     for (int k = 0; k < BQ; ++k) rq[k] = 0.f;
-    if (W % 4 == 0 && ((uintptr_t)o.dc & 15) == 0) {
+    if (W % 4 == 0 && ((uintptr_t)o.dc & 15) == 0 && ((uintptr_t)o.cpart & 15) == 0) {
         // 4 consecutive cells of one row per thread: one 16-B LDS read of level 0, one 8-B read of
         // level 1 (W/2 even, so its 2 cells are 8-B aligned), one value of each coarser level
         // (shared by the 4 cells), one 16-B store of dC
@@ -950,16 +952,16 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
             for (int k = 0; k < BQ; ++k) {
                 if (n0 + k >= NQ) continue;
                 float lv[kFusedLv][4];
-                const float4 t0 = *reinterpret_cast<const float4 *>(fsm + off[0] + k * o.msz[0]);
+                const float4 t0 = *reinterpret_cast<const float4 *>(fsm + off[0] + k * o.qstr[0]);
                 lv[0][0] = t0.x, lv[0][1] = t0.y, lv[0][2] = t0.z, lv[0][3] = t0.w;
                 if (L > 1) {
-                    const float2 t1 = *reinterpret_cast<const float2 *>(fsm + off[1] + k * o.msz[1]);
+                    const float2 t1 = *reinterpret_cast<const float2 *>(fsm + off[1] + k * o.qstr[1]);
                     lv[1][0] = lv[1][1] = t1.x;
                     lv[1][2] = lv[1][3] = t1.y;
                 }
 #pragma unroll
                 for (int v = 2; v < kFusedLv; ++v)
-                    if (v < L) lv[v][0] = lv[v][1] = lv[v][2] = lv[v][3] = fsm[off[v] + k * o.msz[v]];
+                    if (v < L) lv[v][0] = lv[v][1] = lv[v][2] = lv[v][3] = fsm[off[v] + k * o.qstr[v]];
                 float res[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -981,7 +983,10 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
                 *reinterpret_cast<float4 *>(o.dc + ((size_t)b * NQ + n0 + k) * N + m) =
                     make_float4(res[0], res[1], res[2], res[3]);
             }
-            if (o.cmax)
+            if (o.cpart)
+                *reinterpret_cast<float4 *>(o.cpart + ((size_t)b * nqb + (blk - b * nqb)) * N + m) =
+                    make_float4(cm[0], cm[1], cm[2], cm[3]);
+            else if (o.cmax)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     if (cm[j] > 0.f) atomicMax(&o.cmax[(size_t)b * N + m + j], __float_as_uint(cm[j]));
@@ -1006,7 +1011,7 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
 #pragma unroll
                 for (int v = kFusedLv - 1; v >= 0; --v) {
                     if (v >= L) continue;
-                    float gv = fsm[off[v] + k * o.msz[v]];
+                    float gv = fsm[off[v] + k * o.qstr[v]];
                     if (have) gv = gv + up * 0.25f;
                     up = gv;
                     have = v > 0 && ((rc >> (v - 1)) & 1u);
@@ -1016,7 +1021,10 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
                 cm = fmaxf(cm, av);
                 rq[k] = fmaxf(rq[k], av);
             }
-            if (o.cmax && cm > 0.f) atomicMax(&o.cmax[(size_t)b * N + m], __float_as_uint(cm));
+            if (o.cpart)
+                o.cpart[((size_t)b * nqb + (blk - b * nqb)) * N + m] = cm;
+            else if (o.cmax && cm > 0.f)
+                atomicMax(&o.cmax[(size_t)b * N + m], __float_as_uint(cm));
         }
     }
 #pragma unroll
@@ -1166,11 +1174,16 @@ namespace {
 template <int S>
 size_t fused_lds_bytes(int H, int W, int levels, FusedOut *o) {
     using ST = FusedStage<S>;
+    // query stride = map cells rounded up to 64 / BQ (mod 64): the BQ queries' maps start in
+    // different LDS banks, so a wave's read-modify-writes of neighbouring queries' windows (whose
+    // anchors differ by about one pixel) do not collide
     size_t maps = 0;
+    const int stag = 64 / ST::BQ;
     for (int l = 0; l < kFusedLv; ++l) {
         const int msz = l < levels ? (H >> l) * (W >> l) : 0;
-        if (o) o->moff[l] = (int)maps, o->msz[l] = msz;
-        maps += (size_t)ST::BQ * msz;
+        const int qs = msz ? (msz + 63) / 64 * 64 + stag : 0;
+        if (o) o->moff[l] = (int)maps, o->msz[l] = msz, o->qstr[l] = qs;
+        maps += (size_t)ST::BQ * qs;
     }
     if (o) o->aux = (int)maps;
     return (maps + (size_t)kFusedLv * ST::SIZE + ST::BQ) * 4;
@@ -1189,9 +1202,15 @@ hipError_t launch_fused_s(const BwdLookups &lk, FusedOut o, hipStream_t s) {
 }
 }  // namespace
 
+int lookup_bwd_fold_groups(int NQ, int radius) {
+    if (radius < 0 || radius > 7) return 0;
+    const int bq = 64 / fused_slots(2 * radius + 1);
+    return (NQ + bq - 1) / bq;
+}
+
 hipError_t launch_lookup_bwd_fold(const float *const *coords, const float *const *grad_out, int T, int B, int NQ,
                                   int H, int W, int levels, int radius, float *dc, unsigned *rmax, unsigned *cmax,
-                                  hipStream_t s) {
+                                  float *cpart, hipStream_t s) {
     if (T < 1 || T > kMaxLookups || levels < 1 || levels > kFusedLv) return hipErrorNotSupported;
     BwdLookups lk{};
     lk.T = T;
@@ -1200,7 +1219,7 @@ hipError_t launch_lookup_bwd_fold(const float *const *coords, const float *const
         lk.grad[k] = grad_out[k];
     }
     FusedOut o{};
-    o.dc = dc, o.rmax = rmax, o.cmax = cmax;
+    o.dc = dc, o.rmax = rmax, o.cmax = cmax, o.cpart = cpart;
     o.B = B, o.NQ = NQ, o.H = H, o.W = W, o.L = levels;
     switch (radius) {
         case 0: return launch_fused_s<1>(lk, o, s);

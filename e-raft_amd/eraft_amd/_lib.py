@@ -103,7 +103,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.corr_voxel_grid_tbilinear.argtypes = [vp, i, i, i, i, i, vp, vp, sz, vp]
     lib.corr_lookup_bwd_multi.argtypes = [vp, vp, i, i, i, i, i, i, i, vp, vp]
     lib.corr_pool_fold.argtypes = [vp, i, i, i, i, i, vp]
-    lib.corr_backward_workspace.argtypes = [i, i, i, i, i, i]
+    lib.corr_backward_workspace.argtypes = [i, i, i, i, i, i, i]
     lib.corr_backward_workspace.restype = sz
     lib.corr_backward.argtypes = [i, vp, vp, i, vp, i, vp, i, i, i, i, i, i, vp, vp, vp, vp, sz, vp]
     for f in ("corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd",
@@ -262,7 +262,7 @@ def backward(coords_list, grad_list, radius, grad_levels, fmap1, fmap2, algo=Non
     B, D, H, W = fmap2.shape
     lib = load()
     NQ = _nq(fmap1)
-    ws_bytes = lib.corr_backward_workspace(algo, B, D, NQ, H, W)
+    ws_bytes = lib.corr_backward_workspace(algo, B, D, NQ, H, W, radius)
     if ws_bytes == ctypes.c_size_t(-1).value:
         raise CorrError(CORR_EUNSUPPORTED, f"unknown backward algorithm {algo}")
     df1 = torch.empty_like(fmap1)

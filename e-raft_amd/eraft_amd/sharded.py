@@ -10,8 +10,8 @@ is O(N^2) (1920x1280: 5.9 GB per pair), so the build partitions the QUERY pixels
     rows plus the FULL fmap2 -> one RCCL broadcast of fmap2 per frame pair (over xGMI);
   * lookups produce the rank's output rows; an optional all-gather assembles the full
     [B, L*K, H, W] tensor when a replicated consumer needs it;
-  * backward (training): every lookup's backward accumulates into the rank's gradient
-    pyramid slab; the build's backward folds it and runs the two GEMMs on the slab, giving
+  * backward (training): every lookup's backward is stashed and the build's backward runs
+    corr_backward on the slab (all lookups' gradients + the pool fold + the two GEMMs), giving
     the slab's dfmap1 rows and a PARTIAL dfmap2 (the slab's queries only).  Gradient rule:
     when every rank holds the FULL fmap1 (a replicated encoder, the default), both gradients
     are SUM-all-reduced (RCCL, B*D*H*W floats each), so every rank ends with the single-GPU
@@ -77,6 +77,15 @@ class HipRows:
         """-> (dfmap1 of the slab, this slab's partial dfmap2)."""
         return _lib.build_bwd(grad_c, f1_rows, f2)
 
+    @staticmethod
+    def backward(coords_list, grad_list, radius, f1_rows, f2, num_levels):
+        """corr_backward on the slab: every stashed lookup's backward, the pool fold and the GEMMs
+        in one call -> (dfmap1 of the slab, this slab's partial dfmap2)."""
+        B, _, rows, W = f1_rows.shape
+        H = f2.shape[2]
+        gl = _alloc_pyramid_rows(B, rows * W, H, W, num_levels, f2)  # scratch
+        return _lib.backward(coords_list, grad_list, radius, gl, f1_rows, f2)
+
 
 def _alloc_pyramid_rows(B, NQ, H, W, num_levels, like):
     shapes = [(H >> l, W >> l) for l in range(num_levels)]
@@ -90,7 +99,8 @@ def _alloc_pyramid_rows(B, NQ, H, W, num_levels, like):
 
 
 class _ShardState:
-    __slots__ = ("levels", "grad_levels", "B", "NQ", "H", "W", "backend", "group", "h0", "h1", "full1")
+    __slots__ = ("levels", "grad_levels", "B", "NQ", "H", "W", "backend", "group", "h0", "h1", "full1", "stash",
+                 "radius")
 
 
 class _ShardBuildFn(torch.autograd.Function):
@@ -110,9 +120,13 @@ class _ShardBuildFn(torch.autograd.Function):
         f1_rows, f2 = ctx.saved_tensors
         st = ctx.st
         gl, st.grad_levels = st.grad_levels, None
-        if gl is None and st.NQ > 0:  # no lookup reached the loss on this rank
-            gl = st.backend.zero_pyramid(st.B, st.NQ, st.H, st.W, ctx.num_levels, f2)
-        if st.NQ > 0:
+        stash, st.stash = st.stash, []
+        if stash and st.NQ > 0:  # fused: every lookup's backward + fold + GEMMs in corr_backward
+            df1, df2 = st.backend.backward([c for c, _ in stash], [g for _, g in stash], st.radius, f1_rows, f2,
+                                           ctx.num_levels)
+        elif st.NQ > 0:
+            if gl is None:  # no lookup reached the loss on this rank
+                gl = st.backend.zero_pyramid(st.B, st.NQ, st.H, st.W, ctx.num_levels, f2)
             st.backend.pool_bwd(gl, st.H, st.W)
             df1, df2 = st.backend.build_bwd(gl[0], f1_rows, f2)
         else:  # a rank without rows still joins the all-reduces
@@ -139,6 +153,10 @@ class _ShardLookupFn(torch.autograd.Function):
     def backward(ctx, grad_rows):
         (coords_rows,) = ctx.saved_tensors
         st = ctx.st
+        if hasattr(st.backend, "backward") and _lib.fused_backward():
+            st.radius = ctx.radius
+            st.stash.append((coords_rows, grad_rows.contiguous()))  # run by the build's backward
+            return None, torch.zeros((), dtype=torch.float32, device=coords_rows.device), None, None
         if st.grad_levels is None:
             st.grad_levels = st.backend.zero_pyramid(st.B, st.NQ, st.H, st.W, len(st.levels), coords_rows)
         st.backend.lookup_bwd(coords_rows, grad_rows.contiguous(), ctx.radius, st.grad_levels, st.H, st.W)
@@ -179,6 +197,7 @@ class RowShardedCorrBlock:
             st = _ShardState()
             st.B, st.NQ, st.H, st.W = B, (self.h1 - self.h0) * W, H, W
             st.backend, st.group, st.grad_levels, st.levels = backend, group, None, None
+            st.stash, st.radius = [], radius
             st.h0, st.h1, st.full1 = self.h0, self.h1, not fmap1_is_slab
             self._st = st
             src1 = fmap1 if st.full1 else f1.contiguous()

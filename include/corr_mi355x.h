@@ -172,14 +172,19 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
  *     zeroing grad_pyr and calling corr_lookup_bwd_rows for t = 0..T-1.
  *   corr_pool_fold: the avg_pool2d backward of every level folded into level 0 in place (one pass;
  *     bit-identical to corr_pool_bwd): afterwards grad_pyr[0] = dLoss/dcorr.
- *   corr_backward: both, then the two GEMMs of corr_build_bwd_ex (the fold also produces dC's row
- *     and column maxima for the F16X3 packs); grad_pyr is scratch (overwritten, left = dC), the
- *     outputs dfmap1_rows / dfmap2 as corr_build_bwd_ex.  Workspace: corr_backward_workspace.
+ *   corr_backward: both, then the two GEMMs of corr_build_bwd_ex; grad_pyr is scratch (left =
+ *     dC in level 0), the outputs dfmap1_rows / dfmap2 as corr_build_bwd_ex.  When the
+ *     workgroup's LDS image fits (levels <= 4, T <= 32, BQ = 64 / pow2ceil(2r+3) queries' maps of
+ *     every level in 160 KiB: e.g. r = 4 up to 60x80 fmaps), the lookups and the fold run as ONE
+ *     kernel whose gradient maps live in LDS and which writes only dC (plus dC's row maxima and
+ *     per-workgroup column maxima for the F16X3 packs); otherwise corr_lookup_bwd_multi +
+ *     corr_pool_fold.  Both give the same bits.  Workspace: corr_backward_workspace (radius
+ *     sizes the column-maxima partials).
  */
 int corr_lookup_bwd_multi(const float *const *coords_rows, const float *const *grad_out_rows, int T, int B,
                           int NQ, int H, int W, int levels, int radius, float *const *grad_pyr, void *stream);
 int corr_pool_fold(float *const *grad_pyr, int B, int NQ, int H, int W, int levels, void *stream);
-size_t corr_backward_workspace(int algo, int B, int D, int NQ, int H, int W);
+size_t corr_backward_workspace(int algo, int B, int D, int NQ, int H, int W, int radius);
 int corr_backward(int algo, const float *const *coords_rows, const float *const *grad_out_rows, int T,
                   const float *fmap1_rows, int NQ, const float *fmap2, int B, int D, int H, int W, int levels,
                   int radius, float *const *grad_pyr, float *dfmap1_rows, float *dfmap2, void *workspace,

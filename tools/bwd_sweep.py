@@ -20,12 +20,13 @@ ys, xs = torch.meshgrid(torch.arange(H, device=dev, dtype=torch.float32),
                         torch.arange(W, device=dev, dtype=torch.float32), indexing="ij")
 base = torch.stack([xs, ys])[None].expand(B, 2, H, W)
 kind = sys.argv[1] if len(sys.argv) > 1 else "grid"
+algo = _lib._ALGOS[sys.argv[2]] if len(sys.argv) > 2 else None
 coords = [(base + (0 if kind == "int" else 2.0 * torch.randn(B, 2, H, W, device=dev, generator=g))).contiguous()
           for _ in range(12)]
 gouts = [torch.randn(B, L * K, H, W, device=dev, generator=g) for _ in range(12)]
 gpyr = _alloc_pyramid(B, H, W, L, f1)
 for T in (1, 2, 4, 12):
     for _ in range(5):
-        _lib.backward(coords[:T], gouts[:T], r, gpyr, f1, f2)
+        _lib.backward(coords[:T], gouts[:T], r, gpyr, f1, f2, algo)
     torch.cuda.synchronize()
     print("T", T, "done", flush=True)
