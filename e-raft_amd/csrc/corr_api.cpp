@@ -300,8 +300,21 @@ int corr_backward(int algo, const float *const *coords_rows, const float *const 
                       fn);
 }
 
+size_t corr_lookup_conv_weights_bytes(void) { return lookup_conv_weights_bytes(); }
+
+int corr_lookup_conv_weights(const float *weight, int out_channels, int in_channels, void *packed, void *stream) {
+    static const char *fn = "corr_lookup_conv_weights";
+    g_err[0] = 0;
+    int rc;
+    if ((rc = check_ptr(fn, weight, "weight")) || (rc = check_ptr(fn, packed, "packed"))) return rc;
+    if (out_channels != 256 || in_channels < 1 || in_channels > 4 * 81)
+        return fail(CORR_EUNSUPPORTED, "%s: built for 256 output and <= 324 input channels (got %d, %d)", fn,
+                    out_channels, in_channels);
+    return hip_status(launch_lookup_conv_weights(weight, out_channels, in_channels, packed, (hipStream_t)stream), fn);
+}
+
 int corr_lookup_conv(const float *const *pyr, const float *coords, int B, int H, int W, int levels, int radius,
-                     const float *weight_t, const float *bias, int relu, float *out, void *stream) {
+                     const void *packed_weight, const float *bias, int relu, float *out, void *stream) {
     static const char *fn = "corr_lookup_conv";
     g_err[0] = 0;
     int rc = check_dims(fn, B, H * W, H, W, levels);
@@ -314,10 +327,10 @@ int corr_lookup_conv(const float *const *pyr, const float *coords, int B, int H,
         if ((rc = check_ptr(fn, pyr[l], "pyr[l]"))) return rc;
         lp.p[l] = pyr[l];
     }
-    if ((rc = check_ptr(fn, coords, "coords")) || (rc = check_ptr(fn, weight_t, "weight_t")) ||
+    if ((rc = check_ptr(fn, coords, "coords")) || (rc = check_ptr(fn, packed_weight, "packed_weight")) ||
         (rc = check_ptr(fn, bias, "bias")) || (rc = check_ptr(fn, out, "out")))
         return rc;
-    return hip_status(launch_lookup_conv(lp, coords, B, H * W, H, W, levels, radius, weight_t, bias, relu, out,
+    return hip_status(launch_lookup_conv(lp, coords, B, H * W, H, W, levels, radius, packed_weight, bias, relu, out,
                                          (hipStream_t)stream),
                       fn);
 }

@@ -46,6 +46,8 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kQB = 64;  // queries per workgroup (one per lane)
 
@@ -328,88 +330,170 @@ __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
 }
 
 // Lookup fused with the consumer's 1x1 convolution (BasicMotionEncoder.convc1, update.py:68,75:
-// cor = relu(convc1(corr)), 324 -> 256 channels).  A workgroup owns 16 queries: four groups of
-// 3 waves look them up at the four pyramid levels CONCURRENTLY (lookup_block, bit-identical
-// values) into an LDS tile ct[L*K][16]; then 8 waves multiply it by the transposed weight
-// wt[L*K][O] on the fp32 MFMA (v_mfma_f32_16x16x4_f32: A = weight rows = output channels,
-// B = the tile; exact fp32 products, fp32 accumulate; weight batches loaded one batch ahead)
-// and write relu(acc + bias) as [B][O][NQ].  The 324-channel lookup output never reaches HBM.
-// Wave w < 8 owns output channels [32 w, 32 w + 32), so O = 256; L <= 4 (groups beyond L
-// repeat the last level and discard it, keeping every barrier collective).
-constexpr int kConvQB = 16, kConvGT = 192, kConvGroups = 4, kConvNT = kConvGT * kConvGroups, kConvO = 256;
+// cor = relu(convc1(corr)), L*K = 324 -> 256 channels), on the f16 MFMA pipe with the same
+// fp32-accurate split as the build: x = 2^-s (hi + lo), products lo.hi + hi.lo + hi.hi into an
+// fp32 accumulator.  A workgroup owns 32 queries: two groups of 5 waves look them up, two levels
+// at a time (lookup_block, bit-identical values), into an LDS tile ct[L*K][32]; each query's
+// 324 values get a power-of-two scale from their max and are split into f16 hi/lo rows; 8 waves
+// then multiply by the pre-split weight (corr_lookup_conv_weights: per output channel scale,
+// hi/lo in the 16x16x32 MFMA A-fragment order, streamed from L2) and write
+// relu(2^-(s_o + s_q) acc + bias) as [B][O][NQ].  The 324-channel lookup output never reaches
+// HBM.  r = 4, L <= 4, O = 256.
+constexpr int kLcQB = 32, kLcO = 256, kLcKC = 11, kLcKP = 32 * kLcKC /* 352 >= 4*81 */, kLcXS = kLcKP + 8;
+constexpr int kLcGT = lookup_threads(9, kLcQB), kLcNT = 2 * kLcGT;
 
-template <int S>
-__global__ __launch_bounds__(kConvNT) void lookup_conv_kernel(ConstLevelPtrs pyr, const float *__restrict__ coords,
-                                                              int B, int NQ, int H, int W, int L,
-                                                              const float *__restrict__ wt,
-                                                              const float *__restrict__ bias, int relu,
-                                                              float *__restrict__ out) {
-    constexpr int K = S * S, QB = kConvQB;
-    static_assert(lookup_threads(S, QB) == kConvGT, "one level per 3-wave group");
-    __shared__ LookupSmem<S, QB> sm[kConvGroups];
-    __shared__ float ct[kConvGroups * K][QB];
+__device__ __forceinline__ int lc_shift(float mm) {  // max * 2^s < 2^15 (split_pack's rule)
+    int s = 0;
+    if (mm > 0.f && mm <= 3.402823466e38f) {
+        int E;
+        (void)frexpf(mm, &E);
+        s = 15 - E;
+    }
+    return s;
+}
+
+// weight [O][C] fp32 -> packed fragments [O/16][kLcKC][hi, lo][64 lanes] (half8: row o = 16 ob +
+// (lane & 15), k = 32 kc + 8 (lane >> 4) + j) followed by int shift[O].  One block (64 lanes) per o.
+__global__ __launch_bounds__(64) void lookup_conv_weights_kernel(const float *__restrict__ w, int C,
+                                                                 u32x4 *__restrict__ frag, int *__restrict__ shift) {
+    const int o = blockIdx.x, lane = threadIdx.x;
+    const float *row = w + (size_t)o * C;
+    float m = 0.f;
+    for (int k = lane; k < C; k += 64) m = fmaxf(m, fabsf(row[k]));
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) m = fmaxf(m, __shfl_xor(m, sh));
+    const int s = lc_shift(m);
+    if (lane == 0) shift[o] = s;
+    const int ob = o >> 4, fl0 = o & 15;
+    for (int t = lane; t < kLcKC * 4; t += 64) {  // (kc, k-group) of this row
+        const int kc = t >> 2, kg = t & 3;
+        half8 hi8, lo8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 32 * kc + 8 * kg + j;
+            const float y = k < C ? ldexpf(row[k], s) : 0.f;
+            const _Float16 hi = (_Float16)y;
+            hi8[j] = hi;
+            lo8[j] = __builtin_isinf(y) ? (_Float16)0.f : (_Float16)(y - (float)hi);
+        }
+        const int fl = fl0 + 16 * kg;
+        frag[(((size_t)ob * kLcKC + kc) * 2 + 0) * 64 + fl] = __builtin_bit_cast(u32x4, hi8);
+        frag[(((size_t)ob * kLcKC + kc) * 2 + 1) * 64 + fl] = __builtin_bit_cast(u32x4, lo8);
+    }
+}
+
+struct LcSmem {
+    union {
+        LookupSmem<9, kLcQB> lk[2];                   // lookups
+        struct {
+            _Float16 xh[kLcQB][kLcXS], xl[kLcQB][kLcXS];  // split rows (after the lookups)
+        } x;
+    } u;
+    float ct[4 * 81][kLcQB];
+    unsigned mx[kLcQB];
+};
+
+__global__ __launch_bounds__(kLcNT) void lookup_conv_kernel(ConstLevelPtrs pyr, const float *__restrict__ coords,
+                                                             int B, int NQ, int H, int W, int L,
+                                                             const u32x4 *__restrict__ frag,
+                                                             const int *__restrict__ wshift,
+                                                             const float *__restrict__ bias, int relu,
+                                                             float *__restrict__ out) {
+    constexpr int S = 9, K = S * S, QB = kLcQB;
+    __shared__ LcSmem sm;
     const int N = NQ;
     const int nqb = (N + QB - 1) / QB;
     const int b = blockIdx.x / nqb;
     const int n0 = (blockIdx.x - b * nqb) * QB;
     const int tid = threadIdx.x;
-    const int g = tid / kConvGT, ltid = tid - g * kConvGT;
-    const int l = g < L ? g : L - 1;
-    const int i = ltid / QB, q = ltid % QB;
-    lookup_block<S, QB, kConvGT, 0>(sm[g], pyr.p[l], coords, b, n0, N, H, W, l, ltid, [&](int j, float acc) {
-        if (g < L) ct[g * K + i * S + j][q] = acc;
-    });
-    __syncthreads();  // the GEMM reads every level's tile
+    const int g = tid / kLcGT, ltid = tid - g * kLcGT;
     const int KC = L * K;
+    if (tid < QB) sm.mx[tid] = 0u;
+    // ---- lookups: levels 2p + g of pass p (groups beyond L repeat the last level, discarded) ----
+#pragma unroll 1
+    for (int p = 0; p < 2; ++p) {
+        const int l = 2 * p + g, lc = l < L ? l : L - 1;
+        const int i = ltid / QB, q = ltid % QB;
+        lookup_block<S, QB, kLcGT, 0>(sm.u.lk[g], pyr.p[lc], coords, b, n0, N, H, W, lc, ltid,
+                                      [&](int j, float acc) {
+                                          if (l < L) sm.ct[l * K + i * S + j][q] = acc;
+                                      });
+        __syncthreads();
+    }
+    // ---- per-query scale from the max over its L*K values ----
+    {
+        const int q = tid % QB, part = tid / QB, nparts = kLcNT / QB;
+        float m = 0.f;
+        for (int k = part; k < KC; k += nparts) m = fmaxf(m, fabsf(sm.ct[k][q]));
+        if (m > 0.f) atomicMax(&sm.mx[q], __float_as_uint(m));
+    }
+    __syncthreads();
+    // ---- split rows xh / xl [q][k] (zero beyond L*K) ----
+    for (int idx = tid; idx < QB * kLcKP; idx += kLcNT) {
+        const int k = idx / QB, q = idx - k * QB;
+        const int s = lc_shift(__uint_as_float(sm.mx[q]));
+        const float y = k < KC ? ldexpf(sm.ct[k][q], s) : 0.f;
+        const _Float16 hi = (_Float16)y;
+        sm.u.x.xh[q][k] = hi;
+        sm.u.x.xl[q][k] = __builtin_isinf(y) ? (_Float16)0.f : (_Float16)(y - (float)hi);
+    }
+    __syncthreads();
+    // ---- 256 x 32 x 352 GEMM: wave w < 8 owns output channels [32 w, 32 w + 32) ----
     const int lane = tid & 63, w = tid >> 6;
     if (w >= 8) return;
-    const int col = lane & 15, kr = lane >> 4;
-    const int o0 = w * 32;
-    f32x4 acc[2];
+    const int fr = lane & 15, fk = 8 * (lane >> 4);
+    f32x4 acc[2][2];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // weight rows stream from L2: batches of KB k-steps are loaded one batch ahead
-    constexpr int KB = 8;
-    const int nsteps = (KC + 3) / 4;
-    float wa[2][KB][2], cb[2][KB];
-    auto load = [&](int buf, int s0) {
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int u = 0; u < KB; ++u) {
-            const int k = 4 * (s0 + u) + kr;
-            const bool kok = k < KC;
-            cb[buf][u] = kok && n0 + col < N ? ct[k][col] : 0.0f;
-            const float *wr = wt + (size_t)(kok ? k : 0) * kConvO + o0 + col;
+        for (int c = 0; c < 2; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    u32x4 ah[2][2], al[2][2];  // [buffer][o-tile]
+    auto load_a = [&](int buf, int kc) {
 #pragma unroll
-            for (int t = 0; t < 2; ++t) wa[buf][u][t] = kok ? wr[16 * t] : 0.0f;
+        for (int t = 0; t < 2; ++t) {
+            const size_t base = (((size_t)(2 * w + t) * kLcKC + kc) * 2) * 64 + lane;
+            ah[buf][t] = frag[base];
+            al[buf][t] = frag[base + 64];
         }
     };
-    load(0, 0);
-    for (int s0 = 0; s0 < nsteps; s0 += 2 * KB) {
-        if (s0 + KB < nsteps) load(1, s0 + KB);
+    load_a(0, 0);
 #pragma unroll
-        for (int u = 0; u < KB; ++u)
+    for (int kc = 0; kc < kLcKC; ++kc) {
+        const int cur = kc & 1;
+        if (kc + 1 < kLcKC) load_a(cur ^ 1, kc + 1);
+        half8 bh[2], bl[2];
 #pragma unroll
-            for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[0][u][t], cb[0][u], acc[t], 0, 0, 0);
-        if (s0 + 2 * KB < nsteps) load(0, s0 + 2 * KB);
-        if (s0 + KB < nsteps) {
+        for (int c = 0; c < 2; ++c) {
+            bh[c] = *reinterpret_cast<const half8 *>(&sm.u.x.xh[16 * c + fr][32 * kc + fk]);
+            bl[c] = *reinterpret_cast<const half8 *>(&sm.u.x.xl[16 * c + fr][32 * kc + fk]);
+        }
 #pragma unroll
-            for (int u = 0; u < KB; ++u)
+        for (int t = 0; t < 2; ++t) {
+            const half8 a_h = __builtin_bit_cast(half8, ah[cur][t]), a_l = __builtin_bit_cast(half8, al[cur][t]);
 #pragma unroll
-                for (int t = 0; t < 2; ++t)
-                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[1][u][t], cb[1][u], acc[t], 0, 0, 0);
+            for (int c = 0; c < 2; ++c) {
+                acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_l, bh[c], acc[t][c], 0, 0, 0);
+                acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h, bl[c], acc[t][c], 0, 0, 0);
+                acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h, bh[c], acc[t][c], 0, 0, 0);
+            }
         }
     }
-    const int n = n0 + col;
-    if (n >= N) return;
+    // ---- epilogue: C[row = o][col = q] = acc[4 (lane >> 4) + r][lane & 15] ----
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int c = 0; c < 2; ++c) {
+        const int q = 16 * c + fr, n = n0 + q;
+        if (n >= N) continue;
+        const int sq = lc_shift(__uint_as_float(sm.mx[q]));
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int o = o0 + 16 * t + 4 * kr + r;
-            float v = acc[t][r] + bias[o];
-            if (relu) v = fmaxf(v, 0.0f);
-            out[((size_t)b * kConvO + o) * N + n] = v;
-        }
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int o = 32 * w + 16 * t + 4 * (lane >> 4) + r;
+                float v = ldexpf(acc[t][c][r], -(wshift[o] + sq)) + bias[o];
+                if (relu) v = fmaxf(v, 0.0f);
+                out[((size_t)b * kLcO + o) * N + n] = v;
+            }
+    }
 }
 
 template <int S, int BQ>
@@ -1109,13 +1193,25 @@ hipError_t launch_lookup(const ConstLevelPtrs &pyr, const float *coords, int B, 
     }
 }
 
+size_t lookup_conv_weights_bytes() { return (size_t)(kLcO / 16) * kLcKC * 2 * 64 * sizeof(u32x4) + kLcO * sizeof(int); }
+
+hipError_t launch_lookup_conv_weights(const float *w, int O, int C, void *packed, hipStream_t s) {
+    if (O != kLcO || C < 1 || C > kLcKP) return hipErrorInvalidValue;
+    u32x4 *frag = static_cast<u32x4 *>(packed);
+    int *shift = reinterpret_cast<int *>(frag + (size_t)(kLcO / 16) * kLcKC * 2 * 64);
+    hipLaunchKernelGGL(lookup_conv_weights_kernel, dim3(kLcO), dim3(64), 0, s, w, C, frag, shift);
+    return hipGetLastError();
+}
+
 hipError_t launch_lookup_conv(const ConstLevelPtrs &pyr, const float *coords, int B, int NQ, int H, int W,
-                              int levels, int radius, const float *wt, const float *bias, int relu, float *out,
+                              int levels, int radius, const void *packed, const float *bias, int relu, float *out,
                               hipStream_t s) {
-    if (radius != 4 || levels > kConvGroups) return hipErrorInvalidValue;  // E-RAFT: r = 4, L <= 4
-    const int nqb = (NQ + kConvQB - 1) / kConvQB;
-    hipLaunchKernelGGL(lookup_conv_kernel<9>, dim3(nqb * B), dim3(kConvNT), 0, s, pyr, coords, B, NQ, H, W, levels,
-                       wt, bias, relu, out);
+    if (radius != 4 || levels < 1 || levels > 4) return hipErrorInvalidValue;  // E-RAFT: r = 4, L <= 4
+    const u32x4 *frag = static_cast<const u32x4 *>(packed);
+    const int *shift = reinterpret_cast<const int *>(frag + (size_t)(kLcO / 16) * kLcKC * 2 * 64);
+    const int nqb = (NQ + kLcQB - 1) / kLcQB;
+    hipLaunchKernelGGL(lookup_conv_kernel, dim3(nqb * B), dim3(kLcNT), 0, s, pyr, coords, B, NQ, H, W, levels, frag,
+                       shift, bias, relu, out);
     return hipGetLastError();
 }
 

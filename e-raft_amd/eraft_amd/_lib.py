@@ -27,7 +27,7 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
            "corr_build_bwd_rows", "corr_build_workspace", "corr_build_ex",
            "corr_build_bwd_ex_workspace", "corr_build_bwd_ex", "corr_forward_splat_workspace",
            "corr_forward_splat", "corr_convex_upsample", "corr_voxel_grid_workspace",
-           "corr_voxel_grid", "corr_lookup_conv", "corr_voxel_grid_tbilinear_workspace",
+           "corr_voxel_grid", "corr_lookup_conv", "corr_lookup_conv_weights", "corr_lookup_conv_weights_bytes", "corr_voxel_grid_tbilinear_workspace",
            "corr_voxel_grid_tbilinear", "corr_lookup_bwd_multi", "corr_pool_fold", "corr_backward_workspace",
            "corr_backward")
 
@@ -95,6 +95,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.corr_forward_splat.argtypes = [vp, i, i, i, vp, vp, sz, vp]
     lib.corr_convex_upsample.argtypes = [vp, vp, i, i, i, vp, vp]
     lib.corr_lookup_conv.argtypes = [vp, vp, i, i, i, i, i, vp, vp, i, vp, vp]
+    lib.corr_lookup_conv_weights.argtypes = [vp, i, i, vp, vp]
+    lib.corr_lookup_conv_weights_bytes.argtypes = []
+    lib.corr_lookup_conv_weights_bytes.restype = sz
     lib.corr_voxel_grid_workspace.argtypes = [i, i, i, i]
     lib.corr_voxel_grid_workspace.restype = sz
     lib.corr_voxel_grid.argtypes = [vp, vp, vp, vp, i, i, i, i, i, vp, vp, sz, vp]
@@ -109,7 +112,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     for f in ("corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd",
               "corr_build_rows", "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows",
               "corr_build_ex", "corr_build_bwd_ex", "corr_forward_splat",
-              "corr_convex_upsample", "corr_voxel_grid", "corr_lookup_conv",
+              "corr_convex_upsample", "corr_voxel_grid", "corr_lookup_conv", "corr_lookup_conv_weights",
               "corr_voxel_grid_tbilinear", "corr_lookup_bwd_multi", "corr_pool_fold", "corr_backward_workspace",
            "corr_backward"):
         getattr(lib, f).restype = i
@@ -342,11 +345,22 @@ def voxel_grid_tbilinear(events, out, normalize):
                                              ws.data_ptr(), ws.numel() * 4, _stream(out)))
 
 
-def lookup_conv(levels, coords, radius, weight_t, bias, out, relu=True):
+def lookup_conv_weights(weight):
+    """corr_lookup_conv_weights: convc1.weight [256, C(, 1, 1)] -> the packed split (an opaque buffer)."""
+    w = weight.detach().reshape(weight.shape[0], -1).contiguous().float()
+    lib = load()
+    packed = torch.empty((lib.corr_lookup_conv_weights_bytes() + 3) // 4, dtype=torch.float32, device=w.device)
+    with torch.cuda.device(w.device):
+        _check(lib.corr_lookup_conv_weights(_dev(w, "weight"), w.shape[0], w.shape[1], packed.data_ptr(),
+                                            _stream(w)))
+    return packed
+
+
+def lookup_conv(levels, coords, radius, packed, bias, out, relu=True):
     """corr_lookup_conv: fused lookup + 1x1 conv (+ReLU) -> out [B, 256, H, W]."""
     B, _, H, W = coords.shape
     pp, c = _ptrs(levels, "pyr"), _dev(coords, "coords")
-    wt, bs, o = _dev(weight_t, "weight_t"), _dev(bias, "bias"), _dev(out, "out")
+    pw, bs, o = _dev(packed, "packed_weight"), _dev(bias, "bias"), _dev(out, "out")
     with torch.cuda.device(coords.device):
-        _check(load().corr_lookup_conv(pp, c, B, H, W, len(levels), radius, wt, bs, int(bool(relu)), o,
+        _check(load().corr_lookup_conv(pp, c, B, H, W, len(levels), radius, pw, bs, int(bool(relu)), o,
                                        _stream(coords)))

@@ -62,6 +62,9 @@ def _validate_fmaps(fmap1, fmap2, num_levels):
         raise RuntimeError(f"{H}x{W} feature maps are too small for {num_levels} pyramid levels")
 
 
+_WEIGHT_PACKS = {}  # (data_ptr, _version) of convc1.weight -> its packed split (lookup_conv)
+
+
 class _State:
     """Per-block state shared by the build and lookup autograd nodes."""
 
@@ -206,13 +209,13 @@ class CorrBlock:
             raise ValueError(f"lookup_conv needs weight [256, {C}, 1, 1] and bias [256] "
                              f"(got {tuple(weight.shape)}, {tuple(bias.shape)})")
         key = (weight.data_ptr(), weight._version)
-        cached = getattr(self, "_wt_cache", None)
-        if cached is None or cached[0] != key:  # transposed once per block, not per iteration
-            wt = weight.detach().reshape(weight.shape[0], self.num_levels * K).t().contiguous().float()
-            self._wt_cache = cached = (key, wt)
-        wt = cached[1]
+        cached = _WEIGHT_PACKS.get(key)
+        if cached is None:  # split once per weight version (every GRU iteration reuses it)
+            if len(_WEIGHT_PACKS) > 8:
+                _WEIGHT_PACKS.clear()
+            _WEIGHT_PACKS[key] = cached = _lib.lookup_conv_weights(weight)
         out = torch.empty((B, weight.shape[0], H, W), dtype=torch.float32, device=coords.device)
-        _lib.lookup_conv(self._state.levels, coords.detach().contiguous(), self.radius, wt,
+        _lib.lookup_conv(self._state.levels, coords.detach().contiguous(), self.radius, cached,
                          bias.detach().contiguous().float(), out, relu)
         return out
 

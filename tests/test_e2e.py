@@ -45,7 +45,11 @@ def _epe(a, b):
 
 
 @pytest.mark.gpu
-def test_e2e_flow_matches_reference():
+def test_e2e_flow_matches_reference(monkeypatch):
+    """Cold and warm start with the unfused lookup + MIOpen convc1 (the fused default is the
+    next test)."""
+    from eraft_amd.model import ERAFT
+    monkeypatch.setattr(ERAFT, "fuse_lookup_conv", False)
     g = load("g_e2e_dsec")
     seed, H, W, bins, iters = (int(v) for v in g["meta"])
     dev = "cuda:0"
