@@ -5,18 +5,19 @@
 //   dF1[b][d][n] = sum_m F2[b][d][m] * dC[b][n][m] / sqrt(D)    rows d of F2,  rows n of dC  (k = m)
 //   dF2[b][d][m] = sum_n F1[b][d][n] * dC[b][n][m] / sqrt(D)    rows d of F1,  cols m of dC  (k = n)
 //
-// Both are "C = A * B^T" with A and B read along k.  Every operand row r is packed once as
-// x = 2^e_r (hi + lo) in f16 (e_r puts the row's largest |x| in [2^14, 2^15)), chunk-major
-//   pk[b][kc][r][4 x 16 B]  = hi(k 16kc..+7), lo(same), hi(k 16kc+8..+15), lo(same)
-// and the GEMM accumulates lo_A hi_B + hi_A lo_B + hi_A hi_B on v_mfma_f32_32x32x16_f16 into
-// one fp32 accumulator (each f16 x f16 product exact in fp32).  The epilogue applies
-// 2^(e_A + e_B); K is split over workgroups (partial slabs, summed in split order by
-// splitk_reduce_kernel of corr_bwd.hip, which applies 1/sqrt(D)) — deterministic, no atomics.
+// Both are "C = A * B^T" with A and B read along k.  Every operand row r is split as
+// x = 2^e_r (hi + lo) in f16 (e_r puts the row's largest |x| in [2^14, 2^15)) WHILE the GEMM
+// stages it from the fp32 operand into LDS (split_gemm_f32_kernel: the fragment layout
+//   per row and 16-deep chunk: hi(k 0..7), lo(same), hi(k 8..15), lo(same)),
+// and accumulates lo_A hi_B + hi_A lo_B + hi_A hi_B on v_mfma_f32_32x32x16_f16 into one fp32
+// accumulator (each f16 x f16 product exact in fp32).  The epilogue applies 2^(e_A + e_B); K is
+// split over workgroups (partial slabs, summed in split order by splitk_reduce_kernel of
+// corr_bwd.hip, which applies 1/sqrt(D)) — deterministic, no atomics.
 //
-// Packs: the row maxima of F1, F2 and dC and the column maxima of dC come from one reading
-// pass (absmax_kernel, unsigned atomicMax on the bits of non-negative floats: exact and order
-// free), then split_convert_kernel writes the f16 pairs (lane = 4 * row + unit, so each
-// store instruction writes 16 rows' chunks = 1 KiB contiguous).
+// Row maxima: F1 / F2 from rowmax2_kernel; dC's row and column maxima from the fused backward
+// (corr_lookup.hip) or, for a caller-supplied dC, from absmax_kernel (unsigned atomicMax on the
+// bits of non-negative floats: exact and order free).  Also here: the pool-backward fold with
+// dC's maxima (pool_fold_max_kernel) and the column-maxima reduce of the fused backward.
 #include <algorithm>
 #include <cmath>
 
@@ -302,119 +303,19 @@ __device__ __forceinline__ int split_shift(float mm) {
     return s;
 }
 
-// f16 pairs of operand rows: element (r, k) of batch b at X[b * sb + r * sr + k * sk].
-// Block: 4 waves x 16 rows; lane = 4 * row + unit; grid.x over row blocks, grid.y over
-// chunk groups (each thread walks its chunks), grid.z = batch.
-struct ConvArgs {
-    const float *X;
-    long sb, sr, sk;
-    int rows, K, nkc;
-    const unsigned *mx;  // [B][rows] float bits of the row max
-    u32x4 *pk;           // [B][nkc][rows][4]
-    int *ex;             // [B][rows] = -s
-};
-
-__global__ __launch_bounds__(256) void split_convert_kernel(ConvArgs a) {
-    const int b = blockIdx.z;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int r = blockIdx.x * 64 + w * 16 + (lane >> 2), u = lane & 3;
-    if (r >= a.rows) return;
-    const int s = split_shift(__uint_as_float(a.mx[(size_t)b * a.rows + r]));
-    if (blockIdx.y == 0 && u == 0) a.ex[(size_t)b * a.rows + r] = -s;
-    const float *x = a.X + (size_t)b * a.sb + (size_t)r * a.sr;
-    for (int kc = blockIdx.y; kc < a.nkc; kc += gridDim.y) {
-        const int k0 = kc * kBK + (u >> 1) * 8;
-        float v[8];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) v[t] = (k0 + t < a.K) ? x[(size_t)(k0 + t) * a.sk] : 0.f;
-        half8 o;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float y = ldexpf(v[j], s);
-            const _Float16 hi = (_Float16)y;
-            o[j] = (u & 1) ? (__builtin_isinf(y) ? (_Float16)0.f : (_Float16)(y - (float)hi)) : hi;
-        }
-        a.pk[(((size_t)b * a.nkc + kc) * a.rows + r) * 4 + u] = __builtin_bit_cast(u32x4, o);
-    }
-}
-
-// Row-contiguous operand (sk == 1: F1, F2 rows and dC rows): lane = u + 4 r + 16 c covers
-// 4 rows x 4 chunks per wave — each row's 4 chunks are 256 contiguous bytes read as float4
-// pairs, and each chunk's 4 rows are 256 contiguous bytes of the pack.  Block: 4 waves =
-// 16 rows; grid.y walks chunk quads.
-__global__ __launch_bounds__(256) void split_convert_rows_kernel(ConvArgs a) {
-    const int b = blockIdx.z;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int u = lane & 3, rr = (lane >> 2) & 3, c = lane >> 4;
-    const int r = blockIdx.x * 16 + w * 4 + rr;
-    if (r >= a.rows) return;
-    const int s = split_shift(__uint_as_float(a.mx[(size_t)b * a.rows + r]));
-    if (blockIdx.y == 0 && c == 0 && u == 0) a.ex[(size_t)b * a.rows + r] = -s;
-    const float *x = a.X + (size_t)b * a.sb + (size_t)r * a.sr;
-    const bool vec = (a.K % 8) == 0 && ((a.sr | a.sb) % 4) == 0;
-    for (int kc = blockIdx.y * 4 + c; kc < a.nkc; kc += gridDim.y * 4) {
-        const int k0 = kc * kBK + (u >> 1) * 8;
-        float v[8];
-        if (vec && k0 + 8 <= a.K) {
-            const float4 p0 = *reinterpret_cast<const float4 *>(x + k0);
-            const float4 p1 = *reinterpret_cast<const float4 *>(x + k0 + 4);
-            v[0] = p0.x, v[1] = p0.y, v[2] = p0.z, v[3] = p0.w;
-            v[4] = p1.x, v[5] = p1.y, v[6] = p1.z, v[7] = p1.w;
-        } else {
-#pragma unroll
-            for (int t = 0; t < 8; ++t) v[t] = (k0 + t < a.K) ? x[k0 + t] : 0.f;
-        }
-        half8 o;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float y = ldexpf(v[j], s);
-            const _Float16 hi = (_Float16)y;
-            o[j] = (u & 1) ? (__builtin_isinf(y) ? (_Float16)0.f : (_Float16)(y - (float)hi)) : hi;
-        }
-        a.pk[(((size_t)b * a.nkc + kc) * a.rows + r) * 4 + u] = __builtin_bit_cast(u32x4, o);
-    }
-}
-
-// Column operand (sr == 1: dC^T, rows = dC columns m, k = query n): lane = row, so each of
-// the 16 loads of a chunk is one 256-B coalesced row segment of dC.  The wave's 64 rows x
-// 4 units are staged in LDS and stored as 4 contiguous 1 KiB runs.  Block: 4 waves = 256 rows.
-__global__ __launch_bounds__(256) void split_convert_cols_kernel(ConvArgs a) {
-    __shared__ u32x4 tile[4][64 * 4];
-    const int b = blockIdx.z;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int rw = blockIdx.x * 256 + w * 64;  // the wave's first row
-    const int r = rw + lane;
-    const bool live = r < a.rows;
-    const int s = live ? split_shift(__uint_as_float(a.mx[(size_t)b * a.rows + r])) : 0;
-    if (live && blockIdx.y == 0) a.ex[(size_t)b * a.rows + r] = -s;
-    const float *x = a.X + (size_t)b * a.sb + (live ? r : 0);
-    const int vunits = min(256, 4 * max(0, a.rows - rw));
-    for (int kc = blockIdx.y; kc < a.nkc; kc += gridDim.y) {  // uniform trip count
-        float v[kBK];
-#pragma unroll
-        for (int t = 0; t < kBK; ++t) {
-            const int k = kc * kBK + t;
-            v[t] = (live && k < a.K) ? x[(size_t)k * a.sk] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            half8 o;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float y = ldexpf(v[(u >> 1) * 8 + j], s);
-                const _Float16 hi = (_Float16)y;
-                o[j] = (u & 1) ? (__builtin_isinf(y) ? (_Float16)0.f : (_Float16)(y - (float)hi)) : hi;
-            }
-            tile[w][lane * 4 + u] = __builtin_bit_cast(u32x4, o);
-        }
-        __syncthreads();
-        u32x4 *dst = a.pk + (((size_t)b * a.nkc + kc) * a.rows + rw) * 4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int e = lane + 64 * i;
-            if (e < vunits) dst[e] = tile[w][e];
-        }
-        __syncthreads();
+// Two elements at once on gfx950's packed converts (v_cvt_pk_f16_f32, v_pk_add_f32).  The inf
+// guard of split_pair is needed only in rows whose max is inf (then s = 0): a finite max bounds
+// every |y| below 2^15, and a NaN gives NaN either way — so `guard` is per row.
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split2(float x0, float x1, int s, bool guard, half2v &hi, half2v &lo) {
+    const f32x2v y = f32x2v{ldexpf(x0, s), ldexpf(x1, s)};
+    hi = __builtin_convertvector(y, half2v);
+    const f32x2v back = __builtin_convertvector(hi, f32x2v);
+    lo = __builtin_convertvector(y - back, half2v);
+    if (guard) {
+        if (__builtin_isinf(y.x)) lo.x = (_Float16)0.f;
+        if (__builtin_isinf(y.y)) lo.y = (_Float16)0.f;
     }
 }
 
@@ -428,24 +329,34 @@ constexpr int kTI = 32 * kMI * kWI;   // 128
 constexpr int kTJ = 32 * kNJ * kWJ;   // 256
 constexpr int kRows = kTI + kTJ;      // LDS rows per stage (64 B each)
 constexpr int kNT = 256;
-constexpr int kRPP = kNT / 4;         // rows per staging pass
-constexpr int kLPT = kRows / kRPP;    // 16-B loads per thread per chunk
-constexpr int kLI = kTI / kRPP;       // passes of A rows
-static_assert(kRows % kRPP == 0 && kTI % kRPP == 0, "staging tiles the chunk");
+static_assert(kTI == kNT / 2 && kTJ == kNT, "staging: one A row-octet and two B row-octets per thread");
 
 __device__ __forceinline__ int swz(int j, int u) { return j * 4 + (u ^ ((j >> 2) & 3)); }
 
-struct SGemmParams {
-    const u32x4 *pkA, *pkB;
-    const int *exA, *exB;
-    float *C;             // slab base: C[split][b][i][j] (ldc = NJ)
-    int B, NI, NJ, nkc;   // batch, rows of A, rows of B, K chunks
+// The same GEMM reading the fp32 operands and splitting them while staging (no convert
+// kernels, no packed copies: the fp32 element is as many bytes as its hi / lo pair).  A rows
+// are k-contiguous (F1 / F2 rows); B rows are k-contiguous (dC rows, BCOL = false) or dC
+// COLUMNS (BCOL = true: element (j, k) at B[k * b_sk + j], read as 16-B runs along j and
+// transposed into the fragment layout through 8-B LDS writes).  Row shifts come from the row
+// maxima (float bits) exactly as the converts compute them, so every staged unit — and the
+// result — is bit-identical to the packed path.  Per chunk (16 k) a thread stages A row
+// tid / 2, k-octet tid % 2 (8 values) and 16 B values: BCOL = false rows tid / 2 + 128 u,
+// k-octet tid % 2; BCOL = true the 4 columns 4 (tid % 64) .. + 3 at 4 k (4 (tid / 64) ..).
+struct FGemmParams {
+    const float *A;
+    long a_sb, a_sr;
+    const float *Bm;
+    long b_sb, b_sr, b_sk;
+    const unsigned *mxA, *mxB;
+    float *C;
+    int B, NI, NJ, K, nkc;
     int ti, tj, splits, kc_per;
-    float alpha;          // applied only when direct (one split)
-    int direct;
+    float alpha;
+    int direct, vec;  // vec: 16-B loads legal (strides / bases / K multiples of 4)
 };
 
-__global__ __launch_bounds__(kNT, 2) void split_gemm_kernel(SGemmParams p) {
+template <bool BCOL>
+__global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
     __shared__ __attribute__((aligned(16))) u32x4 lds[2 * kRows * 4];
     __shared__ int lex[kRows];
     int id = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -460,36 +371,131 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_kernel(SGemmParams p) {
 
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
     const int wv = tid >> 6, wi = wv / kWJ, wj = wv % kWJ;
-    const int unit = tid & 3, r0 = tid >> 2;
 
-    const u32x4 *src[kLPT];
-    size_t plane[kLPT];
+    for (int row = tid; row < kRows; row += kNT) {
+        const unsigned m = row < kTI ? p.mxA[(size_t)b * p.NI + min(i0 + row, p.NI - 1)]
+                                     : p.mxB[(size_t)b * p.NJ + min(j0 + row - kTI, p.NJ - 1)];
+        lex[row] = -split_shift(__uint_as_float(m));
+    }
+    __syncthreads();
+
+    // staging tasks
+    const int arow = tid >> 1, aoct = tid & 1;
+    const float *ap = p.A + (size_t)b * p.a_sb + (size_t)min(i0 + arow, p.NI - 1) * p.a_sr + aoct * 8;
+    const int sa = -lex[arow];
+    auto row_inf = [&](const unsigned *mx, int row, int n) {
+        return __uint_as_float(mx[(size_t)b * n + min(row, n - 1)]) > 3.402823466e38f;
+    };
+    const bool ga = row_inf(p.mxA, i0 + arow, p.NI);
+    const float *bp[2];
+    int sb[4];
+    bool gb[4];
+    int brow[2];
+    if (!BCOL) {
 #pragma unroll
-    for (int k = 0; k < kLPT; ++k) {
-        const int row = r0 + kRPP * k;
-        if (k < kLI) {
-            const int i = min(i0 + row, p.NI - 1);  // clamped rows feed discarded outputs
-            src[k] = p.pkA + ((size_t)b * p.nkc * p.NI + i) * 4 + unit;
-            plane[k] = (size_t)p.NI * 4;
-        } else {
-            const int j = min(j0 + row - kTI, p.NJ - 1);
-            src[k] = p.pkB + ((size_t)b * p.nkc * p.NJ + j) * 4 + unit;
-            plane[k] = (size_t)p.NJ * 4;
+        for (int u = 0; u < 2; ++u) {
+            brow[u] = (tid >> 1) + 128 * u;
+            bp[u] = p.Bm + (size_t)b * p.b_sb + (size_t)min(j0 + brow[u], p.NJ - 1) * p.b_sr + aoct * 8;
+            sb[u] = -lex[kTI + brow[u]];
+            gb[u] = row_inf(p.mxB, j0 + brow[u], p.NJ);
+        }
+    } else {
+        const int mq = tid & 63;
+        bp[0] = p.Bm + (size_t)b * p.b_sb + (size_t)(tid >> 6) * 4 * p.b_sk;  // + n * b_sk + j
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            sb[c] = -lex[kTI + 4 * mq + c];
+            gb[c] = row_inf(p.mxB, j0 + 4 * mq + c, p.NJ);
         }
     }
-    for (int row = tid; row < kRows; row += kNT)
-        lex[row] = row < kTI ? p.exA[(size_t)b * p.NI + min(i0 + row, p.NI - 1)]
-                             : p.exB[(size_t)b * p.NJ + min(j0 + row - kTI, p.NJ - 1)];
-
-    u32x4 rg[kLPT];
+    const bool vec = p.vec;
+    float ra[8], rb[16];
     auto load_chunk = [&](int kc) {
+        const int k0 = kc * kBK;
+        const int ka = k0 + aoct * 8;  // this thread's A octet
+        if (vec && ka + 8 <= p.K) {
+            const float4 x0 = *reinterpret_cast<const float4 *>(ap + k0);
+            const float4 x1 = *reinterpret_cast<const float4 *>(ap + k0 + 4);
+            ra[0] = x0.x, ra[1] = x0.y, ra[2] = x0.z, ra[3] = x0.w;
+            ra[4] = x1.x, ra[5] = x1.y, ra[6] = x1.z, ra[7] = x1.w;
+        } else {
 #pragma unroll
-        for (int k = 0; k < kLPT; ++k) rg[k] = src[k][kc * plane[k]];
+            for (int t = 0; t < 8; ++t) ra[t] = ka + t < p.K ? ap[k0 + t] : 0.f;
+        }
+        if (!BCOL) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                if (vec && ka + 8 <= p.K) {
+                    const float4 x0 = *reinterpret_cast<const float4 *>(bp[u] + k0);
+                    const float4 x1 = *reinterpret_cast<const float4 *>(bp[u] + k0 + 4);
+                    rb[8 * u + 0] = x0.x, rb[8 * u + 1] = x0.y, rb[8 * u + 2] = x0.z, rb[8 * u + 3] = x0.w;
+                    rb[8 * u + 4] = x1.x, rb[8 * u + 5] = x1.y, rb[8 * u + 6] = x1.z, rb[8 * u + 7] = x1.w;
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) rb[8 * u + t] = ka + t < p.K ? bp[u][k0 + t] : 0.f;
+                }
+            }
+        } else {
+            const int jc = j0 + 4 * (tid & 63);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {  // k = k0 + 4 (tid / 64) + t
+                const int k = k0 + 4 * (tid >> 6) + t;
+                const float *q = bp[0] + (size_t)(k0 + t) * p.b_sk + jc;
+                if (vec && k < p.K && jc + 4 <= p.NJ) {
+                    const float4 x = *reinterpret_cast<const float4 *>(q);
+                    rb[4 * t + 0] = x.x, rb[4 * t + 1] = x.y, rb[4 * t + 2] = x.z, rb[4 * t + 3] = x.w;
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const int jj = min(jc + c, p.NJ - 1);  // clamped columns feed discarded outputs
+                        rb[4 * t + c] = k < p.K ? bp[0][(size_t)(k0 + t) * p.b_sk + jj] : 0.f;
+                    }
+                }
+            }
+        }
     };
     auto store_chunk = [&](int st) {
         u32x4 *S = lds + (size_t)st * kRows * 4;
+        auto split8 = [&](const float *v, int sh, bool guard, u32x4 &hi, u32x4 &lo) {
+            half2v h[4], l[4];
 #pragma unroll
-        for (int k = 0; k < kLPT; ++k) S[swz(r0 + kRPP * k, unit)] = rg[k];
+            for (int t = 0; t < 4; ++t) split2(v[2 * t], v[2 * t + 1], sh, guard, h[t], l[t]);
+            hi = u32x4{__builtin_bit_cast(unsigned, h[0]), __builtin_bit_cast(unsigned, h[1]),
+                       __builtin_bit_cast(unsigned, h[2]), __builtin_bit_cast(unsigned, h[3])};
+            lo = u32x4{__builtin_bit_cast(unsigned, l[0]), __builtin_bit_cast(unsigned, l[1]),
+                       __builtin_bit_cast(unsigned, l[2]), __builtin_bit_cast(unsigned, l[3])};
+        };
+        {
+            u32x4 hi, lo;
+            split8(ra, sa, ga, hi, lo);
+            S[swz(arow, 2 * aoct)] = hi;
+            S[swz(arow, 2 * aoct + 1)] = lo;
+        }
+        if (!BCOL) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                u32x4 hi, lo;
+                split8(rb + 8 * u, sb[u], gb[u], hi, lo);
+                S[swz(kTI + brow[u], 2 * aoct)] = hi;
+                S[swz(kTI + brow[u], 2 * aoct + 1)] = lo;
+            }
+        } else {
+            // column m = 4 (tid % 64) + c holds k 4 kq .. 4 kq + 3 (kq = tid / 64): half of the
+            // k-octet kq / 2, at byte 8 (kq % 2) of its hi and lo units
+            const int kq = tid >> 6, oct = kq >> 1, half = kq & 1;
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                half2v h0, l0, h1, l1;
+                split2(rb[c], rb[4 + c], sb[c], gb[c], h0, l0);
+                split2(rb[8 + c], rb[12 + c], sb[c], gb[c], h1, l1);
+                const int row = kTI + 4 * (tid & 63) + c;
+                u32x2 *H = reinterpret_cast<u32x2 *>(S + swz(row, 2 * oct)) + half;
+                u32x2 *L = reinterpret_cast<u32x2 *>(S + swz(row, 2 * oct + 1)) + half;
+                *H = u32x2{__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1)};
+                *L = u32x2{__builtin_bit_cast(unsigned, l0), __builtin_bit_cast(unsigned, l1)};
+            }
+        }
     };
 
     f32x16 acc[kMI][kNJ];
@@ -537,10 +543,7 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_kernel(SGemmParams p) {
         __syncthreads();
     }
 
-    // epilogue: register g of lane (h, l32) in block (m, n) = C row i0 + wi*64 + 32m +
-    // (g & 3) + 8 (g >> 2) + 4h, column j0 + wj*128 + 32n + l32 (32 consecutive floats per
-    // half-wave store)
-    const size_t slab = (size_t)p.B * p.NI * p.NJ;  // one split's partial sums, [B][NI][NJ]
+    const size_t slab = (size_t)p.B * p.NI * p.NJ;
     float *C = p.C + (p.direct ? 0 : (size_t)split * slab) + (size_t)b * p.NI * p.NJ;
 #pragma unroll
     for (int n = 0; n < kNJ; ++n) {
@@ -571,27 +574,17 @@ int plan_split_k(int NI, int NJ, int nkc, int batch) {
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct BwdWs {
-    u32x4 *pkA, *pkB;
-    int *exA, *exB;
     unsigned *mxA, *mxB, *mxC, *mxA2;  // row max of F2, of dC rows, column max of dC, row max of F1
     unsigned *mx0;                     // start of the four (contiguous, zeroed once per call)
     size_t mx_bytes;
-    float *slab;
+    float *slab;                       // split-K partial sums
 };
 
-// One region per operand pair: A rows (D), B rows (up to max(N, NQ)), K up to max(N, NQ).
+// The maxima (B rows up to max(N, NQ)), then the split-K slabs.
 BwdWs carve(void *ws, int B, int D, int NQ, int N) {
-    const size_t R = std::max(NQ, N), KP = (size_t)(std::max(NQ, N) + kBK - 1) / kBK * kBK;
+    const size_t R = std::max(NQ, N);
     char *w = (char *)ws;
     BwdWs r;
-    r.pkA = (u32x4 *)w;
-    w += al256((size_t)B * KP * D * 4);
-    r.pkB = (u32x4 *)w;
-    w += al256((size_t)B * KP * R * 4);
-    r.exA = (int *)w;
-    w += al256((size_t)B * D * 4);
-    r.exB = (int *)w;
-    w += al256((size_t)B * R * 4);
     r.mx0 = r.mxA = (unsigned *)w;
     w += al256((size_t)B * D * 4);
     r.mxB = (unsigned *)w;
@@ -628,43 +621,31 @@ hipError_t rowmax2(const float *X0, int cols0, unsigned *rmax0, const float *X1,
     return hipGetLastError();
 }
 
-hipError_t convert(const float *X, long sb, long sr, long sk, int B, int rows, int K, const unsigned *mx, u32x4 *pk,
-                   int *ex, hipStream_t s) {
-    ConvArgs a{X, sb, sr, sk, rows, K, (K + kBK - 1) / kBK, mx, pk, ex};
-    if (sk == 1) {
-        const int rb = (rows + 15) / 16, nq = (a.nkc + 3) / 4;
-        const int gy = std::max(1, std::min(nq, 4096 / std::max(1, rb * B)));
-        hipLaunchKernelGGL(split_convert_rows_kernel, dim3(rb, gy, B), dim3(256), 0, s, a);
-    } else if (sr == 1) {
-        const int rb = (rows + 255) / 256;
-        const int gy0 = std::max(1, std::min(a.nkc, 4096 / std::max(1, rb * B)));
-        const int per = (a.nkc + gy0 - 1) / gy0, gy = (a.nkc + per - 1) / per;  // equal chunk counts
-        hipLaunchKernelGGL(split_convert_cols_kernel, dim3(rb, gy, B), dim3(256), 0, s, a);
-    } else {
-        const int rb = (rows + 63) / 64;
-        const int gy = std::max(1, std::min(a.nkc, 2048 / std::max(1, rb * B)));
-        hipLaunchKernelGGL(split_convert_kernel, dim3(rb, gy, B), dim3(256), 0, s, a);
-    }
-    return hipGetLastError();
-}
-
-// C[b] (NI x NJ) = A[b] B[b]^T / sqrt(D) from packed operands; slabs + ordered reduce.
-hipError_t gemm(const BwdWs &w, int B, int NI, int NJ, int K, float sD, float *C, hipStream_t s);
 
 }  // namespace
 
 hipError_t launch_splitk_reduce(const float *ws, float *C, int splits, size_t per, float sD, hipStream_t s);
 
 namespace {
-hipError_t gemm(const BwdWs &w, int B, int NI, int NJ, int K, float sD, float *C, hipStream_t s) {
-    SGemmParams p{};
-    p.pkA = w.pkA;
-    p.pkB = w.pkB;
-    p.exA = w.exA;
-    p.exB = w.exB;
-    p.B = B;
-    p.NI = NI;
-    p.NJ = NJ;
+}  // namespace
+
+size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W) {
+    const int N = H * W;
+    const size_t R = std::max(NQ, N);
+    return 2 * al256((size_t)B * D * 4) + 2 * al256((size_t)B * R * 4) + slab_floats(B, D, NQ, N) * sizeof(float);
+}
+
+// The GEMMs once dC's row maxima (w.mxB) and column maxima (w.mxC) are in the workspace.
+// C[b] (NI x NJ) = A[b] B[b]^T / sqrt(D) straight from the fp32 operands (split while staging).
+template <bool BCOL>
+hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long b_sb, long b_sr, long b_sk,
+                    const unsigned *mxA, const unsigned *mxB, int B, int NI, int NJ, int K, float sD, float *C,
+                    float *slab, hipStream_t s) {
+    FGemmParams p{};
+    p.A = A, p.a_sb = a_sb, p.a_sr = a_sr;
+    p.Bm = Bm, p.b_sb = b_sb, p.b_sr = b_sr, p.b_sk = b_sk;
+    p.mxA = mxA, p.mxB = mxB;
+    p.B = B, p.NI = NI, p.NJ = NJ, p.K = K;
     p.nkc = (K + kBK - 1) / kBK;
     p.ti = (NI + kTI - 1) / kTI;
     p.tj = (NJ + kTJ - 1) / kTJ;
@@ -674,24 +655,17 @@ hipError_t gemm(const BwdWs &w, int B, int NI, int NJ, int K, float sD, float *C
     const bool exact = is_pow2(sD);
     p.alpha = 1.0f / sD;
     p.direct = p.splits == 1 && exact;
-    p.C = p.direct ? C : w.slab;
+    p.C = p.direct ? C : slab;
+    auto al16 = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
+    p.vec = al16(A) && al16(Bm) && a_sb % 4 == 0 && a_sr % 4 == 0 && b_sb % 4 == 0 &&
+            (BCOL ? b_sk % 4 == 0 : b_sr % 4 == 0);
     const long grid = (long)p.ti * p.tj * p.splits * B;
-    hipLaunchKernelGGL(split_gemm_kernel, dim3((unsigned)grid), dim3(kNT), 0, s, p);
+    hipLaunchKernelGGL(split_gemm_f32_kernel<BCOL>, dim3((unsigned)grid), dim3(kNT), 0, s, p);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || p.direct) return e;
-    return launch_splitk_reduce(w.slab, C, p.splits, (size_t)B * NI * NJ, sD, s);
-}
-}  // namespace
-
-size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W) {
-    const int N = H * W;
-    const size_t R = std::max(NQ, N), KP = (size_t)(std::max(NQ, N) + kBK - 1) / kBK * kBK;
-    return al256((size_t)B * KP * D * 4) + al256((size_t)B * KP * R * 4) + al256((size_t)B * D * 4) +
-           al256((size_t)B * R * 4) + 2 * al256((size_t)B * D * 4) + 2 * al256((size_t)B * R * 4) +
-           slab_floats(B, D, NQ, N) * sizeof(float);
+    return launch_splitk_reduce(slab, C, p.splits, (size_t)B * NI * NJ, sD, s);
 }
 
-// The GEMMs once dC's row maxima (w.mxB) and column maxima (w.mxC) are in the workspace.
 hipError_t bwd_split_gemms(const float *grad_c, const float *f1, int NQ, const float *f2, int B, int D, int H, int W,
                            float *df1, float *df2, const BwdWs &w, hipStream_t s) {
     const int N = H * W;
@@ -699,15 +673,12 @@ hipError_t bwd_split_gemms(const float *grad_c, const float *f1, int NQ, const f
     hipError_t e;
 #define CK_(x)                          \
     if ((e = (x)) != hipSuccess) return e;
-    // dF1 = F2 . dC^T : A = F2 rows d (k = m), B = dC rows n (k = m)
     CK_(rowmax2(f2, N, w.mxA, f1, NQ, w.mxA2, B, D, s));
-    CK_(convert(f2, (long)D * N, N, 1, B, D, N, w.mxA, w.pkA, w.exA, s));
-    CK_(convert(grad_c, (long)NQ * N, N, 1, B, NQ, N, w.mxB, w.pkB, w.exB, s));
-    CK_(gemm(w, B, D, NQ, N, sD, df1, s));
+    // dF1 = F2 . dC^T : A = F2 rows d (k = m), B = dC rows n (k = m)
+    CK_(gemm_f32<false>(f2, (long)D * N, N, grad_c, (long)NQ * N, N, 1, w.mxA, w.mxB, B, D, NQ, N, sD, df1, w.slab, s));
     // dF2 = F1 . dC : A = F1 rows d (k = n), B = dC columns m (k = n)
-    CK_(convert(f1, (long)D * NQ, NQ, 1, B, D, NQ, w.mxA2, w.pkA, w.exA, s));
-    CK_(convert(grad_c, (long)NQ * N, 1, N, B, N, NQ, w.mxC, w.pkB, w.exB, s));
-    CK_(gemm(w, B, D, N, NQ, sD, df2, s));
+    CK_(gemm_f32<true>(f1, (long)D * NQ, NQ, grad_c, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, df2, w.slab,
+                       s));
 #undef CK_
     return hipSuccess;
 }
