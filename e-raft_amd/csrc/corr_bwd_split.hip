@@ -262,9 +262,9 @@ __global__ __launch_bounds__(256) void pool_fold_max_kernel(FoldArgs a) {
 
 // Column maxima of dC from the fused backward's per-workgroup partials: cmax[b][m] = max over
 // groups g of part[b][g][m] (float bits; fmaxf drops NaN as absmax_kernel does).  Block: 64
-// columns x 4 slices of the groups (lane = column: coalesced 256-B rows), 8 loads in flight per
+// columns x 16 slices of the groups (lane = column: coalesced 256-B rows), 8 loads in flight per
 // thread, the slices combined through LDS.
-constexpr int kCmCols = 64, kCmSlices = 4;
+constexpr int kCmCols = 64, kCmSlices = 16;
 
 __global__ __launch_bounds__(kCmCols *kCmSlices) void colmax_reduce_kernel(const float *__restrict__ part, int G, int N,
                                                                          unsigned *__restrict__ cmax) {

@@ -337,6 +337,30 @@ def test_corr_backward_matches_staged_path(algo, B, D, H, W, L, r, T):
     assert bit_equal(g2.cpu().numpy(), r2.cpu().numpy())
 
 
+def test_lookup_only_loss_runs_one_backward_call(monkeypatch):
+    """a loss that reaches the pyramid only through lookups makes no zero-filled
+    pyramid gradient (materialize_grads off) and no per-lookup kernel: the build's backward is
+    ONE corr_backward call (and nothing of the staged path)."""
+    from eraft_amd import _lib
+    calls = {"backward": 0, "lookup_bwd": 0, "pool_bwd": 0, "build_bwd": 0}
+    for name in calls:
+        orig = getattr(_lib, name)
+
+        def spy(*a, _o=orig, _n=name, **k):
+            calls[_n] += 1
+            return _o(*a, **k)
+        monkeypatch.setattr(_lib, name, spy)
+    monkeypatch.setenv("ERAFT_AMD_FUSED_BWD", "1")
+    B, D, H, W, L, r = 2, 32, 24, 32, 4, 4
+    t1 = torch.from_numpy(prng.gauss(91, (B, D, H, W))).to(DEV).requires_grad_(True)
+    t2 = torch.from_numpy(prng.gauss(92, (B, D, H, W))).to(DEV).requires_grad_(True)
+    cb = _cb()(t1, t2, L, r)
+    cs, gs = _bwd_case(4, B, H, W, L, r, 950)
+    sum((cb(c) * g).sum() for c, g in zip(cs, gs)).backward()
+    assert calls == {"backward": 1, "lookup_bwd": 0, "pool_bwd": 0, "build_bwd": 0}, calls
+    assert t1.grad is not None and t2.grad is not None
+
+
 def test_autograd_fused_backward_equals_per_lookup(monkeypatch):
     """CorrBlock autograd: the stash + corr_backward path and ERAFT_AMD_FUSED_BWD=0's per-lookup
     path give bit-identical fmap gradients, also when a direct pyramid gradient is present."""
