@@ -3,8 +3,8 @@
 CPU tests run world_size 2 and 3 on the gloo backend with an oracle-backed row backend
 (tests only — the product backend is HipRows): they check the row partition, the fmap2
 broadcast, the all-gather, and that sharded outputs equal the unsharded ones bit for bit.
-The GPU test runs the same partition with the HIP *_rows kernels as G logical shards on one
-device.
+The GPU tests run the same partition with the HIP *_rows kernels as G logical shards on one
+device, and as two real processes sharing the device (gloo carrying the CUDA tensors).
 """
 import os
 import socket
@@ -242,6 +242,79 @@ def test_row_sharded_encoder_param_grads():
     for rank, grads in res:
         for a, b in zip(grads, ref):
             assert np.abs(a - b).max() <= 1e-5 * np.abs(b).max(), rank
+
+
+def _gpu_worker(rank, world, port, shape, q):
+    """HIP row kernels in world processes sharing cuda:0 (gloo carries the CUDA tensors: RCCL
+    refuses two ranks on one device): broadcast of fmap2, slab build + lookups, the gather, and
+    the training backward with both fmap gradients all-reduced."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from eraft_amd.sharded import RowShardedCorrBlock, row_partition
+
+        B, D, H, W, L, r, T = shape
+        dev = "cuda:0"
+        f1 = torch.from_numpy(prng.gauss(1, (B, D, H, W))).to(dev).requires_grad_(True)
+        f2 = (torch.from_numpy(prng.gauss(2, (B, D, H, W))) if rank == 0 else torch.zeros(B, D, H, W)).to(dev)
+        f2.requires_grad_(True)
+        h0, h1 = row_partition(H, world, rank)
+        blk = RowShardedCorrBlock(f1, f2, L, r)
+        K = (2 * r + 1) ** 2
+        loss, outs = 0, []
+        for t in range(T):
+            c = torch.from_numpy(prng.lookup_coords(40 + t, B, H, W, 2.0)).to(dev)
+            g = torch.from_numpy(prng.gauss(50 + t, (B, L * K, H, W))).to(dev)
+            o = blk(c)
+            outs.append(o.detach().cpu().numpy())
+            loss = loss + (o * g[:, :, h0:h1]).sum()
+        full = blk.gather(torch.from_numpy(outs[-1]).to(dev)).cpu().numpy()
+        loss.backward()
+        torch.cuda.synchronize()
+        q.put((rank, h0, h1, outs, full, f1.grad.cpu().numpy(), f2.grad.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_row_sharded_multiprocess_on_gpu():
+    """Two processes on the MI355X through the product backend (HipRows): lookup rows and the
+    gathered output bit-identical to the one-process CorrBlock; training gradients (both
+    all-reduced) within 1e-5 of it."""
+    from eraft_amd import CorrBlock
+    world, shape = 2, (2, 32, 18, 24, 4, 4, 3)
+    B, D, H, W, L, r, T = shape
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(g, world, port, shape, q)) for g in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dev = "cuda:0"
+    K = (2 * r + 1) ** 2
+    t1 = torch.from_numpy(prng.gauss(1, (B, D, H, W))).to(dev).requires_grad_(True)
+    t2 = torch.from_numpy(prng.gauss(2, (B, D, H, W))).to(dev).requires_grad_(True)
+    cb = CorrBlock(t1, t2, L, r)
+    loss, ref = 0, []
+    for t in range(T):
+        c = torch.from_numpy(prng.lookup_coords(40 + t, B, H, W, 2.0)).to(dev)
+        g = torch.from_numpy(prng.gauss(50 + t, (B, L * K, H, W))).to(dev)
+        o = cb(c)
+        ref.append(o.detach().cpu().numpy())
+        loss = loss + (o * g).sum()
+    loss.backward()
+    d1, d2 = t1.grad.cpu().numpy(), t2.grad.cpu().numpy()
+    for rank, h0, h1, outs, full, g1, g2 in res:
+        for o, rf in zip(outs, ref):
+            assert bit_equal(o, rf[:, :, h0:h1]), rank
+        assert bit_equal(full, ref[-1]), rank
+        assert np.abs(g1 - d1).max() <= 1e-5 * np.abs(d1).max(), rank
+        assert np.abs(g2 - d2).max() <= 1e-5 * np.abs(d2).max(), rank
 
 
 def test_row_partition_covers_rows():
