@@ -31,7 +31,7 @@ extern "C" {
 
 #define CORR_OK 0
 #define CORR_EINVAL -1       /* bad sizes / null or misaligned pointers            */
-#define CORR_EUNSUPPORTED -2 /* valid for the reference, not supported here (none yet) */
+#define CORR_EUNSUPPORTED -2 /* valid for the reference, not built here (e.g. lookup_conv r != 4) */
 #define CORR_EHIP -3         /* HIP launch / runtime error                          */
 
 #define CORR_MAX_LEVELS 8

@@ -102,3 +102,32 @@ def test_build_algo_env(monkeypatch):
     monkeypatch.setenv("ERAFT_AMD_BUILD", "bf16")
     with pytest.raises(ValueError):
         _lib.default_algo()
+
+
+def test_backward_workspace_and_validation(lib):
+    """corr_backward: the workspace covers the GEMM slabs plus the per-workgroup column maxima
+    (r = 4: 4 queries per workgroup), and a short workspace or a missing pointer is refused
+    before any HIP call."""
+    B, D, H, W, r = 8, 256, 36, 48, 4
+    N = H * W
+    ws = lib.corr_backward_workspace(1, B, D, N, H, W, r)
+    assert ws >= lib.corr_build_bwd_ex_workspace(1, B, D, N, H, W) + B * (N // 4) * N * 4
+    assert lib.corr_backward_workspace(0, B, D, N, H, W, r) == lib.corr_build_bwd_ex_workspace(0, B, D, N, H, W)
+    assert lib.corr_backward_workspace(1, 0, D, N, H, W, r) == 0
+    ptrs = (ctypes.c_void_p * 1)(16)
+    gp = (ctypes.c_void_p * 4)(16, 16, 16, 16)
+    rc = lib.corr_backward(1, ptrs, ptrs, 1, 16, N, 16, B, D, H, W, 4, r, gp, 16, 16, 16, 4, None)
+    assert rc == -1 and "workspace" in lib.corr_last_error().decode()
+    rc = lib.corr_backward(1, ptrs, ptrs, 1, None, N, 16, B, D, H, W, 4, r, gp, 16, 16, 16, ws, None)
+    assert rc == -1
+
+
+def test_lookup_conv_validation(lib):
+    assert lib.corr_lookup_conv_weights_bytes() >= 256 * 352 * 4
+    rc = lib.corr_lookup_conv_weights(16, 128, 324, 16, None)  # 128 output channels: not convc1
+    assert rc != 0 and "256" in lib.corr_last_error().decode()
+    rc = lib.corr_lookup_conv_weights(None, 256, 324, 16, None)
+    assert rc == -1
+    pyr = (ctypes.c_void_p * 4)(16, 16, 16, 16)
+    rc = lib.corr_lookup_conv(pyr, 16, 1, 60, 80, 4, 3, 16, 16, 1, 16, None)  # radius 3
+    assert rc != 0 and "radius 4" in lib.corr_last_error().decode()
