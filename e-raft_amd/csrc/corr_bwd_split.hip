@@ -336,12 +336,12 @@ __device__ __forceinline__ int swz(int j, int u) { return j * 4 + (u ^ ((j >> 2)
 // The same GEMM reading the fp32 operands and splitting them while staging (no convert
 // kernels, no packed copies: the fp32 element is as many bytes as its hi / lo pair).  A rows
 // are k-contiguous (F1 / F2 rows); B rows are k-contiguous (dC rows, BCOL = false) or dC
-// COLUMNS (BCOL = true: element (j, k) at B[k * b_sk + j], read as 16-B runs along j and
-// transposed into the fragment layout through 8-B LDS writes).  Row shifts come from the row
+// COLUMNS (BCOL = true: element (j, k) at B[k * b_sk + j]; thread = column, so each of its 16
+// loads per chunk is, across the wave, one 256-B run of a dC row).  Row shifts come from the row
 // maxima (float bits) exactly as the converts compute them, so every staged unit — and the
 // result — is bit-identical to the packed path.  Per chunk (16 k) a thread stages A row
 // tid / 2, k-octet tid % 2 (8 values) and 16 B values: BCOL = false rows tid / 2 + 128 u,
-// k-octet tid % 2; BCOL = true the 4 columns 4 (tid % 64) .. + 3 at 4 k (4 (tid / 64) ..).
+// k-octet tid % 2; BCOL = true column tid, all 16 k.
 struct FGemmParams {
     const float *A;
     long a_sb, a_sr;
@@ -400,13 +400,9 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
             gb[u] = row_inf(p.mxB, j0 + brow[u], p.NJ);
         }
     } else {
-        const int mq = tid & 63;
-        bp[0] = p.Bm + (size_t)b * p.b_sb + (size_t)(tid >> 6) * 4 * p.b_sk;  // + n * b_sk + j
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            sb[c] = -lex[kTI + 4 * mq + c];
-            gb[c] = row_inf(p.mxB, j0 + 4 * mq + c, p.NJ);
-        }
+        bp[0] = p.Bm + (size_t)b * p.b_sb;  // + n * b_sk + j
+        sb[0] = -lex[kTI + tid];
+        gb[0] = row_inf(p.mxB, j0 + tid, p.NJ);
     }
     const bool vec = p.vec;
     float ra[8], rb[16];
@@ -436,22 +432,11 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
                 }
             }
         } else {
-            const int jc = j0 + 4 * (tid & 63);
+            // column j0 + tid (lanes = consecutive columns: every load is a 256-B row run)
+            const int jc = min(j0 + tid, p.NJ - 1);  // clamped columns feed discarded outputs
+            const float *q = bp[0] + (size_t)k0 * p.b_sk + jc;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {  // k = k0 + 4 (tid / 64) + t
-                const int k = k0 + 4 * (tid >> 6) + t;
-                const float *q = bp[0] + (size_t)(k0 + t) * p.b_sk + jc;
-                if (vec && k < p.K && jc + 4 <= p.NJ) {
-                    const float4 x = *reinterpret_cast<const float4 *>(q);
-                    rb[4 * t + 0] = x.x, rb[4 * t + 1] = x.y, rb[4 * t + 2] = x.z, rb[4 * t + 3] = x.w;
-                } else {
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        const int jj = min(jc + c, p.NJ - 1);  // clamped columns feed discarded outputs
-                        rb[4 * t + c] = k < p.K ? bp[0][(size_t)(k0 + t) * p.b_sk + jj] : 0.f;
-                    }
-                }
-            }
+            for (int t = 0; t < 16; ++t) rb[t] = k0 + t < p.K ? q[(size_t)t * p.b_sk] : 0.f;
         }
     };
     auto store_chunk = [&](int st) {
@@ -480,20 +465,12 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
                 S[swz(kTI + brow[u], 2 * aoct + 1)] = lo;
             }
         } else {
-            // column m = 4 (tid % 64) + c holds k 4 kq .. 4 kq + 3 (kq = tid / 64): half of the
-            // k-octet kq / 2, at byte 8 (kq % 2) of its hi and lo units
-            const int kq = tid >> 6, oct = kq >> 1, half = kq & 1;
-            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                half2v h0, l0, h1, l1;
-                split2(rb[c], rb[4 + c], sb[c], gb[c], h0, l0);
-                split2(rb[8 + c], rb[12 + c], sb[c], gb[c], h1, l1);
-                const int row = kTI + 4 * (tid & 63) + c;
-                u32x2 *H = reinterpret_cast<u32x2 *>(S + swz(row, 2 * oct)) + half;
-                u32x2 *L = reinterpret_cast<u32x2 *>(S + swz(row, 2 * oct + 1)) + half;
-                *H = u32x2{__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1)};
-                *L = u32x2{__builtin_bit_cast(unsigned, l0), __builtin_bit_cast(unsigned, l1)};
+            for (int o = 0; o < 2; ++o) {  // this column's two k-octets
+                u32x4 hi, lo;
+                split8(rb + 8 * o, sb[0], gb[0], hi, lo);
+                S[swz(kTI + tid, 2 * o)] = hi;
+                S[swz(kTI + tid, 2 * o + 1)] = lo;
             }
         }
     };
