@@ -405,8 +405,10 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
         gb[0] = row_inf(p.mxB, j0 + tid, p.NJ);
     }
     const bool vec = p.vec;
-    float ra[8], rb[16];
-    auto load_chunk = [&](int kc) {
+    // BCOL: two register sets — chunk c is loaded two iterations before its MFMAs (one iteration
+    // before it is staged into LDS), so a load has two MFMA phases to arrive
+    float ra0[8], rb0[16], ra1[8], rb1[16];
+    auto load_chunk = [&](int kc, float (&ra)[8], float (&rb)[16]) {
         const int k0 = kc * kBK;
         const int ka = k0 + aoct * 8;  // this thread's A octet
         if (vec && ka + 8 <= p.K) {
@@ -439,7 +441,7 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
             for (int t = 0; t < 16; ++t) rb[t] = k0 + t < p.K ? q[(size_t)t * p.b_sk] : 0.f;
         }
     };
-    auto store_chunk = [&](int st) {
+    auto store_chunk = [&](int st, const float (&ra)[8], const float (&rb)[16]) {
         u32x4 *S = lds + (size_t)st * kRows * 4;
         auto split8 = [&](const float *v, int sh, bool guard, u32x4 &hi, u32x4 &lo) {
             half2v h[4], l[4];
@@ -484,14 +486,7 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
             for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
 
     const int arow0 = wi * (32 * kMI) + l32, brow0 = kTI + wj * (32 * kNJ) + l32;
-    if (kc0 < kc1) {
-        load_chunk(kc0);
-        store_chunk(0);
-    }
-    __syncthreads();
-    for (int kc = kc0; kc < kc1; ++kc) {
-        const int st = (kc - kc0) & 1;
-        if (kc + 1 < kc1) load_chunk(kc + 1);
+    auto mfma_chunk = [&](int st) {
         const u32x4 *S = lds + (size_t)st * kRows * 4;
         half8 ah[kMI], al[kMI], bh[kNJ], bl[kNJ];
 #pragma unroll
@@ -516,8 +511,40 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
         for (int m = 0; m < kMI; ++m)
 #pragma unroll
             for (int n = 0; n < kNJ; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh[n], acc[m][n], 0, 0, 0);
-        if (kc + 1 < kc1) store_chunk(st ^ 1);
+    };
+    if constexpr (!BCOL) {  // row operands: one set (two would spill at 256 VGPRs)
+        if (kc0 < kc1) {
+            load_chunk(kc0, ra0, rb0);
+            store_chunk(0, ra0, rb0);
+        }
         __syncthreads();
+        for (int kc = kc0; kc < kc1; ++kc) {
+            const int st = (kc - kc0) & 1;
+            if (kc + 1 < kc1) load_chunk(kc + 1, ra0, rb0);
+            mfma_chunk(st);
+            if (kc + 1 < kc1) store_chunk(st ^ 1, ra0, rb0);
+            __syncthreads();
+        }
+    } else {
+    if (kc0 < kc1) {
+        load_chunk(kc0, ra0, rb0);
+        if (kc0 + 1 < kc1) load_chunk(kc0 + 1, ra1, rb1);
+        store_chunk(0, ra0, rb0);
+    }
+    __syncthreads();
+    for (int kc = kc0; kc < kc1; kc += 2) {
+        // even step: chunk kc in stage 0, chunk kc + 1 in set 1, chunk kc + 2 -> set 0
+        if (kc + 2 < kc1) load_chunk(kc + 2, ra0, rb0);
+        mfma_chunk(0);
+        if (kc + 1 < kc1) store_chunk(1, ra1, rb1);
+        __syncthreads();
+        if (kc + 1 >= kc1) break;
+        // odd step: chunk kc + 1 in stage 1, chunk kc + 2 in set 0, chunk kc + 3 -> set 1
+        if (kc + 3 < kc1) load_chunk(kc + 3, ra1, rb1);
+        mfma_chunk(1);
+        if (kc + 2 < kc1) store_chunk(0, ra0, rb0);
+        __syncthreads();
+    }
     }
 
     const size_t slab = (size_t)p.B * p.NI * p.NJ;
