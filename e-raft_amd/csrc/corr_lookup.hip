@@ -803,6 +803,20 @@ __device__ __forceinline__ int xcd_contiguous(int bid, int n) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
 
+// x of the previous lane of a SLOTS-lane group, 0 for the group's first lane (cx = 0).  Groups of
+// <= 16 lanes sit inside one DPP row: row_shr:1 (bound_ctrl: lane 0 of a row reads 0); larger
+// groups use a bpermute.
+template <int SLOTS>
+__device__ __forceinline__ float lane_prev(float x, int cx) {
+    if constexpr (SLOTS <= 16) {
+        const int y = __builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x111, 0xF, 0xF, true);
+        return cx == 0 ? 0.f : __int_as_float(y);
+    } else {
+        const float y = __shfl_up(x, 1, 64);
+        return cx == 0 ? 0.f : y;
+    }
+}
+
 // Orders this wave's LDS traffic (LDS executes one wave's operations in issue order; the asm
 // also keeps the compiler from moving LDS accesses across it).
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -817,7 +831,9 @@ __device__ __forceinline__ void kernarg_lookup(int t, const float *&c, const flo
     g = kp->grad[t];
 }
 
-template <int S>
+// PROBE (measurement builds only, tools/kbench_bwd.hip; the library uses 0): bit 0 = no lookup
+// loop, bit 1 = no fold (no dC / maxima), bit 2 = no LDS zero-init (wrong results, timing only).
+template <int S, int PROBE = 0>
 __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLookups lk, FusedOut o) {
     using ST = FusedStage<S>;
     constexpr int R = (S - 1) / 2, K = S * S, C = S + 1, WIN = ST::WIN;
@@ -845,7 +861,8 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     auto gg = [&](int k) -> float & { return st[ST::GG + k * BQ + q]; };
     unsigned *RM = reinterpret_cast<unsigned *>(fsm + o.aux + kFusedLv * ST::SIZE);  // [BQ]
 
-    for (int i = tid; i < o.aux; i += NT) fsm[i] = 0.0f;  // every map of the workgroup
+    if (!(PROBE & 4))
+        for (int i = tid; i < o.aux; i += NT) fsm[i] = 0.0f;  // every map of the workgroup
     if (tid < BQ) RM[tid] = 0u;
     __syncthreads();
 
@@ -866,7 +883,7 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     };
     if (act) prefetch(0);
 
-    for (int t = 0; act && t < lk.T; ++t) {  // waves of absent levels (l >= L) only join the fold
+    for (int t = 0; !(PROBE & 1) && act && t < lk.T; ++t) {  // absent levels (l >= L) only join the fold
         // ---- 1. tap cx of both axes and the upstream gradients of x-tap cx -> staging ----
         const float cxv = loader ? pcx : 0.0f, cyv = loader ? pcy : 0.0f;
         float v[S];
@@ -878,8 +895,6 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         if (cx < S) {
             tx(0, cx) = a.f, tx(1, cx) = a.lo, tx(2, cx) = a.hi;
             ty(0, cx) = c.f, ty(1, cx) = c.lo, ty(2, cx) = c.hi;
-#pragma unroll
-            for (int u = 0; u < S; ++u) gg(cx * S + u) = v[u];
             if (cx == 0) {
                 reinterpret_cast<int *>(st)[ST::AX + q] = anchor_of(a.f);
                 reinterpret_cast<int *>(st)[ST::AY + q] = anchor_of(c.f);
@@ -893,6 +908,14 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         const bool irregular = (__ballot(bad) & gmask) != 0;
         const bool far = anchor_of(fx0) == kFarAnchor || anchor_of(fy0) == kFarAnchor;
         const bool unc = qok && !window_covers<S>(fx0, tx(0, S - 1), fy0, ty(0, S - 1));
+        // the range form and the sequential scatter read any tap's gradients: stage them only
+        // when some group of the wave takes one of those paths
+        if (__ballot(irregular || unc)) {
+            if (cx < S)
+#pragma unroll
+                for (int u = 0; u < S; ++u) gg(cx * S + u) = v[u];
+            wave_lds_sync();
+        }
         const int ax = reinterpret_cast<int *>(st)[ST::AX + q], ay = reinterpret_cast<int *>(st)[ST::AY + q];
         const int X = ax + cx;
         const bool colok = qok && !unc && !far && cx < WIN && X >= 0 && X < Wl;
@@ -909,10 +932,14 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
             // go through each packed-fp32 instruction (v_pk_mul_f32 / v_pk_add_f32, IEEE per lane).
             const float wlo = cx < S ? tx(1, cx) : 0.f;
             const float whi = cx >= 1 && cx <= S ? tx(2, cx - 1) : 0.f;
-            const bool hp = cx >= 1 && cx <= S, hc = cx < S;  // x-tap cx - 1 / cx exists
             auto yv = [&](int c, int j) { return j >= 0 && j < S ? ty(c, j) : 0.f; };
-            auto gpv = [&](int j) { return hp && j >= 0 && j < S ? gg((cx - 1) * S + j) : 0.f; };
-            auto gcv = [&](int j) { return hc && j >= 0 && j < S ? gg(cx * S + j) : 0.f; };
+            // the gradients of x-tap cx are this lane's own loads (v: zero for cx >= S and for
+            // absent queries), those of x-tap cx - 1 the previous lane's (lane_prev: zero at cx = 0)
+            float gpr[S];
+#pragma unroll
+            for (int j = 0; j < S; ++j) gpr[j] = lane_prev<SLOTS>(v[j], cx);
+            auto gpv = [&](int j) { return j >= 0 && j < S ? gpr[j] : 0.f; };
+            auto gcv = [&](int j) { return j >= 0 && j < S ? v[j] : 0.f; };
             const f32x2 WH = f32x2{whi, whi}, WL = f32x2{wlo, wlo};
             float sv[C + 1];
 #pragma unroll
@@ -1013,6 +1040,7 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     }
     __syncthreads();
 
+    if constexpr ((PROBE & 2) != 0) return;
     // ---- 3. fold into level 0, write dC with its row / column maxima ----
     float rq[BQ];
 #pragma unroll

@@ -1,0 +1,112 @@
+// kbench_bwd.hip — where lookup_bwd_fold_kernel (corr_lookup.hip) spends its time at the train
+// shape (B8, 36x48, r4, L4, 12 lookups): the full kernel against probes that drop the lookup
+// loop, the fold (dC + maxima), or the LDS zero-init (timing only; wrong results).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++20 -ffp-contract=off -o tools/_build/kbench_bwd tools/kbench_bwd.hip
+//   ./kbench_bwd [rounds]
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../e-raft_amd/csrc/corr_lookup.hip"
+
+using namespace corr;
+
+#define CK(x)                                                                                 \
+    do {                                                                                      \
+        hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) {                                                               \
+            fprintf(stderr, "%s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                          \
+        }                                                                                     \
+    } while (0)
+
+__global__ void fill_coords(float *c, int B, int H, int W, unsigned seed) {
+    const int N = H * W;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B * 2 * N; i += gridDim.x * blockDim.x) {
+        const int n = i % N, axis = (i / N) % 2;
+        unsigned x = (unsigned)i * 2654435761u ^ seed;
+        x ^= x >> 13;
+        x *= 0x5bd1e995u;
+        x ^= x >> 15;
+        const float noise = ((x >> 8) * (1.0f / 16777216.0f) - 0.5f) * 6.0f;
+        c[i] = (axis == 0 ? (float)(n % W) : (float)(n / W)) + noise;
+    }
+}
+
+__global__ void fill(float *p, size_t n, unsigned seed) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned x = (unsigned)i * 2654435761u ^ seed;
+        x ^= x >> 13;
+        x *= 0x5bd1e995u;
+        p[i] = ((x >> 8) * (1.0f / 16777216.0f)) * 2.0f - 1.0f;
+    }
+}
+
+int main(int argc, char **argv) {
+    const int rounds = argc > 1 ? atoi(argv[1]) : 10;
+    constexpr int S = 9, K = S * S, PER = 4;
+    const int B = 8, H = 36, W = 48, L = 4, N = H * W, T = 12;
+    using ST = FusedStage<S>;
+    std::vector<float *> cs(T), gs(T);
+    for (int t = 0; t < T; ++t) {
+        CK(hipMalloc(&cs[t], (size_t)B * 2 * N * 4));
+        CK(hipMalloc(&gs[t], (size_t)B * L * K * N * 4));
+        hipLaunchKernelGGL(fill_coords, dim3(256), dim3(256), 0, 0, cs[t], B, H, W, 17u + t);
+        hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, gs[t], (size_t)B * L * K * N, 101u + t);
+    }
+    const int G = (N + ST::BQ - 1) / ST::BQ;
+    float *dc, *cpart;
+    unsigned *rmax;
+    CK(hipMalloc(&dc, (size_t)B * N * N * 4));
+    CK(hipMalloc(&cpart, (size_t)B * G * N * 4));
+    CK(hipMalloc(&rmax, (size_t)B * N * 4));
+    BwdLookups lk{};
+    for (int t = 0; t < T; ++t) lk.coords[t] = cs[t], lk.grad[t] = gs[t];
+    FusedOut o{};
+    o.dc = dc, o.rmax = rmax, o.cmax = nullptr, o.cpart = cpart;
+    o.B = B, o.NQ = N, o.H = H, o.W = W, o.L = L;
+    const size_t bytes = fused_lds_bytes<S>(H, W, L, &o);
+    printf("LDS %zu B per workgroup, %d workgroups\n", bytes, G * B);
+    struct V {
+        std::string name;
+        std::function<void()> run;
+        std::vector<float> us;
+    };
+    auto launch = [&](auto kern, int t_count) {
+        BwdLookups l2 = lk;
+        l2.T = t_count;
+        CK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+        hipLaunchKernelGGL(kern, dim3((unsigned)(G * B)), dim3(64 * kFusedLv), bytes, 0, l2, o);
+    };
+    std::vector<V> vs;
+    vs.push_back({"full T=12", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12); }, {}});
+    vs.push_back({"full T=1", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 1); }, {}});
+    vs.push_back({"no lookups (zero + fold)", [&] { launch(lookup_bwd_fold_kernel<S, 1>, 12); }, {}});
+    vs.push_back({"no fold T=12", [&] { launch(lookup_bwd_fold_kernel<S, 2>, 12); }, {}});
+    vs.push_back({"zero-init only", [&] { launch(lookup_bwd_fold_kernel<S, 3>, 12); }, {}});
+    vs.push_back({"fold only (no zero)", [&] { launch(lookup_bwd_fold_kernel<S, 5>, 12); }, {}});
+    vs.push_back({"empty (no zero, no fold)", [&] { launch(lookup_bwd_fold_kernel<S, 7>, 12); }, {}});
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (auto &v : vs) v.run();
+    CK(hipDeviceSynchronize());
+    for (int r = 0; r < rounds; ++r)
+        for (auto &v : vs) {
+            CK(hipEventRecord(e0, 0));
+            for (int i = 0; i < PER; ++i) v.run();
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            v.us.push_back(ms * 1e3f / PER);
+        }
+    for (auto &v : vs) {
+        std::sort(v.us.begin(), v.us.end());
+        printf("%-28s median %8.2f us  min %8.2f us\n", v.name.c_str(), v.us[v.us.size() / 2], v.us[0]);
+    }
+    return 0;
+}
