@@ -38,6 +38,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <utility>
 
 #include "corr_build_common.h"
 
@@ -153,6 +154,84 @@ __global__ __launch_bounds__(256) void split_pack_kernel(PackArgs a) {
     }
 }
 
+// Operand pack, wide form: one workgroup per PX pixels (PX / 16 image blocks) of one batch
+// item and tensor; wave w owns K steps [SPW w, SPW (w + 1)), lane = (pixel, octet half): with
+// PX = 64 a lane holds its pixel's 4 k octets of a step, with PX = 32 two of them.  Every load
+// instruction reads whole feature rows of the PX pixels (PX * 4-B runs where the blocks are
+// contiguous), the pixel maxima meet in LDS, and each lane writes its own 16-B pieces of the
+// records.  Same exponents and halves as split_pack_kernel, bit for bit.
+template <int SPW, int PX>
+__global__ __launch_bounds__(512) void split_pack_wide_kernel(PackArgs a) {
+    constexpr int OPL = 4 * PX / 64;  // k octets per lane and step
+    __shared__ float red[8][64];
+    const int z = blockIdx.z, b = blockIdx.y;
+    const int nblk = a.nblk[z];
+    if ((int)blockIdx.x * (PX / 16) >= nblk) return;  // the grid covers the larger image (uniform exit)
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+    const int pix = lane % PX, o0 = (lane / PX) * OPL;
+    const int blk = blockIdx.x * (PX / 16) + (pix >> 4), ci = pix & 15;
+    int n, exi;
+    bool valid;
+    if (z == 0) {
+        n = blk * 16 + ci;
+        valid = blk < nblk && n < a.np[0];
+        exi = b * a.NQp + n;
+    } else {
+        const int y = blk / a.CB, x = (blk - y * a.CB) * 16 + ci;
+        valid = blk < nblk && y < a.H && x < a.W;
+        n = y * a.W + x;
+        exi = (b * a.Hp + y) * a.Wp + x;
+    }
+    const int NP = a.np[z], D = a.D;
+    const float *src = a.f[z] + (size_t)b * D * NP + (valid ? n : 0);
+    float v[SPW][8 * OPL];
+#pragma unroll
+    for (int c = 0; c < SPW; ++c)
+#pragma unroll
+        for (int j = 0; j < 8 * OPL; ++j) {
+            const int d = (SPW * w + c) * kStepK + 8 * o0 + j;
+            v[c][j] = (valid && d < D) ? src[(size_t)d * NP] : 0.f;
+        }
+    float m = 0.f;
+#pragma unroll
+    for (int c = 0; c < SPW; ++c)
+#pragma unroll
+        for (int j = 0; j < 8 * OPL; ++j) m = fmaxf(m, fabsf(v[c][j]));
+    red[w][lane] = m;
+    __syncthreads();
+    float mm = 0.f;
+    for (int i = 0; i < nw; ++i)
+#pragma unroll
+        for (int h = 0; h < 64 / PX; ++h) mm = fmaxf(mm, red[i][pix + PX * h]);
+    int s = 0;
+    if (mm > 0.f && mm <= 3.402823466e38f) {
+        int E;
+        (void)frexpf(mm, &E);  // mm < 2^E
+        s = 15 - E;            // mm * 2^s < 2^15: neither half overflows
+    }
+    if (w == 0 && lane < PX && blk < nblk) a.ex[z][exi] = -s;
+#pragma unroll
+    for (int c = 0; c < SPW; ++c) {
+        const int ks = SPW * w + c;  // K step
+        if (ks >= a.S || blk >= nblk) break;
+        u32x4 *rec = a.pk[z] + (((size_t)b * a.S + ks) * nblk + blk) * kRecU;
+#pragma unroll
+        for (int oo = 0; oo < OPL; ++oo) {  // k octet of the step = fragment lane group
+            const int o = o0 + oo;
+            half8 hi8, lo8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float y = ldexpf(v[c][8 * oo + j], s);
+                const _Float16 hi = (_Float16)y;
+                hi8[j] = hi;
+                lo8[j] = __builtin_isinf(y) ? (_Float16)0.f : (_Float16)(y - (float)hi);
+            }
+            rec[16 * o + ci] = __builtin_bit_cast(u32x4, hi8);
+            rec[64 + 16 * o + ci] = __builtin_bit_cast(u32x4, lo8);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // The MFMA build.
 // ---------------------------------------------------------------------------------------
@@ -165,6 +244,7 @@ struct BuildArgs {
     int eshift;      // log2(1/sqrt(D)) when that is exact (folded into the exponent), else 0
     int exact;       // 1/sqrt(D) is a power of two
     int mode0, mode1;  // store width of levels 0 / 1: 2 = 16 B, 1 = 8 B, 0 = elements
+    int cons;          // levels 1 and 2 as 16-B stores (W/2, W/4 multiples of 4, 16-B aligned bases)
     float inv_s;     // 1/sqrt(D) otherwise (multiplied: within tolerance, not bitwise)
 };
 
@@ -392,20 +472,46 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
             l1[r][0] = pool4(v[2 * r][0], v[2 * r][1], v[2 * r + 1][0], v[2 * r + 1][1]);
             l1[r][1] = pool4(v[2 * r][2], v[2 * r][3], v[2 * r + 1][2], v[2 * r + 1][3]);
         }
-        if (!(PROBE & 8) && qok && nlev > 1) {
-            float *row1 = p.lvl[1] + qrow * N1;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if ((y0 >> 1) + r < H1) store2(row1 + (size_t)((y0 >> 1) + r) * W1, X0 >> 1, W1, l1[r][0], l1[r][1], p.mode1);
-        }
         float l2[2];
 #pragma unroll
         for (int r = 0; r < 2; ++r) l2[r] = pool4(l1[2 * r][0], l1[2 * r][1], l1[2 * r + 1][0], l1[2 * r + 1][1]);
-        if (!(PROBE & 8) && qok && nlev > 2) {
-            float *row2 = p.lvl[2] + qrow * N2;
+        if (p.cons) {
+            // Levels 1 and 2 as 16-B stores.  Level 1: lanes grp 2m and 2m + 1 hold level-1 columns
+            // x0/2 + 4m + {0,1} and {2,3} of the patch's 4 rows; they swap one row's pair (lanes 16
+            // apart) so that the even lane stores rows 0, 2 and the odd lane rows 1, 3, 4 columns each.
+            const bool odd = grp & 1;
+            const int X1 = (x0 >> 1) + 4 * (grp >> 1);
 #pragma unroll
-            for (int r = 0; r < 2; ++r)
-                if ((y0 >> 2) + r < H2 && (X0 >> 2) < W2) row2[((y0 >> 2) + r) * W2 + (X0 >> 2)] = l2[r];
+            for (int rp = 0; rp < 2; ++rp) {
+                const int ra = 2 * rp, rb = ra + 1, r = odd ? rb : ra;
+                const float g0 = __shfl_xor(odd ? l1[ra][0] : l1[rb][0], 16);
+                const float g1 = __shfl_xor(odd ? l1[ra][1] : l1[rb][1], 16);
+                const float4 o = odd ? make_float4(g0, g1, l1[rb][0], l1[rb][1]) : make_float4(l1[ra][0], l1[ra][1], g0, g1);
+                if (!(PROBE & 8) && qok && nlev > 1 && (y0 >> 1) + r < H1 && X1 < W1)
+                    *reinterpret_cast<float4 *>(p.lvl[1] + qrow * N1 + (size_t)((y0 >> 1) + r) * W1 + X1) = o;
+            }
+            // Level 2: lanes grp 0..3 hold columns x0/4 + grp of 2 rows; lane grp 0 gathers row 0,
+            // lane grp 1 row 1 (three exchanges, lanes 16, 32, 48 apart).
+            const float t16 = __shfl_xor(l2[1 - (grp & 1)], 16);
+            const float t32 = __shfl_xor(l2[grp & 1], 32);
+            const float t48 = __shfl_xor(l2[1 - (grp & 1)], 48);
+            if (!(PROBE & 8) && qok && nlev > 2 && grp < 2 && (y0 >> 2) + grp < H2 && (x0 >> 2) < W2) {
+                const float4 o = grp == 0 ? make_float4(l2[0], t16, t32, t48) : make_float4(t16, l2[1], t48, t32);
+                *reinterpret_cast<float4 *>(p.lvl[2] + qrow * N2 + (size_t)((y0 >> 2) + grp) * W2 + (x0 >> 2)) = o;
+            }
+        } else {
+            if (!(PROBE & 8) && qok && nlev > 1) {
+                float *row1 = p.lvl[1] + qrow * N1;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if ((y0 >> 1) + r < H1) store2(row1 + (size_t)((y0 >> 1) + r) * W1, X0 >> 1, W1, l1[r][0], l1[r][1], p.mode1);
+            }
+            if (!(PROBE & 8) && qok && nlev > 2) {
+                float *row2 = p.lvl[2] + qrow * N2;
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+                    if ((y0 >> 2) + r < H2 && (X0 >> 2) < W2) row2[((y0 >> 2) + r) * W2 + (X0 >> 2)] = l2[r];
+            }
         }
         // level 3: the 2x2 window of level-2 values (row pair here, column pair at lane + 16)
         const float b0 = __shfl_xor(l2[0], 16), b1 = __shfl_xor(l2[1], 16);
@@ -458,8 +564,11 @@ size_t build_split_workspace(int B, int D, int NQ, int H, int W) {
 
 bool build_split_supported(int D) { return D >= 1 && (D + kStepK - 1) / kStepK * 4 <= 16 * kMaxPackCpt; }
 
+// wide: split_pack_wide_kernel (the default); false: split_pack_kernel (kept for the A/B).
+// px: pixels per workgroup of the wide pack, 0 = by grid size (32 px unless that grid reaches
+// 1,024 workgroups: DSEC 7.4 us at 32 px vs 8.4 at 64; 1280x960 17.8 vs 15.7).
 hipError_t launch_split_pack(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, void *ws,
-                             hipStream_t s) {
+                             hipStream_t s, bool wide = true, int px = 0) {
     const SplitGeom g = split_geom(D, NQ, H, W);
     const SplitWs w = split_ws(ws, B, g);
     PackArgs a{};
@@ -469,6 +578,23 @@ hipError_t launch_split_pack(const float *f1, int NQ, const float *f2, int B, in
     a.np[0] = NQ, a.np[1] = H * W;
     a.nblk[0] = g.NQB, a.nblk[1] = g.Hp * g.CB;
     a.D = D, a.S = g.S, a.H = H, a.W = W, a.CB = g.CB, a.Hp = g.Hp, a.Wp = g.Wp, a.NQp = g.NQp;
+    if (wide) {
+        const int waves = std::min(g.S, 8), spw = (g.S + waves - 1) / waves;
+        const int nb = std::max(a.nblk[0], a.nblk[1]);
+        const dim3 blk(64 * waves);
+        const dim3 g64((unsigned)((nb + 3) / 4), B, 2), g32((unsigned)((nb + 1) / 2), B, 2);
+        const bool px32 = px == 32 || (px == 0 && (long)g32.x * B * 2 < 1024);
+        switch (spw) {
+            case 1:
+                if (px32) hipLaunchKernelGGL((split_pack_wide_kernel<1, 32>), g32, blk, 0, s, a);
+                else hipLaunchKernelGGL((split_pack_wide_kernel<1, 64>), g64, blk, 0, s, a);
+                return hipGetLastError();
+            case 2: hipLaunchKernelGGL((split_pack_wide_kernel<2, 64>), g64, blk, 0, s, a); return hipGetLastError();
+            case 3:
+            case 4: hipLaunchKernelGGL((split_pack_wide_kernel<4, 64>), g64, blk, 0, s, a); return hipGetLastError();
+            default: return hipErrorInvalidValue;
+        }
+    }
     const dim3 grid((unsigned)std::max(a.nblk[0], a.nblk[1]), B, 2), blk(256);
     switch ((4 * g.S + 15) / 16) {
 #define CORR_PACK_CASE(c) \
@@ -481,10 +607,11 @@ hipError_t launch_split_pack(const float *f1, int NQ, const float *f2, int B, in
 }
 
 // The MFMA part (operands already packed in ws).  levels == 0: the MFMAs and epilogue
-// arithmetic without stores (measurement).
+// arithmetic without stores (measurement).  cons = false: levels 1-2 as element stores (the
+// previous epilogue, kept for the A/B; same bits).
 template <int PROBE = 0>
 hipError_t launch_split_mfma(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
-                             hipStream_t s) {
+                             hipStream_t s, bool cons = true) {
     const SplitGeom g = split_geom(D, NQ, H, W);
     const SplitWs w = split_ws(ws, B, g);
     BuildArgs p{};
@@ -505,8 +632,10 @@ hipError_t launch_split_mfma(int NQ, int B, int D, int H, int W, int levels, con
     }
     p.mode0 = p.nlev > 0 ? store_mode(W, pyr.p[0]) : 0;
     p.mode1 = p.nlev > 1 ? store_mode(W >> 1, pyr.p[1]) : 0;
+    p.cons = cons && p.mode1 == 2 && (p.nlev <= 2 || store_mode(W >> 2, pyr.p[2]) == 2);
     const long tiles = (long)B * p.npatch * g.NQG;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
+    hipError_t e;
     static std::atomic<unsigned long long> lds_done[9];
     const int ss = g.S <= 8 ? g.S : 0;
     const void *fns[9] = {
@@ -515,7 +644,7 @@ hipError_t launch_split_mfma(int NQ, int B, int D, int H, int W, int levels, con
         (const void *)corr_build_split_kernel<4, PROBE>, (const void *)corr_build_split_kernel<5, PROBE>,
         (const void *)corr_build_split_kernel<6, PROBE>, (const void *)corr_build_split_kernel<7, PROBE>,
         (const void *)corr_build_split_kernel<8, PROBE>};
-    hipError_t e = ensure_lds_limit(fns[ss], kBuildLds, lds_done[ss]);
+    e = ensure_lds_limit(fns[ss], kBuildLds, lds_done[ss]);
     if (e != hipSuccess) return e;
     const dim3 grid((unsigned)tiles), blk(256);
     switch (ss) {

@@ -18,6 +18,7 @@
 #include "../e-raft_amd/csrc/corr_build.hip"
 #include "../e-raft_amd/csrc/corr_build_split.hip"
 #include "legacy/build_split_r01.hip"
+#include "legacy/build_split_ps.hip"
 
 using namespace corr;
 
@@ -120,11 +121,23 @@ int main(int argc, char **argv) {
         vs.push_back({"x3 pack only", [&](float *) {
                           return launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0);
                       }, false});
+        vs.push_back({"x3 pack only (wide 64 px)", [&](float *) {
+                          return launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, true, 64);
+                      }, false});
+        vs.push_back({"x3 pack only (256-thread)", [&](float *) {
+                          return launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, false);
+                      }, false});
         vs.push_back({"x3 mfma only", [&](float *o) {
                           return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
                       }, false});
         vs.push_back({"x3 mfma NOSTORE", [&](float *o) {
                           return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), ws, 0);
+                      }, false});
+        vs.push_back({"x3 mfma persistent (legacy)", [&](float *o) {
+                          return launch_split_mfma_ps(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
+                      }, false});
+        vs.push_back({"x3 mfma elem L1/2", [&](float *o) {
+                          return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, false);
                       }, false});
         vs.push_back({"x3 mfma L0tiled", [&](float *o) {
                           return launch_split_mfma<4>(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
@@ -164,6 +177,41 @@ int main(int argc, char **argv) {
                 std::memcpy(&rm, &hv[1], 4);
                 printf("%-10s scale %-6g %-28s max|x-f32|/max|f32| = %.3e\n", sh.name, sc, vs[k].name.c_str(), dm / rm);
             }
+        }
+        {  // the wide pack against the 256-thread pack: the whole workspace bitwise
+            std::vector<unsigned char> ha(wsb), hb(wsb);
+            CK(hipMemset(ws, 0x5a, wsb));
+            CK(launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, true));
+            CK(hipMemcpy(ha.data(), ws, wsb, hipMemcpyDeviceToHost));
+            CK(hipMemset(ws, 0x5a, wsb));
+            CK(launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, false));
+            CK(hipMemcpy(hb.data(), ws, wsb, hipMemcpyDeviceToHost));
+            printf("%-10s wide pack vs 256-thread pack, workspace: %s\n", sh.name,
+                   std::memcmp(ha.data(), hb.data(), wsb) ? "DIFFER" : "bit-identical");
+            CK(hipMemset(ws, 0x5a, wsb));
+            CK(launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, true, 64));
+            CK(hipMemcpy(ha.data(), ws, wsb, hipMemcpyDeviceToHost));
+            printf("%-10s wide pack (64 px) vs 256-thread pack, workspace: %s\n", sh.name,
+                   std::memcmp(ha.data(), hb.data(), wsb) ? "DIFFER" : "bit-identical");
+        }
+        {  // kernel variants against the one-tile-per-workgroup kernel (level-1/2 element stores): every level bitwise
+            auto same = [&](const char *what, std::function<hipError_t(float *)> fa) {
+                CK(launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0));
+                CK(hipMemset(out, 0xff, tot * 4));
+                CK(hipMemset(ref, 0x7f, tot * 4));
+                CK(fa(out));
+                CK(launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(ref), ws, 0, false));
+                std::vector<unsigned> ha(tot), hb(tot);
+                CK(hipMemcpy(ha.data(), out, tot * 4, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(hb.data(), ref, tot * 4, hipMemcpyDeviceToHost));
+                size_t bad = 0;
+                for (int l = 0; l < 4; ++l)
+                    for (size_t i = off[l]; i < off[l] + cnt[l]; ++i) bad += ha[i] != hb[i];
+                printf("%-10s %s vs 1-tile element stores, all levels: %s (%zu mismatches)\n", sh.name, what,
+                       bad ? "DIFFER" : "bit-identical", bad);
+            };
+            same("persistent (legacy)", [&](float *o) { return launch_split_mfma_ps(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
+            same("16-B level 1/2 stores", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
         }
         {  // pooling of the new kernel: every level bit-identical to avg_pool2d of its own level 0
             CK(launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), ws, 0));
