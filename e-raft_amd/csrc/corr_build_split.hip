@@ -284,6 +284,11 @@ __device__ __forceinline__ void dma16(const void *g, uint32_t lds) {
     asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(lds) : "memory");
 }
 
+// One LDS-DMA dword per lane: g -> LDS at lds + 4 * lane.
+__device__ __forceinline__ void dma4(const void *g, uint32_t lds) {
+    asm volatile("global_load_lds_dword %0, off" ::"v"(g), "{m0}"(lds) : "memory");
+}
+
 // A run of 4 at column X (a multiple of 4) of a row of width Wl; mode per level (uniform).
 __device__ __forceinline__ void store4(float *row, int X, int Wl, const float (&v)[4], int mode) {
     if (mode == 2) {
@@ -327,9 +332,17 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
     const int qb0 = tl.qg * (kQPerWG / 16) + 2 * w;  // this wave's first 16-query block
     const int S = SS > 0 ? SS : p.S;
 
-    // the patch's target exponents -> LDS (read after the first barrier)
-    if (tid < kPatchRows * 16)
+    // The patch's target exponents -> LDS by LDS-DMA (waves 0 and 1, one dword per lane) and
+    // the query exponents -> registers, issued ahead of the operand stream and never waited for
+    // on their own: they are older than every counted DMA, so step 0's wait covers them (the
+    // epilogue reads them after several barriers).  No memory round trip before the first load.
+    if (SS > 0 && w < 2) {
+        const int idx = w * 64 + lane;
+        dma4(p.et + ((size_t)b * p.Hp + y0 + (idx >> 4)) * p.Wp + x0 + (idx & 15),
+             (uint32_t)(uintptr_t)(lds_void_t *)lds_et + w * 256);
+    } else if (SS == 0 && tid < kPatchRows * 16) {
         lds_et[tid] = p.et[((size_t)b * p.Hp + y0 + (tid >> 4)) * p.Wp + x0 + (tid & 15)];
+    }
     int eqv[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) eqv[i] = p.eq[(size_t)b * p.NQp + (qb0 + i) * 16 + ci] + p.eshift;
@@ -396,7 +409,6 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
         }
     };
 
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // exponent loads out of the count
     if constexpr (SS > 0) {
         issue_q(0, 0);
         if (SS > 1) issue_q(1, 1);
@@ -418,6 +430,7 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
         }
     } else {
         // any S: no prefetch (one group in flight, drained every step)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         for (int s = 0; s < S; ++s) {
             issue_q(s, 0);
             issue_t(s, 0);

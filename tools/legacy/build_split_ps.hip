@@ -1,7 +1,7 @@
 // build_split_ps.hip — measured and dropped (round 2): the persistent role-split build kernel.
 // Included by tools/kbench_build.hip after e-raft_amd/csrc/corr_build_split.hip; not part of
 // the library.  Bit-identical to corr_build_split_kernel, but slower on every shape measured
-// (profiles/r02p_kbench_build_ps.txt: DSEC 52-56 vs 49-52 us, 1280x960 1389 vs 1007 us): with
+// (profiles/r02p_kbench_build_ps_nt_stagger_ab.txt: DSEC 52-56 vs 49-52 us, 1280x960 1389 vs 1007 us): with
 // one workgroup per CU each SIMD runs ONE MFMA wave, so the MFMA phase loses the latency
 // hiding of three co-resident workgroups (no-store 39 vs 34 us at DSEC), and the stores still
 // cost what they cost in the one-tile kernel (about 40 cycles of CU time per store
@@ -47,10 +47,6 @@ __device__ __forceinline__ void wait_vm_bar() {
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(N) : "memory");
 }
 
-// One LDS-DMA dword per lane: g -> LDS at lds + 4 * lane.
-__device__ __forceinline__ void dma4(const void *g, uint32_t lds) {
-    asm volatile("global_load_lds_dword %0, off" ::"v"(g), "{m0}"(lds) : "memory");
-}
 
 __device__ __forceinline__ void bar_lgkm() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
