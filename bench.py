@@ -317,10 +317,17 @@ def build_roofline(algo, fl, bb, t_ms, traffic_b):
     executed = 3 * fl if algo == 1 else fl
     peak = PEAK_F16_MFMA_TFLOPS if algo == 1 else PEAK_FP32_MFMA_TFLOPS
     ach = executed / (t_ms * 1e-3) / 1e12
+    # The build is bounded by BOTH its pipe and its HBM bytes (the pyramid write); report which
+    # floor binds and the fraction of that floor achieved, beside the pipe fraction above.
+    t_pipe_us = executed / (peak * 1e12) * 1e6
+    t_hbm_us = bb / (PEAK_HBM_GBS * 1e9) * 1e6
+    floor_us = max(t_pipe_us, t_hbm_us)
     return {"bound": "mfma", "kernel": BUILD_KERNELS[algo], "achieved": round(ach, 2), "peak": peak,
             "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic_b,
             "avg_us": round(t_ms * 1e3, 2), "flops_per_launch": executed, "algorithmic_fp32_flops": fl,
             "fp32_equivalent_tflops": round(fl / (t_ms * 1e-3) / 1e12, 2), "bytes_per_launch": bb,
+            "binding_floor": {"bound": "hbm" if t_hbm_us > t_pipe_us else "mfma", "pipe_floor_us": round(t_pipe_us, 2),
+                              "hbm_floor_us": round(t_hbm_us, 2), "frac": round(floor_us / (t_ms * 1e3), 4)},
             "note": BUILD_NOTE[algo]}
 
 
