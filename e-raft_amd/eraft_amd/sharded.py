@@ -100,7 +100,7 @@ def _alloc_pyramid_rows(B, NQ, H, W, num_levels, like):
 
 class _ShardState:
     __slots__ = ("levels", "grad_levels", "B", "NQ", "H", "W", "backend", "group", "h0", "h1", "full1", "stash",
-                 "radius")
+                 "radius", "token_sent")
 
 
 class _ShardBuildFn(torch.autograd.Function):
@@ -121,6 +121,7 @@ class _ShardBuildFn(torch.autograd.Function):
         st = ctx.st
         gl, st.grad_levels = st.grad_levels, None
         stash, st.stash = st.stash, []
+        st.token_sent = False
         if stash and st.NQ > 0:  # fused: every lookup's backward + fold + GEMMs in corr_backward
             df1, df2 = st.backend.backward([c for c, _ in stash], [g for _, g in stash], st.radius, f1_rows, f2,
                                            ctx.num_levels)
@@ -156,11 +157,16 @@ class _ShardLookupFn(torch.autograd.Function):
         if hasattr(st.backend, "backward") and _lib.fused_backward():
             st.radius = ctx.radius
             st.stash.append((coords_rows, grad_rows.contiguous()))  # run by the build's backward
-            return None, torch.zeros((), dtype=torch.float32, device=coords_rows.device), None, None
-        if st.grad_levels is None:
-            st.grad_levels = st.backend.zero_pyramid(st.B, st.NQ, st.H, st.W, len(st.levels), coords_rows)
-        st.backend.lookup_bwd(coords_rows, grad_rows.contiguous(), ctx.radius, st.grad_levels, st.H, st.W)
-        return None, torch.zeros((), dtype=torch.float32, device=coords_rows.device), None, None
+        else:
+            if st.grad_levels is None:
+                st.grad_levels = st.backend.zero_pyramid(st.B, st.NQ, st.H, st.W, len(st.levels), coords_rows)
+            st.backend.lookup_bwd(coords_rows, grad_rows.contiguous(), ctx.radius, st.grad_levels, st.H, st.W)
+        # one lookup per pass hands the token a gradient (its value is never read): see
+        # corr._LookupFn.backward
+        if getattr(st, "token_sent", False):
+            return None, None, None, None
+        st.token_sent = True
+        return None, coords_rows.new_empty(()), None, None
 
 
 class RowShardedCorrBlock:
