@@ -749,8 +749,10 @@ hipError_t launch_backward(int algo, const float *const *coords, const float *co
         BwdWs w{};
         const int N = H * W, G = lookup_bwd_fold_groups(NQ, radius);
         if (algo == CORR_BUILD_F16X3) {
+            // no memset: every maximum is stored whole — dC's row maxima by the fold kernel, its
+            // column maxima by colmax_reduce_kernel, F1's and F2's by rowmax2_kernel (the
+            // fallback below zeroes them for pool_fold_max_kernel's atomics itself)
             w = carve(ws, B, D, NQ, N);
-            if ((e = hipMemsetAsync(w.mx0, 0, w.mx_bytes, s)) != hipSuccess) return e;
             rmax = w.mxB, cmax = w.mxC;
             cpart = reinterpret_cast<float *>(static_cast<char *>(ws) +
                                               (build_bwd_split_workspace(B, D, NQ, H, W) + 255) / 256 * 256);
