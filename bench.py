@@ -39,7 +39,7 @@ PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA (= vector)
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec
 PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense BF16/F16 MFMA
 BUILD_ALGO = {0: "fp32", 1: "f16x3"}
-BUILD_KERNELS = {0: "corr_build_kernel", 1: "split_pack_kernel+corr_build_split_kernel"}
+BUILD_KERNELS = {0: "corr_build_kernel", 1: "split_pack_wide_kernel+corr_build_split_kernel"}
 BUILD_NOTE = {
     0: "fp32 operands on v_mfma_f32_32x32x2_f32: achieved = 2*B*N^2*D flops / build kernel time, "
        "against the fp32 MFMA peak",

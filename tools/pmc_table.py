@@ -2,7 +2,7 @@
 import collections, csv, glob, re, sys
 d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pk"
 def short(k):
-    m = re.search(r"(corr_build_split\w*|corr_build_kernel|split_pack_kernel|lookup\w*kernel)", k)
+    m = re.search(r"(corr_build_split\w*|corr_build_kernel|split_pack_wide_kernel|split_pack_kernel|lookup\w*kernel)", k)
     t = re.findall(r"Li(\d+)E", k)
     return (m.group(1) if m else k[:30]) + ("<" + ",".join(t) + ">" if t else "")
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
