@@ -332,7 +332,13 @@ constexpr int kRows = kTI + kTJ;      // LDS rows per stage (64 B each)
 constexpr int kNT = 256;
 static_assert(kTI == kNT / 2 && kTJ == kNT, "staging: one A row-octet and two B row-octets per thread");
 
-__device__ __forceinline__ int swz(int j, int u) { return j * 4 + (u ^ ((j >> 2) & 3)); }
+// LDS slot of 16-B unit u (k-octet x hi/lo) of staging row j.  The (j >> 2) & 3 term keeps the
+// fragment reads (ds_read_b128: 16-lane groups of rows {0-3, 12-15, 20-27} / {4-11, 16-19,
+// 28-31}) on 16 distinct 4-bank groups; XOR-ing 3 into it for odd j >> 1 puts the staging
+// writes (ds_write_b128, 8-lane groups) on 8 distinct 4-bank groups as well, both the row-octet
+// writes (rows 4k..4k+3 x 2 octets) and the column writes (rows 8k..8k+7) — without it rows 4k
+// and 4k + 2 collide (2-way conflicts on every staging write).  Checked exhaustively offline.
+__device__ __forceinline__ int swz(int j, int u) { return j * 4 + (u ^ ((j >> 2) & 3) ^ (((j >> 1) & 1) * 3)); }
 
 // The same GEMM reading the fp32 operands and splitting them while staging (no convert
 // kernels, no packed copies: the fp32 element is as many bytes as its hi / lo pair).  A rows
