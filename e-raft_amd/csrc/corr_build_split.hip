@@ -451,6 +451,7 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
     const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
     const int N1 = H1 * W1, N2 = H2 * W2, N3 = H3 * W3;
     const int X0 = x0 + 4 * grp;
+    float l2s[2][2];  // both blocks' level-2 values: their stores are merged below
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int q = (qb0 + i) * 16 + ci;
@@ -488,6 +489,7 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
         float l2[2];
 #pragma unroll
         for (int r = 0; r < 2; ++r) l2[r] = pool4(l1[2 * r][0], l1[2 * r][1], l1[2 * r + 1][0], l1[2 * r + 1][1]);
+        l2s[i][0] = l2[0], l2s[i][1] = l2[1];
         if (p.cons) {
             // Levels 1 and 2 as 16-B stores.  Level 1: lanes grp 2m and 2m + 1 hold level-1 columns
             // x0/2 + 4m + {0,1} and {2,3} of the patch's 4 rows; they swap one row's pair (lanes 16
@@ -503,15 +505,6 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
                 if (!(PROBE & 8) && qok && nlev > 1 && (y0 >> 1) + r < H1 && X1 < W1)
                     *reinterpret_cast<float4 *>(p.lvl[1] + qrow * N1 + (size_t)((y0 >> 1) + r) * W1 + X1) = o;
             }
-            // Level 2: lanes grp 0..3 hold columns x0/4 + grp of 2 rows; lane grp 0 gathers row 0,
-            // lane grp 1 row 1 (three exchanges, lanes 16, 32, 48 apart).
-            const float t16 = __shfl_xor(l2[1 - (grp & 1)], 16);
-            const float t32 = __shfl_xor(l2[grp & 1], 32);
-            const float t48 = __shfl_xor(l2[1 - (grp & 1)], 48);
-            if (!(PROBE & 8) && qok && nlev > 2 && grp < 2 && (y0 >> 2) + grp < H2 && (x0 >> 2) < W2) {
-                const float4 o = grp == 0 ? make_float4(l2[0], t16, t32, t48) : make_float4(t16, l2[1], t48, t32);
-                *reinterpret_cast<float4 *>(p.lvl[2] + qrow * N2 + (size_t)((y0 >> 2) + grp) * W2 + (x0 >> 2)) = o;
-            }
         } else {
             if (!(PROBE & 8) && qok && nlev > 1) {
                 float *row1 = p.lvl[1] + qrow * N1;
@@ -526,13 +519,33 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
                     if ((y0 >> 2) + r < H2 && (X0 >> 2) < W2) row2[((y0 >> 2) + r) * W2 + (X0 >> 2)] = l2[r];
             }
         }
-        // level 3: the 2x2 window of level-2 values (row pair here, column pair at lane + 16)
-        const float b0 = __shfl_xor(l2[0], 16), b1 = __shfl_xor(l2[1], 16);
-        if (!(PROBE & 8) && qok && nlev > 3 && (grp & 1) == 0) {
-            const float l3 = pool4(l2[0], b0, l2[1], b1);
-            const int Y3 = y0 >> 3, X3 = X0 >> 3;
-            if (Y3 < H3 && X3 < W3) p.lvl[3][qrow * N3 + Y3 * W3 + X3] = l3;
-        }
+    }
+    // Levels 2 and 3 of BOTH query blocks in one store instruction each.  An xor exchange has one
+    // receiver per sender, so every sender sends what its receiver's block needs.
+    if (p.cons) {
+        // Level 2: lanes grp 0..3 hold columns x0/4 + grp of 2 rows per block; lane g gathers row
+        // g & 1 of block g >> 1 (exchanges with lanes 16, 32, 48 apart), 16 B per lane.
+        const int bl = grp >> 1, rw = grp & 1;
+        // value k = 2 * block + row of this lane, by selects (a dynamic register index goes to scratch)
+        auto sel = [&](int k) { return k == 0 ? l2s[0][0] : k == 1 ? l2s[0][1] : k == 2 ? l2s[1][0] : l2s[1][1]; };
+        const float t0 = sel(grp);
+        const float t1 = __shfl_xor(sel(grp ^ 1), 16), t2 = __shfl_xor(sel(grp ^ 2), 32), t3 = __shfl_xor(sel(grp ^ 3), 48);
+        // t_d is column grp ^ d of the wanted row, so component c (column c) is t_(c ^ grp)
+        auto pick = [&](int k) { return k == 0 ? t0 : k == 1 ? t1 : k == 2 ? t2 : t3; };
+        const float4 o = make_float4(pick(grp), pick(grp ^ 1), pick(grp ^ 2), pick(grp ^ 3));
+        const int q = (qb0 + bl) * 16 + ci;
+        if (!(PROBE & 8) && q < NQ && nlev > 2 && (y0 >> 2) + rw < H2 && (x0 >> 2) < W2)
+            *reinterpret_cast<float4 *>(p.lvl[2] + ((size_t)b * NQ + q) * N2 + (size_t)((y0 >> 2) + rw) * W2 + (x0 >> 2)) = o;
+    }
+    {
+        // Level 3: the 2x2 window of level-2 values (a row pair in one lane, the column pair in the
+        // lanes 16 apart); even lanes pool block 0, odd lanes block 1, in ((a + b) + c) + d order.
+        const int bl = grp & 1;
+        const float y0v = __shfl_xor(bl ? l2s[0][0] : l2s[1][0], 16), y1v = __shfl_xor(bl ? l2s[0][1] : l2s[1][1], 16);
+        const float l3 = bl == 0 ? pool4(l2s[0][0], y0v, l2s[0][1], y1v) : pool4(y0v, l2s[1][0], y1v, l2s[1][1]);
+        const int q = (qb0 + bl) * 16 + ci;
+        const int Y3 = y0 >> 3, X3 = X0 >> 3;
+        if (!(PROBE & 8) && q < NQ && nlev > 3 && Y3 < H3 && X3 < W3) p.lvl[3][((size_t)b * NQ + q) * N3 + Y3 * W3 + X3] = l3;
     }
 }
 
