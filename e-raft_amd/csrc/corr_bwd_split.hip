@@ -412,6 +412,22 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
         gb[0] = row_inf(p.mxB, j0 + tid, p.NJ);
     }
     const bool vec = p.vec;
+    // Fast staging (wave-uniform): no staged row has an inf max and every shift has a normal
+    // 2^s (s <= 127; s >= -113 always), so x * 2^s — one v_pk_mul_f32 per element pair — is
+    // exactly ldexp(x, s) and the inf guard is dead.  Otherwise the exact split2 path.
+    bool slow_t = ga || sa > 127;
+    if (!BCOL) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) slow_t = slow_t || gb[u] || sb[u] > 127;
+    } else {
+        slow_t = slow_t || gb[0] || sb[0] > 127;
+    }
+    const bool fast = __builtin_amdgcn_ballot_w64(slow_t) == 0;
+    auto pow2f = [](int e) { return __uint_as_float((unsigned)(e + 127) << 23); };  // 2^e, normal e
+    const float fa = pow2f(fast ? sa : 0);
+    float fb[2];
+    fb[0] = pow2f(fast ? sb[0] : 0);
+    fb[1] = BCOL ? 1.0f : pow2f(fast ? sb[1] : 0);
     // BCOL: two register sets — chunk c is loaded two iterations before its MFMAs (one iteration
     // before it is staged into LDS), so a load has two MFMA phases to arrive
     float ra0[8], rb0[16], ra1[8], rb1[16];
@@ -450,10 +466,19 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
     };
     auto store_chunk = [&](int st, const float (&ra)[8], const float (&rb)[16]) {
         u32x4 *S = lds + (size_t)st * kRows * 4;
-        auto split8 = [&](const float *v, int sh, bool guard, u32x4 &hi, u32x4 &lo) {
+        auto split8 = [&](const float *v, int sh, bool guard, float f, u32x4 &hi, u32x4 &lo) {
             half2v h[4], l[4];
+            if (fast) {
 #pragma unroll
-            for (int t = 0; t < 4; ++t) split2(v[2 * t], v[2 * t + 1], sh, guard, h[t], l[t]);
+                for (int t = 0; t < 4; ++t) {
+                    const f32x2v y = f32x2v{v[2 * t], v[2 * t + 1]} * f32x2v{f, f};
+                    h[t] = __builtin_convertvector(y, half2v);
+                    l[t] = __builtin_convertvector(y - __builtin_convertvector(h[t], f32x2v), half2v);
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) split2(v[2 * t], v[2 * t + 1], sh, guard, h[t], l[t]);
+            }
             hi = u32x4{__builtin_bit_cast(unsigned, h[0]), __builtin_bit_cast(unsigned, h[1]),
                        __builtin_bit_cast(unsigned, h[2]), __builtin_bit_cast(unsigned, h[3])};
             lo = u32x4{__builtin_bit_cast(unsigned, l[0]), __builtin_bit_cast(unsigned, l[1]),
@@ -461,7 +486,7 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
         };
         {
             u32x4 hi, lo;
-            split8(ra, sa, ga, hi, lo);
+            split8(ra, sa, ga, fa, hi, lo);
             S[swz(arow, 2 * aoct)] = hi;
             S[swz(arow, 2 * aoct + 1)] = lo;
         }
@@ -469,7 +494,7 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 u32x4 hi, lo;
-                split8(rb + 8 * u, sb[u], gb[u], hi, lo);
+                split8(rb + 8 * u, sb[u], gb[u], fb[u], hi, lo);
                 S[swz(kTI + brow[u], 2 * aoct)] = hi;
                 S[swz(kTI + brow[u], 2 * aoct + 1)] = lo;
             }
@@ -477,7 +502,7 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
 #pragma unroll
             for (int o = 0; o < 2; ++o) {  // this column's two k-octets
                 u32x4 hi, lo;
-                split8(rb + 8 * o, sb[0], gb[0], hi, lo);
+                split8(rb + 8 * o, sb[0], gb[0], fb[0], hi, lo);
                 S[swz(kTI + tid, 2 * o)] = hi;
                 S[swz(kTI + tid, 2 * o + 1)] = lo;
             }
