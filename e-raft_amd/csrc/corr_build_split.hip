@@ -27,7 +27,7 @@
 // waves; each wave loads its own queries' records straight into registers, also two steps
 // ahead.  One barrier per K step.  Two workgroups per CU (49.7 KiB LDS each, <= 256 VGPRs).
 //
-// Packed operand images (split_pack_kernel), one 2 KiB record per (K step s, 16-pixel block):
+// Packed operand images (split_pack_wide_kernel), one 2 KiB record per (K step s, 16-pixel block):
 //   bytes [0, 1024)    hi: lane l = 16 grp + ci at 16 l: 8 f16 of k = 32 s + 8 grp + j, pixel ci
 //   bytes [1024, 2048) lo: the same positions
 // i.e. exactly the MFMA fragment image of that block, so the LDS fill and every fragment read
@@ -89,77 +89,13 @@ struct PackArgs {
     int D, S, H, W, CB, Hp, Wp, NQp;
 };
 
-template <int CPT>
-__global__ __launch_bounds__(256) void split_pack_kernel(PackArgs a) {
-    __shared__ float red[4][16];
-    const int z = blockIdx.z, b = blockIdx.y, blk = blockIdx.x;
-    if (blk >= a.nblk[z]) return;  // the grid covers the larger image (uniform exit)
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int ci = lane & 15, og = (w << 2) | (lane >> 4);
-    int n, exi;
-    bool valid;
-    if (z == 0) {
-        n = blk * 16 + ci;
-        valid = n < a.np[0];
-        exi = b * a.NQp + n;
-    } else {
-        const int y = blk / a.CB, x = (blk - y * a.CB) * 16 + ci;
-        valid = y < a.H && x < a.W;
-        n = y * a.W + x;
-        exi = (b * a.Hp + y) * a.Wp + x;
-    }
-    const int NP = a.np[z], D = a.D;
-    const float *src = a.f[z] + (size_t)b * D * NP + (valid ? n : 0);
-    float v[CPT][8];
-#pragma unroll
-    for (int c = 0; c < CPT; ++c)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int d = 8 * (og + 16 * c) + j;
-            v[c][j] = (valid && d < D) ? src[(size_t)d * NP] : 0.f;
-        }
-    float m = 0.f;
-#pragma unroll
-    for (int c = 0; c < CPT; ++c)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(v[c][j]));
-    m = fmaxf(m, __shfl_xor(m, 16));
-    m = fmaxf(m, __shfl_xor(m, 32));
-    if (lane < 16) red[w][ci] = m;
-    __syncthreads();
-    const float mm = fmaxf(fmaxf(red[0][ci], red[1][ci]), fmaxf(red[2][ci], red[3][ci]));
-    int s = 0;
-    if (mm > 0.f && mm <= 3.402823466e38f) {
-        int E;
-        (void)frexpf(mm, &E);  // mm < 2^E
-        s = 15 - E;            // mm * 2^s < 2^15: neither half overflows
-    }
-    if (tid < 16) a.ex[z][exi] = -s;
-    const int OCT = 4 * a.S;
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) {
-        const int o = og + 16 * c;
-        if (o >= OCT) break;
-        half8 hi8, lo8;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float y = ldexpf(v[c][j], s);
-            const _Float16 hi = (_Float16)y;
-            hi8[j] = hi;
-            lo8[j] = __builtin_isinf(y) ? (_Float16)0.f : (_Float16)(y - (float)hi);
-        }
-        u32x4 *rec = a.pk[z] + (((size_t)b * a.S + (o >> 2)) * a.nblk[z] + blk) * kRecU;
-        rec[lane] = __builtin_bit_cast(u32x4, hi8);  // lane = 16 (o & 3) + ci
-        rec[64 + lane] = __builtin_bit_cast(u32x4, lo8);
-    }
-}
-
 // Operand pack, wide form: one workgroup per PX pixels (PX / 16 image blocks) of one batch
 // item and tensor; wave w owns K steps [SPW w, SPW (w + 1)), lane = (pixel, octet half): with
 // PX = 64 a lane holds its pixel's 4 k octets of a step, with PX = 32 two of them.  Every load
 // instruction reads whole feature rows of the PX pixels (PX * 4-B runs where the blocks are
 // contiguous), the pixel maxima meet in LDS, and each lane writes its own 16-B pieces of the
-// records.  Same exponents and halves as split_pack_kernel, bit for bit.
+// records.  Same exponents and halves as the round-1 256-thread pack (tools/legacy/pack_256.hip),
+// bit for bit.
 template <int SPW, int PX>
 __global__ __launch_bounds__(512) void split_pack_wide_kernel(PackArgs a) {
     constexpr int OPL = 4 * PX / 64;  // k octets per lane and step
@@ -590,11 +526,10 @@ size_t build_split_workspace(int B, int D, int NQ, int H, int W) {
 
 bool build_split_supported(int D) { return D >= 1 && (D + kStepK - 1) / kStepK * 4 <= 16 * kMaxPackCpt; }
 
-// wide: split_pack_wide_kernel (the default); false: split_pack_kernel (kept for the A/B).
-// px: pixels per workgroup of the wide pack, 0 = by grid size (32 px unless that grid reaches
-// 1,024 workgroups: DSEC 7.4 us at 32 px vs 8.4 at 64; 1280x960 17.8 vs 15.7).
+// px: pixels per workgroup, 0 = by grid size (32 px unless that grid reaches 1,024 workgroups:
+// DSEC 7.4 us at 32 px vs 8.4 at 64; 1280x960 17.8 vs 15.7).
 hipError_t launch_split_pack(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, void *ws,
-                             hipStream_t s, bool wide = true, int px = 0) {
+                             hipStream_t s, int px = 0) {
     const SplitGeom g = split_geom(D, NQ, H, W);
     const SplitWs w = split_ws(ws, B, g);
     PackArgs a{};
@@ -604,30 +539,19 @@ hipError_t launch_split_pack(const float *f1, int NQ, const float *f2, int B, in
     a.np[0] = NQ, a.np[1] = H * W;
     a.nblk[0] = g.NQB, a.nblk[1] = g.Hp * g.CB;
     a.D = D, a.S = g.S, a.H = H, a.W = W, a.CB = g.CB, a.Hp = g.Hp, a.Wp = g.Wp, a.NQp = g.NQp;
-    if (wide) {
-        const int waves = std::min(g.S, 8), spw = (g.S + waves - 1) / waves;
-        const int nb = std::max(a.nblk[0], a.nblk[1]);
-        const dim3 blk(64 * waves);
-        const dim3 g64((unsigned)((nb + 3) / 4), B, 2), g32((unsigned)((nb + 1) / 2), B, 2);
-        const bool px32 = px == 32 || (px == 0 && (long)g32.x * B * 2 < 1024);
-        switch (spw) {
-            case 1:
-                if (px32) hipLaunchKernelGGL((split_pack_wide_kernel<1, 32>), g32, blk, 0, s, a);
-                else hipLaunchKernelGGL((split_pack_wide_kernel<1, 64>), g64, blk, 0, s, a);
-                return hipGetLastError();
-            case 2: hipLaunchKernelGGL((split_pack_wide_kernel<2, 64>), g64, blk, 0, s, a); return hipGetLastError();
-            case 3:
-            case 4: hipLaunchKernelGGL((split_pack_wide_kernel<4, 64>), g64, blk, 0, s, a); return hipGetLastError();
-            default: return hipErrorInvalidValue;
-        }
-    }
-    const dim3 grid((unsigned)std::max(a.nblk[0], a.nblk[1]), B, 2), blk(256);
-    switch ((4 * g.S + 15) / 16) {
-#define CORR_PACK_CASE(c) \
-    case c: hipLaunchKernelGGL(split_pack_kernel<c>, grid, blk, 0, s, a); return hipGetLastError();
-        CORR_PACK_CASE(1) CORR_PACK_CASE(2) CORR_PACK_CASE(3) CORR_PACK_CASE(4)
-        CORR_PACK_CASE(5) CORR_PACK_CASE(6) CORR_PACK_CASE(7) CORR_PACK_CASE(8)
-#undef CORR_PACK_CASE
+    const int waves = std::min(g.S, 8), spw = (g.S + waves - 1) / waves;
+    const int nb = std::max(a.nblk[0], a.nblk[1]);
+    const dim3 blk(64 * waves);
+    const dim3 g64((unsigned)((nb + 3) / 4), B, 2), g32((unsigned)((nb + 1) / 2), B, 2);
+    const bool px32 = px == 32 || (px == 0 && (long)g32.x * B * 2 < 1024);
+    switch (spw) {
+        case 1:
+            if (px32) hipLaunchKernelGGL((split_pack_wide_kernel<1, 32>), g32, blk, 0, s, a);
+            else hipLaunchKernelGGL((split_pack_wide_kernel<1, 64>), g64, blk, 0, s, a);
+            return hipGetLastError();
+        case 2: hipLaunchKernelGGL((split_pack_wide_kernel<2, 64>), g64, blk, 0, s, a); return hipGetLastError();
+        case 3:
+        case 4: hipLaunchKernelGGL((split_pack_wide_kernel<4, 64>), g64, blk, 0, s, a); return hipGetLastError();
         default: return hipErrorInvalidValue;
     }
 }

@@ -293,7 +293,7 @@ __global__ __launch_bounds__(kCmCols *kCmSlices) void colmax_reduce_kernel(const
     }
 }
 
-// Exponent of a row from its max (as split_pack_kernel): max * 2^s < 2^15.
+// Exponent of a row from its max (as split_pack_wide_kernel): max * 2^s < 2^15.
 __device__ __forceinline__ int split_shift(float mm) {
     int s = 0;
     if (mm > 0.f && mm <= 3.402823466e38f) {

@@ -19,6 +19,7 @@
 #include "../e-raft_amd/csrc/corr_build_split.hip"
 #include "legacy/build_split_r01.hip"
 #include "legacy/build_split_ps.hip"
+#include "legacy/pack_256.hip"
 
 using namespace corr;
 
@@ -122,10 +123,10 @@ int main(int argc, char **argv) {
                           return launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0);
                       }, false});
         vs.push_back({"x3 pack only (wide 64 px)", [&](float *) {
-                          return launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, true, 64);
+                          return launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, 64);
                       }, false});
         vs.push_back({"x3 pack only (256-thread)", [&](float *) {
-                          return launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, false);
+                          return launch_split_pack_256(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0);
                       }, false});
         vs.push_back({"x3 mfma only", [&](float *o) {
                           return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
@@ -181,15 +182,15 @@ int main(int argc, char **argv) {
         {  // the wide pack against the 256-thread pack: the whole workspace bitwise
             std::vector<unsigned char> ha(wsb), hb(wsb);
             CK(hipMemset(ws, 0x5a, wsb));
-            CK(launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, true));
+            CK(launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0));
             CK(hipMemcpy(ha.data(), ws, wsb, hipMemcpyDeviceToHost));
             CK(hipMemset(ws, 0x5a, wsb));
-            CK(launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, false));
+            CK(launch_split_pack_256(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0));
             CK(hipMemcpy(hb.data(), ws, wsb, hipMemcpyDeviceToHost));
             printf("%-10s wide pack vs 256-thread pack, workspace: %s\n", sh.name,
                    std::memcmp(ha.data(), hb.data(), wsb) ? "DIFFER" : "bit-identical");
             CK(hipMemset(ws, 0x5a, wsb));
-            CK(launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, true, 64));
+            CK(launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, 64));
             CK(hipMemcpy(ha.data(), ws, wsb, hipMemcpyDeviceToHost));
             printf("%-10s wide pack (64 px) vs 256-thread pack, workspace: %s\n", sh.name,
                    std::memcmp(ha.data(), hb.data(), wsb) ? "DIFFER" : "bit-identical");
