@@ -708,14 +708,16 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     return launch_splitk_reduce(slab, C, p.splits, (size_t)B * NI * NJ, sD, s);
 }
 
+// rowmax_done: F2's and F1's row maxima are already in w.mxA / w.mxA2 (computed by the fold
+// launch's appended workgroups).
 hipError_t bwd_split_gemms(const float *grad_c, const float *f1, int NQ, const float *f2, int B, int D, int H, int W,
-                           float *df1, float *df2, const BwdWs &w, hipStream_t s) {
+                           float *df1, float *df2, const BwdWs &w, hipStream_t s, bool rowmax_done = false) {
     const int N = H * W;
     const float sD = std::sqrt((float)D);
     hipError_t e;
 #define CK_(x)                          \
     if ((e = (x)) != hipSuccess) return e;
-    CK_(rowmax2(f2, N, w.mxA, f1, NQ, w.mxA2, B, D, s));
+    if (!rowmax_done) CK_(rowmax2(f2, N, w.mxA, f1, NQ, w.mxA2, B, D, s));
     // dF1 = F2 . dC^T : A = F2 rows d (k = m), B = dC rows n (k = m)
     CK_(gemm_f32<false>(f2, (long)D * N, N, grad_c, (long)NQ * N, N, 1, w.mxA, w.mxB, B, D, NQ, N, sD, df1, w.slab, s));
     // dF2 = F1 . dC : A = F1 rows d (k = n), B = dC columns m (k = n)
@@ -788,13 +790,21 @@ hipError_t launch_backward(int algo, const float *const *coords, const float *co
             cpart = reinterpret_cast<float *>(static_cast<char *>(ws) +
                                               (build_bwd_split_workspace(B, D, NQ, H, W) + 255) / 256 * 256);
         }
-        e = launch_lookup_bwd_fold(coords, grad_out, T, B, NQ, H, W, levels, radius, gpyr.p[0], rmax, cmax, cpart, s);
+        FoldRowMax rm{};
+        if (algo == CORR_BUILD_F16X3) {  // F2's and F1's row maxima in the fold launch's tail
+            rm.x[0] = f2, rm.x[1] = f1;
+            rm.out[0] = w.mxA, rm.out[1] = w.mxA2;
+            rm.cols[0] = N, rm.cols[1] = NQ;
+            rm.rows = D;
+        }
+        e = launch_lookup_bwd_fold(coords, grad_out, T, B, NQ, H, W, levels, radius, gpyr.p[0], rmax, cmax, cpart, s,
+                                   rm);
         if (e == hipSuccess) {
             if (algo == CORR_BUILD_F16X3) {
                 hipLaunchKernelGGL(colmax_reduce_kernel, dim3((unsigned)((N + kCmCols - 1) / kCmCols), (unsigned)B),
                                    dim3(kCmCols * kCmSlices), 0, s, cpart, G, N, cmax);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
-                return bwd_split_gemms(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, w, s);
+                return bwd_split_gemms(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, w, s, true);
             }
             return launch_build_bwd(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, (float *)ws, s);
         }

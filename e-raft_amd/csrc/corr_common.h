@@ -40,9 +40,17 @@ hipError_t launch_pool_bwd(const LevelPtrs &gpyr, long BN, int H, int W, int lev
 hipError_t launch_lookup_bwd_multi(const float *const *coords, const float *const *grad_out, int T, int B, int NQ,
                                    int H, int W, int levels, int radius, const LevelPtrs &gpyr, hipStream_t s);
 int lookup_bwd_fold_groups(int NQ, int radius);
+// Row |max| of two row-major operands [B][rows][cols[t]] (the backward GEMMs' F2 and F1 row
+// maxima), computed by extra workgroups appended to a launch's grid; out[t] gets float bits.
+struct FoldRowMax {
+    const float *x[2];
+    unsigned *out[2];
+    int cols[2];
+    int rows;  // 0: none
+};
 hipError_t launch_lookup_bwd_fold(const float *const *coords, const float *const *grad_out, int T, int B, int NQ,
                                   int H, int W, int levels, int radius, float *dc, unsigned *rmax, unsigned *cmax,
-                                  float *cpart, hipStream_t s);
+                                  float *cpart, hipStream_t s, const FoldRowMax &rm = FoldRowMax{});
 size_t backward_workspace(int algo, int B, int D, int NQ, int H, int W, int radius);
 hipError_t launch_pool_fold(const LevelPtrs &gpyr, int B, int NQ, int H, int W, int levels, void *ws, int D,
                             hipStream_t s);

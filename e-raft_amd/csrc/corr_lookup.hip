@@ -781,7 +781,40 @@ struct FusedOut {
     int moff[kFusedLv], msz[kFusedLv];  // LDS float offset of level l's maps, cells per map
     int qstr[kFusedLv];                 // LDS floats between two queries' maps (bank-staggered)
     int aux;                            // LDS float offset of the per-wave staging
+    int nfold;                          // fold workgroups; blocks past them compute rm
+    int rm_rows_per_wave;
+    FoldRowMax rm;
 };
+
+// Row |max| work of the blocks appended to the fold grid (rowmax2_kernel's per-row reduction:
+// a wave walks each of its rows with 16-B loads, one cross-lane reduction per row).  They sit
+// at the end of the grid, so they run in the fold's last, partly empty round of workgroups.
+__device__ __forceinline__ void fold_rowmax_block(const FusedOut &o, int blk) {
+    const FoldRowMax &a = o.rm;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int per_op = o.B * a.rows;  // rows of one operand, over the batch
+    for (int k = 0; k < o.rm_rows_per_wave; ++k) {
+        const int g = (blk * kFusedLv + wv) * o.rm_rows_per_wave + k;
+        if (g >= 2 * per_op) return;  // whole waves
+        const int t = g / per_op, br = g - t * per_op;
+        const int cols = a.cols[t];
+        const float *x = a.x[t] + (size_t)br * cols;
+        float m = 0.f;
+        if ((cols & 3) == 0 && ((uintptr_t)a.x[t] & 15) == 0) {
+#pragma unroll 4
+            for (int c = lane * 4; c < cols; c += 256) {
+                const float4 q = *reinterpret_cast<const float4 *>(x + c);
+                m = fmaxf(m, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w))));
+            }
+        } else {
+#pragma unroll 4
+            for (int c = lane; c < cols; c += 64) m = fmaxf(m, fabsf(x[c]));
+        }
+#pragma unroll
+        for (int sh = 32; sh >= 1; sh >>= 1) m = fmaxf(m, __shfl_xor(m, sh));
+        if (lane == 0) a.out[t][br] = m > 0.f ? __float_as_uint(m) : 0u;
+    }
+}
 
 // Per-wave staging (floats): taps TX/TY [3][S][BQ], gradients [K][BQ], anchors [2][BQ], dump
 // slots [64].
@@ -840,9 +873,13 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     constexpr int SLOTS = ST::SLOTS, BQ = ST::BQ, NT = 64 * kFusedLv;
     extern __shared__ float fsm[];
 
+    if ((int)blockIdx.x >= o.nfold) {  // appended row-maxima blocks (uniform per workgroup)
+        fold_rowmax_block(o, (int)blockIdx.x - o.nfold);
+        return;
+    }
     const int NQ = o.NQ, H = o.H, W = o.W, L = o.L, N = H * W;
     const int nqb = (NQ + BQ - 1) / BQ;
-    const int blk = xcd_contiguous(blockIdx.x, gridDim.x);
+    const int blk = xcd_contiguous(blockIdx.x, o.nfold);
     const int b = blk / nqb, n0 = (blk - b * nqb) * BQ;
     const int tid = threadIdx.x, lane = tid & 63;
     const int l = tid >> 6;  // wave = level
@@ -1332,7 +1369,17 @@ hipError_t launch_fused_s(const BwdLookups &lk, FusedOut o, hipStream_t s) {
     hipError_t e = ensure_lds_limit((const void *)lookup_bwd_fold_kernel<S>, (int)bytes, done);
     if (e != hipSuccess) return e;
     const int nqb = (o.NQ + FusedStage<S>::BQ - 1) / FusedStage<S>::BQ;
-    hipLaunchKernelGGL(lookup_bwd_fold_kernel<S>, dim3((unsigned)(nqb * o.B)), dim3(64 * kFusedLv), bytes, s, lk, o);
+    o.nfold = nqb * o.B;
+    // row-maxima blocks: at most half a round of workgroup slots (the fold's tail), >= 1 row per wave
+    int extra = 0;
+    if (o.rm.rows > 0) {
+        const long rows = 2L * o.B * o.rm.rows;
+        const long cap = std::max(1L, (long)(256 * std::max<size_t>(1, 160 * 1024 / bytes)) / 2);
+        o.rm_rows_per_wave = (int)std::max(1L, (rows + cap * kFusedLv - 1) / (cap * kFusedLv));
+        extra = (int)((rows + (long)o.rm_rows_per_wave * kFusedLv - 1) / ((long)o.rm_rows_per_wave * kFusedLv));
+    }
+    hipLaunchKernelGGL(lookup_bwd_fold_kernel<S>, dim3((unsigned)(o.nfold + extra)), dim3(64 * kFusedLv), bytes, s,
+                       lk, o);
     return hipGetLastError();
 }
 }  // namespace
@@ -1345,7 +1392,7 @@ int lookup_bwd_fold_groups(int NQ, int radius) {
 
 hipError_t launch_lookup_bwd_fold(const float *const *coords, const float *const *grad_out, int T, int B, int NQ,
                                   int H, int W, int levels, int radius, float *dc, unsigned *rmax, unsigned *cmax,
-                                  float *cpart, hipStream_t s) {
+                                  float *cpart, hipStream_t s, const FoldRowMax &rm) {
     if (T < 1 || T > kMaxLookups || levels < 1 || levels > kFusedLv) return hipErrorNotSupported;
     BwdLookups lk{};
     lk.T = T;
@@ -1356,6 +1403,7 @@ hipError_t launch_lookup_bwd_fold(const float *const *coords, const float *const
     FusedOut o{};
     o.dc = dc, o.rmax = rmax, o.cmax = cmax, o.cpart = cpart;
     o.B = B, o.NQ = NQ, o.H = H, o.W = W, o.L = levels;
+    o.rm = rm;
     switch (radius) {
         case 0: return launch_fused_s<1>(lk, o, s);
         case 1: return launch_fused_s<3>(lk, o, s);

@@ -68,6 +68,7 @@ int main(int argc, char **argv) {
     FusedOut o{};
     o.dc = dc, o.rmax = rmax, o.cmax = nullptr, o.cpart = cpart;
     o.B = B, o.NQ = N, o.H = H, o.W = W, o.L = L;
+    o.nfold = G * B;  // no appended row-maxima blocks
     const size_t bytes = fused_lds_bytes<S>(H, W, L, &o);
     printf("LDS %zu B per workgroup, %d workgroups\n", bytes, G * B);
     struct V {
