@@ -104,7 +104,13 @@ def traffic(workload, kernel):
     16-B/lane streaming reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, in bytes.  The PMC
     passes are separate rocprofv3 runs of this script; null when no profile exists."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_pmc.json")))
+    import re
+
+    def tag_order(path):  # r02u < r02z < r02aa < r02ac < r03a: round, then suffix length, then suffix
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_pmc.json")), key=tag_order)
     if not files:
         return None
     with open(files[-1]) as fh:
