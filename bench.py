@@ -98,11 +98,18 @@ def lookup_bytes(B, H, W, L, r):
     return B * N * (L * (2 * r + 2) ** 2 * 4 + L * (2 * r + 1) ** 2 * 4 + 8)
 
 
+# FETCH_SIZE correction per kernel, calibrated on known byte counts (tools/kbench_fetchcal.hip,
+# profiles/r02ag_fetch_size_calibration.txt): coalesced streams (16-B or 4-B per lane, and the
+# build's LDS-DMA) report half their bytes (x2, as MI355X_MICROARCH.md §HBM states for 16-B
+# streams); the lookup's scattered 44-B window rows are counted at face value in 64-B sectors (x1).
+FETCH_FACTOR = {"lookup_kernel": 1}
+
+
 def traffic(workload, kernel):
     """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/*_pmc.json,
-    written by tools/pmc_summary.py --json): FETCH_SIZE x 2 (gfx950 reports half the bytes of
-    16-B/lane streaming reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, in bytes.  The PMC
-    passes are separate rocprofv3 runs of this script; null when no profile exists."""
+    written by tools/pmc_summary.py --json): FETCH_SIZE x FETCH_FACTOR (2 unless calibrated
+    otherwise) + WRITE_SIZE, in bytes.  The PMC passes are separate rocprofv3 runs of this
+    script; null when no profile exists."""
     import glob
     import re
 
@@ -118,7 +125,7 @@ def traffic(workload, kernel):
     k = d.get("kernels", {}).get(kernel)
     if not k or "FETCH_SIZE" not in k or "WRITE_SIZE" not in k:
         return None
-    return int(round((2 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024))
+    return int(round((FETCH_FACTOR.get(kernel, 2) * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024))
 
 
 def build_traffic(workload, algo):
