@@ -408,6 +408,40 @@ def test_build_bwd_vs_oracle(B, D, H, W, algo, spread):
     assert norm_rel(g2.cpu().numpy(), d2) < REL_TOL
 
 
+def test_build_bwd_special_rows_vs_oracle():
+    """The f16x3 backward GEMMs' exact staging path: waves that stage a row whose max is below
+    2^-112 (shift > 127: 2^s is not a float, so the split keeps ldexp) or whose max is inf (the
+    lo-half guard) take it; the others the fast one-multiply split.  dC rows / columns and fmap
+    feature rows at 1e-36, one inf and a few NaN entries, against the fp64 oracle: the same
+    non-finite pattern, and every finite output column / row within 1e-5 of its OWN scale (so
+    the tiny outputs are checked, not hidden under the global max)."""
+    from eraft_amd import _lib
+    B, D, H, W = 1, 64, 12, 16
+    N = H * W
+    f1, f2 = prng.gauss(21, (B, D, H, W)), prng.gauss(22, (B, D, H, W))
+    gc = prng.gauss(23, (B * N, N))
+    gc[[5, 77, 150]] *= np.float32(1e-36)     # tiny dC rows (dF1 columns)
+    gc[:, [9, 100]] *= np.float32(1e-36)      # tiny dC columns (dF2 columns)
+    f1[0, 3] *= np.float32(1e-36)             # tiny feature rows of both operands
+    f2[0, 7] *= np.float32(1e-36)
+    gc[40, 60] = np.float32(np.inf)
+    gc[120, [3, 4]] = np.float32(np.nan)
+    d1, d2 = oracle.corr_bwd(gc.reshape(B * N, 1, H, W), f1, f2)
+    g1, g2 = _lib.build_bwd(torch.from_numpy(gc).to(DEV), torch.from_numpy(f1).to(DEV),
+                            torch.from_numpy(f2).to(DEV), _lib.BUILD_F16X3)
+    g1, g2 = g1.cpu().numpy().reshape(D, N), g2.cpu().numpy().reshape(D, N)
+    r1, r2 = np.asarray(d1).reshape(D, N), np.asarray(d2).reshape(D, N)
+    for got, ref in ((g1, r1), (g2, r2)):
+        assert np.array_equal(np.isfinite(got), np.isfinite(ref))
+        fin = np.isfinite(ref)
+        ref_f, got_f = np.where(fin, ref, 0.0), np.where(fin, got.astype(np.float64), 0.0)
+        for axis in (0, 1):  # per output column (query / target pixel), then per feature row
+            scale = np.abs(ref_f).max(axis=axis)
+            err = np.abs(got_f - ref_f).max(axis=axis)
+            ok = (scale == 0) | (err <= 1e-5 * scale)
+            assert ok.all(), (axis, np.flatnonzero(~ok)[:8], (err / np.maximum(scale, 1e-300)).max())
+
+
 def test_training_shape_backward_vs_oracle():
     """BASELINE config 4 shape (36x48 fmaps), B and D reduced so the C oracle stays fast."""
     B, D, H, W, L, r = 2, 32, 36, 48, 4, 4
