@@ -117,6 +117,11 @@ int main(int argc, char **argv) {
         vs.push_back({"QB32", [=](float *o) { return launch_qb<32>(lp, coords, B, H, W, o); }, {}});
         vs.push_back({"QB64", [=](float *o) { return launch_qb<64>(lp, coords, B, H, W, o); }, {}});
         vs.push_back({"QB8", [=](float *o) { return launch_qb<8>(lp, coords, B, H, W, o); }, {}});
+        // thread counts that fill whole waves (QB * 9 just below a multiple of 64)
+        vs.push_back({"QB7", [=](float *o) { return launch_qb<7>(lp, coords, B, H, W, o); }, {}});
+        vs.push_back({"QB14", [=](float *o) { return launch_qb<14>(lp, coords, B, H, W, o); }, {}});
+        vs.push_back({"QB28", [=](float *o) { return launch_qb<28>(lp, coords, B, H, W, o); }, {}});
+        vs.push_back({"QB56", [=](float *o) { return launch_qb<56>(lp, coords, B, H, W, o); }, {}});
         vs.push_back({"prod smooth-flow", [=](float *o) { return launch_lookup(lp, coords_s, B, H * W, H, W, 4, 4, o, 0); }, {}});
         vs.push_back({"prod grid (integer)", [=](float *o) { return launch_lookup(lp, coords_g, B, H * W, H, W, 4, 4, o, 0); }, {}});
         vs.push_back({"QB16 smooth-flow", [=](float *o) { return launch_qb<16>(lp, coords_s, B, H, W, o); }, {}});
