@@ -448,25 +448,26 @@ def main():
         run_lookups()
         torch.cuda.synchronize()
 
-        # row-sharded, N > 1: fmap2 double-buffered.  Pair k's fmap2 arrived during pair k-1;
-        # pair k issues the (async, RCCL stream) broadcast of pair k+1's fmap2 and builds from its
-        # own buffer meanwhile, so the broadcast overlaps the build and the 12 lookups.
-        f2bufs = [f2, f2.clone()] if sharded and world > 1 else [f2]
-        pipe = {"k": 0, "work": None}
+        # row-sharded, N > 1: the product API for a stream of pairs (eraft_amd.sharded):
+        # Fmap2DoubleBuffer.prefetch issues pair k+1's fmap2 broadcast (async, RCCL stream) before
+        # pair k's RowShardedCorrBlock is built from the buffer whose broadcast was issued one
+        # pair earlier, so the broadcast overlaps the build and the 12 lookups.
+        pipe = {"pending": None}
         if sharded and world > 1:
-            dist.broadcast(f2bufs[0], src=0)  # prologue: pair 0's fmap2
+            from eraft_amd.sharded import Fmap2DoubleBuffer, RowShardedCorrBlock
+            dbuf = Fmap2DoubleBuffer(tuple(f2.shape), dev)
+            pipe["pending"] = dbuf.prefetch(f2 if rank == 0 else None)  # prologue: pair 0's fmap2
 
         def pair():
             if sharded and world > 1:
-                k = pipe["k"]
-                if pipe["work"] is not None:
-                    pipe["work"].wait()  # pair k's fmap2 (the stream waits, not the host)
-                pipe["work"] = dist.broadcast(f2bufs[(k + 1) % 2], src=0, async_op=True)
-                _lib.build(f1, f2bufs[k % 2], pyr, algo, ws)
-                pipe["k"] = k + 1
+                cur = pipe["pending"]
+                pipe["pending"] = dbuf.prefetch(f2 if rank == 0 else None)
+                blk = RowShardedCorrBlock(f1, cur, num_levels=L, radius=r, fmap1_is_slab=True)
+                for c in coords:
+                    blk(c)
             else:
                 build_only()
-            run_lookups()
+                run_lookups()
 
         launch = "eager" if args.eager or (sharded and world > 1) else "hipgraph"
         step = pair
@@ -493,11 +494,6 @@ def main():
 
         for _ in range(args.warmup):
             step()
-        if pipe["work"] is not None:
-            pipe["work"].wait()
-            pipe["work"] = None
-            pipe["k"] = 0
-            dist.broadcast(f2bufs[0], src=0)
         torch.cuda.synchronize()
 
         if world > 1:
@@ -506,9 +502,8 @@ def main():
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
-        if pipe["work"] is not None:  # the in-flight broadcast counts inside the timed region
-            pipe["work"].wait()
-            pipe["work"] = None
+        if pipe["pending"] is not None:  # the in-flight broadcast counts inside the timed region
+            pipe["pending"].wait()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         if world > 1:
@@ -604,9 +599,9 @@ def main():
         if bcast_ms is not None:
             res["sharded_timing"] = {
                 "per_rank": per_rank,
-                "overlap": "fmap2 double-buffered: pair k+1's broadcast (async, on the collective stream) "
-                           "runs during pair k's build + lookups; per-rank broadcast_ms is the broadcast "
-                           "timed alone",
+                "overlap": "eraft_amd.sharded.Fmap2DoubleBuffer: pair k+1's broadcast (async, on the "
+                           "collective stream) runs during pair k's RowShardedCorrBlock build + lookups; "
+                           "per-rank broadcast_ms is the broadcast timed alone",
                 "backend": os.environ.get("ERAFT_AMD_DIST_BACKEND", "nccl")}
         if world == 1 and not args.no_cpu_baseline and wl_name not in CPU_SKIP:
             cb = cpu_baseline(wl, args.cpu_seconds, train)

@@ -77,7 +77,7 @@ using namespace corr;
 
 extern "C" {
 
-int corr_version(void) { return 101; }
+int corr_version(void) { return 102; }
 
 const char *corr_last_error(void) { return g_err; }
 

@@ -182,6 +182,7 @@ struct BuildArgs {
     int mode0, mode1;  // store width of levels 0 / 1: 2 = 16 B, 1 = 8 B, 0 = elements
     int cons;          // levels 1 and 2 as 16-B stores (W/2, W/4 multiples of 4, 16-B aligned bases)
     float inv_s;     // 1/sqrt(D) otherwise (multiplied: within tolerance, not bitwise)
+    int ntiles;      // persistent kernel: B * npatch * NQG
 };
 
 // Tile order (L2 reuse): per batch item, query groups in groups of kGroupQ; inside a group the
@@ -486,6 +487,305 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Persistent form (the default wherever it applies: S = 4 or 8 K steps, 4+ levels, levels 0-2
+// stored as 16-B runs).  Same tiles, same arithmetic and the same bits as the kernel above;
+// what changes is the schedule:
+//   * a workgroup stays resident and walks a list of tiles (its XCD's contiguous share of the
+//     tile order, every P8-th tile), and the operand stream never stops at a tile boundary:
+//     the last K steps of tile k already issue the query loads and target DMA of tile k+1's
+//     first steps, so no workgroup waits out a cold prologue after the first;
+//   * the epilogue's pyramid stores are issued AFTER those loads and are never waited for at
+//     the tile boundary: tile k+1's first two barriers count them among the younger memory
+//     operations (vmcnt(30) = 8 loads + 22 stores), so the stores drain while the MFMAs of
+//     tile k+1 run, and the workgroups of one CU, which leave the store queue one after the
+//     other, fall out of step: one's store phase meets another's MFMA phase;
+//   * every wave issues exactly 22 store instructions per tile (buffer stores; a lane with
+//     nothing to write gets an out-of-range offset, which the hardware drops), so the
+//     hand-counted vmcnt immediates are exact.  No store is skipped by a branch.
+//   * the MFMA loop reads the next row's target fragments from LDS while the current row's
+//     six MFMAs issue, and alternates the two query blocks' accumulators.
+// ---------------------------------------------------------------------------------------
+constexpr int kExpInts = kPatchRows * 16 + kQPerWG;  // a tile's exponents: targets, then queries
+constexpr int kBuildLdsP = kRing * kSlotBytes + 2 * kExpInts * 4;  // exponents double-buffered
+constexpr int kStoresPerTile = 22;  // per wave: level 0 16, level 1 4, level 2 1, level 3 1
+constexpr uint32_t kOOB = 0x7ffffff0u;  // a buffer offset beyond every num_records (dropped store)
+
+__device__ __forceinline__ const void *sgpr_ptr(const void *p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (const void *)(((uint64_t)hi << 32) | lo);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait_barrier() {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// One LDS-DMA piece with a wave-uniform (SGPR) source base: 16 B per lane from base + voff.
+__device__ __forceinline__ void dma16s(const void *base, uint32_t voff, uint32_t lds) {
+    asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(base), "{m0}"(lds) : "memory");
+}
+
+// Group(s') = the vector-memory operations a wave issues at step s': [1 at s' = SS-2: the next
+// tile's exponent DMA] + 4 query loads + 4 DMA pieces of flat step s'+2 (this tile's or the
+// next one's; the last tile prefetches itself again, so every group is issued).  At step s's
+// barrier the operations younger than step s's DMA (the last issue of Group(s-2)) are
+// Group(s-1), and at steps 0 and 1 also the previous tile's kStoresPerTile stores.
+template <int SS>
+__host__ __device__ constexpr int group_ops(int s) {
+    return (s == SS - 2 ? 1 : 0) + 8;
+}
+
+template <int SS>
+__global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p) {
+    static_assert(SS == 4 || SS == 8, "query register slots and ring slots assume SS % 4 == 0, SS >= 4");
+    extern __shared__ __attribute__((aligned(16))) char smem_build[];
+    char *smem = smem_build;
+    int *lds_et = reinterpret_cast<int *>(smem + kRing * kSlotBytes);  // [2][kExpInts]
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_void_t *)smem;
+    const uint32_t lds_et_base = (uint32_t)(uintptr_t)(lds_void_t *)lds_et;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ci = lane & 15, grp = lane >> 4;
+
+    // This workgroup's tiles: XCD x (= blockIdx % 8 under round-robin dispatch; speed only)
+    // owns a contiguous range of the tile order, and its P8 workgroups deal it out.
+    const int xcd = blockIdx.x & 7, jj = blockIdx.x >> 3, P8 = gridDim.x >> 3;
+    const int T = p.ntiles, qT = T >> 3, rT = T & 7;
+    const int t0 = xcd < rT ? xcd * (qT + 1) : rT * (qT + 1) + (xcd - rT) * qT;
+    const int len = qT + (xcd < rT ? 1 : 0);
+    const int nmine = jj < len ? (len - 1 - jj) / P8 + 1 : 0;
+    if (nmine == 0) return;
+
+    const int H = p.H, W = p.W, N = p.N, NQ = p.NQ;
+    const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
+    const int N1 = H1 * W1, N2 = H2 * W2, N3 = H3 * W3;
+    const size_t trowB = (size_t)p.CB * kRecU * 16;  // bytes per patch row of the target image
+
+    struct TA {
+        int b, y0, x0, qb0;
+    };
+    auto tile_addr = [&](int k) __attribute__((always_inline)) {
+        const Tile tl = tile_of(p, t0 + jj + k * P8);
+        return TA{tl.b, tl.py * kPatchRows, tl.cb * 16, tl.qg * (kQPerWG / 16) + 2 * w};
+    };
+
+    u32x4 qv[4][2][2];  // [register slot][query block][hi, lo]
+    auto issue_q = [&](const TA &a, int s, int slot) __attribute__((always_inline)) {
+        const u32x4 *q = p.pq + ((size_t)(a.b * SS + s) * p.NQB + a.qb0) * kRecU + lane;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            qv[slot][i][0] = q[i * kRecU];
+            qv[slot][i][1] = q[i * kRecU + 64];
+        }
+    };
+    // the 4 DMA pieces of this wave: piece pc = w + 4 m = (patch row pc >> 1, half pc & 1)
+    auto issue_t = [&](const TA &a, int s, int slot) __attribute__((always_inline)) {
+        const uint32_t base = lds_base + slot * kSlotBytes;
+        const char *t = (const char *)(p.pt + (((size_t)(a.b * SS + s) * p.Hp + a.y0) * p.CB + (a.x0 >> 4)) * kRecU);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int pc = w + 4 * m;
+            dma16s(sgpr_ptr(t + (pc >> 1) * trowB + (pc & 1) * 1024), lane * 16, base + pc * 1024);
+        }
+    };
+    // A tile's exponents, one LDS-DMA dword per lane: waves 0, 1 the patch's 128 target
+    // exponents, waves 2, 3 the workgroup's 128 query exponents.
+    auto issue_e = [&](const TA &a, int buf) __attribute__((always_inline)) {
+        const int idx = (w & 1) * 64 + lane;
+        const int *src = w < 2 ? p.et + ((size_t)a.b * p.Hp + a.y0 + (idx >> 4)) * p.Wp + a.x0 + (idx & 15)
+                               : p.eq + (size_t)a.b * p.NQp + (a.qb0 - 2 * w) * 16 + idx;
+        dma4(src, lds_et_base + buf * (kExpInts * 4) + w * 256);
+    };
+    // c ? a : b without control flow
+    auto fsel = [](int c, float a, float b) __attribute__((always_inline)) {
+        const uint32_t m = c ? 0xffffffffu : 0u;
+        return __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, a) & m) | (__builtin_bit_cast(uint32_t, b) & ~m));
+    };
+    // A store's offset, opaque to the compiler: it must not split the store into one per value
+    // (that would make the number of issued stores data-dependent).
+    auto opq = [](uint32_t o) __attribute__((always_inline)) {
+        asm volatile("" : "+v"(o));
+        return o;
+    };
+
+    f32x4 acc[2][kPatchRows];
+    auto compute = [&](int tslot, int qslot) __attribute__((always_inline)) {
+        const u32x4 *A = reinterpret_cast<const u32x4 *>(smem + tslot * kSlotBytes) + lane;
+        half8 qh[2], ql[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            qh[i] = __builtin_bit_cast(half8, qv[qslot][i][0]);
+            ql[i] = __builtin_bit_cast(half8, qv[qslot][i][1]);
+        }
+        half8 fh[2], fl[2];
+        fh[0] = __builtin_bit_cast(half8, A[0]);
+        fl[0] = __builtin_bit_cast(half8, A[64]);
+#pragma unroll
+        for (int r = 0; r < kPatchRows; ++r) {
+            const int c = r & 1;
+            if (r + 1 < kPatchRows) {
+                fh[c ^ 1] = __builtin_bit_cast(half8, A[(2 * r + 2) * 64]);
+                fl[c ^ 1] = __builtin_bit_cast(half8, A[(2 * r + 3) * 64]);
+            }
+            // per accumulator the product order of the kernel above (lo_t hi_q, hi_t lo_q, hi_t hi_q)
+            acc[0][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl[c], qh[0], acc[0][r], 0, 0, 0);
+            acc[1][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl[c], qh[1], acc[1][r], 0, 0, 0);
+            acc[0][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], ql[0], acc[0][r], 0, 0, 0);
+            acc[1][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], ql[1], acc[1][r], 0, 0, 0);
+            acc[0][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], qh[0], acc[0][r], 0, 0, 0);
+            acc[1][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], qh[1], acc[1][r], 0, 0, 0);
+        }
+    };
+
+    // Epilogue: exactly kStoresPerTile buffer stores per wave.  Resources are per wave and
+    // level, based at the wave's first query row, sized to its valid queries.
+    auto epilogue = [&](const TA &a, int buf) __attribute__((always_inline)) {
+        const int q0 = a.qb0 * 16;
+        const int nq = min(max(NQ - q0, 0), 32);
+        const size_t qrow0 = (size_t)a.b * NQ + q0;
+        const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(p.lvl[0] + qrow0 * N, 0, nq * N * 4, 0x00020000);
+        const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(p.lvl[1] + qrow0 * N1, 0, nq * N1 * 4, 0x00020000);
+        const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc(p.lvl[2] + qrow0 * N2, 0, nq * N2 * 4, 0x00020000);
+        const __amdgpu_buffer_rsrc_t r3 = __builtin_amdgcn_make_buffer_rsrc(p.lvl[3] + qrow0 * N3, 0, nq * N3 * 4, 0x00020000);
+        const int *etb = lds_et + buf * kExpInts;
+        int eqv[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) eqv[i] = etb[kPatchRows * 16 + (2 * w + i) * 16 + ci] + p.eshift;
+        int et[kPatchRows][4];
+#pragma unroll
+        for (int r = 0; r < kPatchRows; ++r) {
+            const int4 e4 = reinterpret_cast<const int4 *>(etb)[r * 4 + grp];
+            et[r][0] = e4.x, et[r][1] = e4.y, et[r][2] = e4.z, et[r][3] = e4.w;
+        }
+        const int y0 = a.y0, x0 = a.x0, X0 = x0 + 4 * grp;
+        float l2s[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int qq = i * 16 + ci;  // query row within the wave's resources
+            float v[kPatchRows][4];
+#pragma unroll
+            for (int r = 0; r < kPatchRows; ++r)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    float x = ldexpf(acc[i][r][g], eqv[i] + et[r][g]);
+                    if (!p.exact) x = x * p.inv_s;
+                    v[r][g] = x;
+                }
+            {
+                const uint32_t o = (uint32_t)(qq * N + y0 * W + X0) * 4u;
+                const bool xok = X0 < W;
+#pragma unroll
+                for (int r = 0; r < kPatchRows; ++r) {
+                    const bool ok = xok && y0 + r < H;
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{v[r][0], v[r][1], v[r][2], v[r][3]}),
+                                                           r0, opq(ok ? o + (uint32_t)(r * W * 4) : kOOB), 0, 0);
+                }
+            }
+            float l1[4][2];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                l1[r][0] = pool4(v[2 * r][0], v[2 * r][1], v[2 * r + 1][0], v[2 * r + 1][1]);
+                l1[r][1] = pool4(v[2 * r][2], v[2 * r][3], v[2 * r + 1][2], v[2 * r + 1][3]);
+            }
+#pragma unroll
+            for (int r = 0; r < 2; ++r) l2s[i][r] = pool4(l1[2 * r][0], l1[2 * r][1], l1[2 * r + 1][0], l1[2 * r + 1][1]);
+            // Level 1 as 16-B stores: lanes grp 2m, 2m + 1 swap one row's column pair (see above).
+            const bool odd = grp & 1;
+            const int X1 = (x0 >> 1) + 4 * (grp >> 1);
+#pragma unroll
+            for (int rp = 0; rp < 2; ++rp) {
+                const int ra = 2 * rp, rb = ra + 1, r = odd ? rb : ra;
+                const float g0 = __shfl_xor(odd ? l1[ra][0] : l1[rb][0], 16);
+                const float g1 = __shfl_xor(odd ? l1[ra][1] : l1[rb][1], 16);
+                const f32x4 o4 = odd ? f32x4{g0, g1, l1[rb][0], l1[rb][1]} : f32x4{l1[ra][0], l1[ra][1], g0, g1};
+                const int Y1 = (y0 >> 1) + r;
+                const bool ok = Y1 < H1 && X1 < W1;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o4), r1,
+                                                       opq(ok ? (uint32_t)(qq * N1 + Y1 * W1 + X1) * 4u : kOOB), 0, 0);
+            }
+        }
+        {  // Level 2 of both blocks in one store (lane g gathers row g & 1 of block g >> 1).
+            const int bl = grp >> 1, rw = grp & 1;
+            // value k = 2 * block + row of this lane, by bit selects (no dynamic register index, no branch)
+            auto sel = [&](int k) { return fsel(k & 2, fsel(k & 1, l2s[1][1], l2s[1][0]), fsel(k & 1, l2s[0][1], l2s[0][0])); };
+            const float t0v = sel(grp);
+            const float t1 = __shfl_xor(sel(grp ^ 1), 16), t2 = __shfl_xor(sel(grp ^ 2), 32), t3 = __shfl_xor(sel(grp ^ 3), 48);
+            auto pick = [&](int k) { return fsel(k & 2, fsel(k & 1, t3, t2), fsel(k & 1, t1, t0v)); };
+            const f32x4 o4 = f32x4{pick(grp), pick(grp ^ 1), pick(grp ^ 2), pick(grp ^ 3)};
+            const int Y2 = (y0 >> 2) + rw, X2 = x0 >> 2;
+            const bool ok = Y2 < H2 && X2 < W2;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o4), r2,
+                                                   opq(ok ? (uint32_t)((bl * 16 + ci) * N2 + Y2 * W2 + X2) * 4u : kOOB), 0, 0);
+        }
+        {  // Level 3: even lanes pool block 0, odd lanes block 1.
+            const int bl = grp & 1;
+            const float y0v = __shfl_xor(bl ? l2s[0][0] : l2s[1][0], 16), y1v = __shfl_xor(bl ? l2s[0][1] : l2s[1][1], 16);
+            const float l3 = bl == 0 ? pool4(l2s[0][0], y0v, l2s[0][1], y1v) : pool4(y0v, l2s[1][0], y1v, l2s[1][1]);
+            const int Y3 = y0 >> 3, X3 = X0 >> 3;
+            const bool ok = Y3 < H3 && X3 < W3;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, l3), r3,
+                                                  opq(ok ? (uint32_t)((bl * 16 + ci) * N3 + Y3 * W3 + X3) * 4u : kOOB), 0, 0);
+        }
+    };
+
+    // ---- prologue of the first tile ----
+    TA cur = tile_addr(0);
+    issue_e(cur, 0);
+    issue_q(cur, 0, 0);
+    issue_t(cur, 0, 0);
+    issue_q(cur, 1, 1);
+    issue_t(cur, 1, 1);
+    {
+        // kStoresPerTile dropped stores (num_records 0): every tile, the first included, then
+        // starts with the same memory operations in flight, so the vmcnt immediates of steps 0
+        // and 1 are one constant each, and so are the compiler's own waits for the query
+        // registers (its loop-header merge would otherwise fall back to the prologue's count).
+        const __amdgpu_buffer_rsrc_t nul = __builtin_amdgcn_make_buffer_rsrc(p.lvl[0], 0, 0, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < kStoresPerTile; ++i) __builtin_amdgcn_raw_buffer_store_b32(0u, nul, opq(kOOB), 0, 0);
+    }
+    int rs0 = 0;  // ring slot of the current tile's step 0
+    for (int k = 0; k < nmine; ++k) {
+        // the tile whose first steps are prefetched at the end of this one (the last tile
+        // prefetches itself: every group is issued, so every count below is a constant)
+        const TA nxt = tile_addr(k + 1 < nmine ? k + 1 : k);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < kPatchRows; ++r) acc[i][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+        auto step = [&]<int s>() __attribute__((always_inline)) {
+            // wait for step s's target DMA (and everything older: its query loads, the exponents)
+            if constexpr (s < 2) vm_wait_barrier<group_ops<SS>(s == 0 ? SS - 1 : 0) + kStoresPerTile>();
+            else vm_wait_barrier<group_ops<SS>(s - 1)>();
+            const int qs = s & 3;
+            asm volatile("" : "+v"(qv[qs][0][0]), "+v"(qv[qs][0][1]), "+v"(qv[qs][1][0]), "+v"(qv[qs][1][1]));
+            if constexpr (s == SS - 2) issue_e(nxt, (k + 1) & 1);
+            const int sl = (rs0 + s + 2) % kRing;
+            if constexpr (s + 2 < SS) {
+                issue_q(cur, s + 2, (s + 2) & 3);
+                issue_t(cur, s + 2, sl);
+            } else {
+                issue_q(nxt, s + 2 - SS, (s + 2) & 3);
+                issue_t(nxt, s + 2 - SS, sl);
+            }
+            compute((rs0 + s) % kRing, qs);
+        };
+        [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
+            (step.template operator()<S>(), ...);
+        }(std::make_integer_sequence<int, SS>{});
+        epilogue(cur, k & 1);
+        cur = nxt;
+        rs0 = (rs0 + SS) % kRing;
+    }
+    // the last tile's self-prefetch is still landing in LDS: drain it before the workgroup's
+    // LDS can be handed to another workgroup
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------------------
 // Host side.
 // ---------------------------------------------------------------------------------------
 namespace {
@@ -610,11 +910,84 @@ hipError_t launch_split_mfma(int NQ, int B, int D, int H, int W, int levels, con
     return hipSuccess;
 }
 
+// Resident workgroups of the persistent kernel per device: CUs x blocks per CU (occupancy API),
+// rounded down to a multiple of 8 (one share per XCD).
+template <int SS>
+int persist_slots() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    std::atomic<int> &c = cache[dev & 63];
+    int v = c.load(std::memory_order_acquire);
+    if (v > 0) return v;
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)corr_build_persist_kernel<SS>, 256, kBuildLdsP) !=
+        hipSuccess)
+        return 0;
+    v = cus * std::max(per, 1) / 8 * 8;
+    c.store(v, std::memory_order_release);
+    return v;
+}
+
+// The persistent form applies: S in {4, 8}, >= 4 levels, levels 0-2 as 16-B runs.
+bool persist_applies(int S, int levels, int mode0, int cons) {
+    return (S == 4 || S == 8) && levels >= kFusedLevels && mode0 == 2 && cons;
+}
+
+constexpr int kPersistDefault = 0;  // the library's choice (measured in tools/kbench_build.hip)
+
+// persist: 1 = persistent kernel where it applies, 0 = the one-tile-per-workgroup
+// kernel.  slots > 0 overrides the resident-workgroup count (measurement).
+hipError_t launch_split_mfma_p(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
+                               hipStream_t s, int persist = 1, int slots = 0) {
+    const SplitGeom g = split_geom(D, NQ, H, W);
+    const int mode0 = store_mode(W, pyr.p[0]);
+    const int cons = levels > 2 && store_mode(W >> 1, pyr.p[1]) == 2 && store_mode(W >> 2, pyr.p[2]) == 2;
+    if (!persist || !persist_applies(g.S, levels, mode0, cons))
+        return launch_split_mfma(NQ, B, D, H, W, levels, pyr, ws, s);
+    const SplitWs w = split_ws(ws, B, g);
+    BuildArgs p{};
+    p.pq = w.pq, p.pt = w.pt, p.eq = w.eq, p.et = w.et;
+    p.B = B, p.H = H, p.W = W, p.N = H * W, p.NQ = NQ, p.S = g.S;
+    p.nlev = kFusedLevels;
+    for (int l = 0; l < kFusedLevels; ++l) p.lvl[l] = pyr.p[l];
+    p.NQp = g.NQp, p.NQB = g.NQB, p.NQG = g.NQG, p.Hp = g.Hp, p.CB = g.CB, p.Wp = g.Wp;
+    p.npatch = (g.Hp / kPatchRows) * g.CB;
+    const float sD = std::sqrt((float)D);
+    p.inv_s = 1.0f / sD;
+    p.exact = is_pow2(sD);
+    p.eshift = 0;
+    if (p.exact) {
+        int e;
+        std::frexp(p.inv_s, &e);
+        p.eshift = e - 1;
+    }
+    p.mode0 = 2, p.mode1 = 2, p.cons = 1;
+    const long tiles = (long)B * p.npatch * g.NQG;
+    if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
+    p.ntiles = (int)tiles;
+    static std::atomic<unsigned long long> lds_done[2];
+    const void *fn = g.S == 4 ? (const void *)corr_build_persist_kernel<4> : (const void *)corr_build_persist_kernel<8>;
+    hipError_t e = ensure_lds_limit(fn, kBuildLdsP, lds_done[g.S == 4 ? 0 : 1]);
+    if (e != hipSuccess) return e;
+    int P = slots > 0 ? slots / 8 * 8 : (g.S == 4 ? persist_slots<4>() : persist_slots<8>());
+    if (P <= 0) return hipErrorInvalidValue;
+    P = (int)std::min<long>(P, (tiles + 7) / 8 * 8);
+    const dim3 grid((unsigned)P), blk(256);
+    if (g.S == 4) hipLaunchKernelGGL(corr_build_persist_kernel<4>, grid, blk, kBuildLdsP, s, p);
+    else hipLaunchKernelGGL(corr_build_persist_kernel<8>, grid, blk, kBuildLdsP, s, p);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (levels > kFusedLevels) return launch_pool_levels(pyr, kFusedLevels, levels, (long)B * NQ, H, W, s);
+    return hipSuccess;
+}
+
 hipError_t launch_build_split(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, int levels,
                               const LevelPtrs &pyr, void *ws, hipStream_t s) {
     hipError_t e = launch_split_pack(f1, NQ, f2, B, D, H, W, ws, s);
     if (e != hipSuccess) return e;
-    return launch_split_mfma(NQ, B, D, H, W, levels, pyr, ws, s);
+    return launch_split_mfma_p(NQ, B, D, H, W, levels, pyr, ws, s, kPersistDefault);
 }
 
 }  // namespace corr

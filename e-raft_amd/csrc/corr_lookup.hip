@@ -1365,8 +1365,10 @@ template <int S>
 hipError_t launch_fused_s(const BwdLookups &lk, FusedOut o, hipStream_t s) {
     const size_t bytes = fused_lds_bytes<S>(o.H, o.W, o.L, &o);
     if (bytes > 160 * 1024) return hipErrorNotSupported;
+    // the dynamic-LDS limit is raised once per device to the largest image this path accepts
+    // (not to this call's size: a later, larger shape must not run against a smaller limit)
     static std::atomic<unsigned long long> done{0};
-    hipError_t e = ensure_lds_limit((const void *)lookup_bwd_fold_kernel<S>, (int)bytes, done);
+    hipError_t e = ensure_lds_limit((const void *)lookup_bwd_fold_kernel<S>, 160 * 1024, done);
     if (e != hipSuccess) return e;
     const int nqb = (o.NQ + FusedStage<S>::BQ - 1) / FusedStage<S>::BQ;
     o.nfold = nqb * o.B;

@@ -62,19 +62,28 @@ def _validate_fmaps(fmap1, fmap2, num_levels):
         raise RuntimeError(f"{H}x{W} feature maps are too small for {num_levels} pyramid levels")
 
 
-_WEIGHT_PACKS = {}  # (data_ptr, _version) of convc1.weight -> its packed split (lookup_conv)
+def _weight_pack(weight):
+    """convc1.weight's packed split for lookup_conv, cached ON the weight tensor itself with the
+    (data_ptr, _version) it was made from: a new tensor (another model, a reloaded checkpoint)
+    never sees another tensor's pack, and an in-place update (optimizer step, load_state_dict's
+    copy_) bumps _version and re-packs."""
+    key = (weight.data_ptr(), weight._version)
+    cached = getattr(weight, "_eraft_amd_pack", None)
+    if cached is None or cached[0] != key:
+        cached = (key, _lib.lookup_conv_weights(weight))
+        weight._eraft_amd_pack = cached
+    return cached[1]
 
 
 class _State:
     """Per-block state shared by the build and lookup autograd nodes."""
 
-    __slots__ = ("levels", "grad_levels", "H", "W", "radius", "stash", "token_sent")
+    __slots__ = ("levels", "grad_levels", "H", "W", "radius", "stash")
 
     def __init__(self, H, W, radius):
         self.levels = None
         self.grad_levels = None  # per-lookup path: the accumulated gradient pyramid
         self.stash = []          # fused path: (coords, grad_out) of every lookup backward
-        self.token_sent = False  # one lookup backward per pass hands the token a gradient
         self.H, self.W, self.radius = H, W, radius
 
 
@@ -98,7 +107,6 @@ class _BuildFn(torch.autograd.Function):
         st = ctx.state
         direct = grads[:-1]  # grads[-1] (the token's) carries no value
         stash, st.stash = st.stash, []
-        st.token_sent = False
         if st.grad_levels is None and not any(g is not None for g in direct):
             if not stash:
                 return None, None, None, None
@@ -154,14 +162,9 @@ class _LookupFn(torch.autograd.Function):
                 B, _, H, W = coords.shape
                 st.grad_levels = _alloc_pyramid(B, H, W, len(st.levels), coords, zero=True)
             _lib.lookup_bwd(coords, grad_out.contiguous(), ctx.radius, st.grad_levels)
-        # The token's gradient only makes autograd run the build's backward (after every lookup
-        # backward: it depends on all of them).  One lookup sends it, as an uninitialised scalar:
-        # a zero per lookup would cost a fill kernel each plus the engine's adds summing them
-        # (23 scalar launches, ~125 us of a 680 us training step at config 4).
-        if st.token_sent:
-            return None, None, None, None
-        st.token_sent = True
-        return None, coords.new_empty(()), None, None
+        # No gradient for the token: the engine still runs the build's backward, after every
+        # lookup backward (it depends on all of them), and nothing is filled or summed for it.
+        return None, None, None, None
 
 
 class CorrBlock:
@@ -218,12 +221,7 @@ class CorrBlock:
         if tuple(weight.shape) not in ((256, C, 1, 1), (256, C)) or tuple(bias.shape) != (256,):
             raise ValueError(f"lookup_conv needs weight [256, {C}, 1, 1] and bias [256] "
                              f"(got {tuple(weight.shape)}, {tuple(bias.shape)})")
-        key = (weight.data_ptr(), weight._version)
-        cached = _WEIGHT_PACKS.get(key)
-        if cached is None:  # split once per weight version (every GRU iteration reuses it)
-            if len(_WEIGHT_PACKS) > 8:
-                _WEIGHT_PACKS.clear()
-            _WEIGHT_PACKS[key] = cached = _lib.lookup_conv_weights(weight)
+        cached = _weight_pack(weight)  # split once per weight version (every GRU iteration reuses it)
         out = torch.empty((B, weight.shape[0], H, W), dtype=torch.float32, device=coords.device)
         _lib.lookup_conv(self._state.levels, coords.detach().contiguous(), self.radius, cached,
                          bias.detach().contiguous().float(), out, relu)

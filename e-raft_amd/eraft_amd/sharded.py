@@ -100,7 +100,7 @@ def _alloc_pyramid_rows(B, NQ, H, W, num_levels, like):
 
 class _ShardState:
     __slots__ = ("levels", "grad_levels", "B", "NQ", "H", "W", "backend", "group", "h0", "h1", "full1", "stash",
-                 "radius", "token_sent")
+                 "radius")
 
 
 class _ShardBuildFn(torch.autograd.Function):
@@ -121,7 +121,6 @@ class _ShardBuildFn(torch.autograd.Function):
         st = ctx.st
         gl, st.grad_levels = st.grad_levels, None
         stash, st.stash = st.stash, []
-        st.token_sent = False
         if stash and st.NQ > 0:  # fused: every lookup's backward + fold + GEMMs in corr_backward
             df1, df2 = st.backend.backward([c for c, _ in stash], [g for _, g in stash], st.radius, f1_rows, f2,
                                            ctx.num_levels)
@@ -161,12 +160,56 @@ class _ShardLookupFn(torch.autograd.Function):
             if st.grad_levels is None:
                 st.grad_levels = st.backend.zero_pyramid(st.B, st.NQ, st.H, st.W, len(st.levels), coords_rows)
             st.backend.lookup_bwd(coords_rows, grad_rows.contiguous(), ctx.radius, st.grad_levels, st.H, st.W)
-        # one lookup per pass hands the token a gradient (its value is never read): see
-        # corr._LookupFn.backward
-        if getattr(st, "token_sent", False):
-            return None, None, None, None
-        st.token_sent = True
-        return None, coords_rows.new_empty(()), None, None
+        # no gradient for the token: the engine still runs the build's backward (corr._LookupFn)
+        return None, None, None, None
+
+
+class PendingFmap2:
+    """A pair's fmap2 whose broadcast from rank `src` is in flight (RowShardedCorrBlock.prefetch).
+
+    Handing it to RowShardedCorrBlock replaces the constructor's blocking broadcast by a wait on
+    this one: with RCCL the compute stream waits for the collective's stream (the host does not
+    block), so the broadcast of pair k+1 runs while pair k is built and looked up."""
+
+    __slots__ = ("tensor", "_work")
+
+    def __init__(self, tensor, work):
+        self.tensor, self._work = tensor, work
+
+    @property
+    def done(self):
+        return self._work is None
+
+    def wait(self):
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
+        return self.tensor
+
+
+class Fmap2DoubleBuffer:
+    """Two receive buffers for a stream of frame pairs: ``prefetch(next_fmap2)`` starts the
+    broadcast of the next pair's fmap2 into the buffer the pair before last used, so pair k's
+    build reads one buffer while pair k+1's broadcast fills the other.  On rank `src` the
+    argument is that rank's fmap2 (it is copied into the buffer on the compute stream, so the
+    caller may reuse its own tensor); the other ranks pass None.  Stream order makes the
+    reuse safe: the collective waits for the compute stream's earlier work (pair k-1's build,
+    the last reader of the buffer it overwrites) before it starts."""
+
+    def __init__(self, shape, device, group=None, src=0, dtype=torch.float32):
+        self.group, self.src = group, src
+        self.rank = dist.get_rank(group)
+        self.bufs = [torch.empty(shape, dtype=dtype, device=device) for _ in range(2)]
+        self.k = 0
+
+    def prefetch(self, fmap2=None):
+        buf = self.bufs[self.k % 2]
+        self.k += 1
+        if self.rank == self.src:
+            if fmap2 is None:
+                raise ValueError(f"rank {self.src} is the broadcast source: pass its fmap2")
+            buf.copy_(fmap2.detach())
+        return RowShardedCorrBlock.prefetch(buf, src=self.src, group=self.group)
 
 
 class RowShardedCorrBlock:
@@ -174,10 +217,22 @@ class RowShardedCorrBlock:
 
     fmap1: the full query map [B, D, H, W] (each rank slices its rows) or, with
            ``fmap1_is_slab=True``, already this rank's rows [B, D, h1-h0, W].
-    fmap2: [B, D, H, W] on every rank; the contents on rank `src` are broadcast to all.
+    fmap2: [B, D, H, W] on every rank; the contents on rank `src` are broadcast to all (a
+           blocking broadcast here), or a PendingFmap2 from ``prefetch`` whose broadcast was
+           started earlier and overlapped the previous pair's work (see Fmap2DoubleBuffer).
     __call__(coords): coords of this rank's rows [B, 2, h1-h0, W] (or the full [B, 2, H, W],
            sliced) -> this rank's lookup rows [B, L*K, h1-h0, W].
     """
+
+    @staticmethod
+    def prefetch(fmap2, src=0, group=None):
+        """Start broadcasting rank `src`'s fmap2 into `fmap2` on every rank without waiting;
+        returns the PendingFmap2 to construct the block from."""
+        if dist.get_world_size(group) == 1:
+            return PendingFmap2(fmap2, None)
+        with torch.no_grad():
+            work = dist.broadcast(fmap2, src=src, group=group, async_op=True)
+        return PendingFmap2(fmap2, work)
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4, group=None, src=0,
                  fmap1_is_slab=False, backend=HipRows, broadcast=True):
@@ -185,6 +240,9 @@ class RowShardedCorrBlock:
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        if isinstance(fmap2, PendingFmap2):  # broadcast already issued (prefetch): wait for it
+            fmap2 = fmap2.wait()
+            broadcast = False
         B, D, H, W = fmap2.shape
         self.B, self.H, self.W = B, H, W
         self.h0, self.h1 = row_partition(H, self.world, self.rank)

@@ -37,7 +37,11 @@ extern "C" {
 #define CORR_MAX_LEVELS 8
 #define CORR_MAX_RADIUS 7
 
-/* ABI version (major * 100 + minor). */
+/* ABI version (major * 100 + minor).
+ *   101: first ABI.
+ *   102: corr_lookup_conv's weight argument is the opaque buffer written by
+ *        corr_lookup_conv_weights (it was an fp32 [L*K][256] transpose under 101); callers
+ *        built against 101 must check this version before calling it. */
 int corr_version(void);
 
 /* Thread-local description of the last error on this thread ("" if none). */

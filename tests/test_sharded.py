@@ -131,6 +131,56 @@ def test_row_sharded_matches_unsharded(world, shape):
     assert covered == list(range(H))
 
 
+def _pipe_worker(rank, world, port, shape, npairs, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from eraft_amd.sharded import Fmap2DoubleBuffer, RowShardedCorrBlock, row_partition
+
+        B, D, H, W, L, r = shape
+        OracleRows.h0 = row_partition(H, world, rank)[0]
+        dbuf = Fmap2DoubleBuffer((B, D, H, W), "cpu")
+        # pair k's fmap2 exists only on rank 0 (seed 100 + k); the next pair's broadcast is
+        # issued before the current pair is built
+        src = lambda k: torch.from_numpy(prng.gauss(100 + k, (B, D, H, W))) if rank == 0 else None  # noqa: E731
+        pending = dbuf.prefetch(src(0))
+        outs = []
+        for k in range(npairs):
+            nxt = dbuf.prefetch(src(k + 1)) if k + 1 < npairs else None
+            f1 = torch.from_numpy(prng.gauss(200 + k, (B, D, H, W)))
+            blk = RowShardedCorrBlock(f1, pending, L, r, backend=OracleRows)
+            coords = torch.from_numpy(prng.lookup_coords(300 + k, B, H, W, 3.0))
+            outs.append(blk.gather(blk(coords)).numpy())
+            pending = nxt
+        q.put((rank, outs))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_row_sharded_prefetch_pipeline():
+    """The product API for a stream of pairs: Fmap2DoubleBuffer.prefetch issues pair k+1's
+    fmap2 broadcast before pair k is built (double-buffered), RowShardedCorrBlock waits on it.
+    Every pair's gathered output is bit-identical to the unsharded block."""
+    world, npairs = 2, 3
+    shape = B, D, H, W, L, r = (1, 8, 12, 16, 3, 3)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(g, world, port, shape, npairs, q)) for g in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k in range(npairs):
+        f1, f2 = prng.gauss(200 + k, (B, D, H, W)), prng.gauss(100 + k, (B, D, H, W))
+        ref = oracle.lookup(oracle.build_pyramid(f1, f2, L), prng.lookup_coords(300 + k, B, H, W, 3.0), r)
+        for _, outs in res:
+            assert bit_equal(outs[k], ref)
+
+
 def _train_worker(rank, world, port, shape, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)

@@ -17,9 +17,6 @@
 
 #include "../e-raft_amd/csrc/corr_build.hip"
 #include "../e-raft_amd/csrc/corr_build_split.hip"
-#include "legacy/build_split_r01.hip"
-#include "legacy/build_split_ps.hip"
-#include "legacy/pack_256.hip"
 
 using namespace corr;
 
@@ -94,15 +91,13 @@ int main(int argc, char **argv) {
         }
         const size_t fe = (size_t)sh.B * sh.D * N;
         float *f1, *f2, *ref, *out;
-        void *ws, *ws1;
+        void *ws;
         const size_t wsb = build_split_workspace(sh.B, sh.D, (int)N, sh.H, sh.W);
-        const size_t wsb1 = r01::build_split_workspace(sh.B, sh.D, (int)N, sh.H, sh.W);
         CK(hipMalloc(&f1, fe * 4));
         CK(hipMalloc(&f2, fe * 4));
         CK(hipMalloc(&ref, tot * 4));
         CK(hipMalloc(&out, tot * 4));
         CK(hipMalloc(&ws, wsb));
-        CK(hipMalloc(&ws1, wsb1));
         auto lp_of = [&](float *base) {
             LevelPtrs lp{};
             for (int l = 0; l < 4; ++l) lp.p[l] = base + off[l];
@@ -113,50 +108,26 @@ int main(int argc, char **argv) {
         vs.push_back({"f32 build (corr_build.hip)", [&](float *o) {
                           return launch_build_cfg<BuildDefault>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
                       }, true});
-        vs.push_back({"r01 x3 pack+mfma", [&](float *o) {
-                          return r01::launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws1, 0);
-                      }, true});
         vs.push_back({"x3 pack+mfma", [&](float *o) {
                           return launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
                       }, true});
         vs.push_back({"x3 pack only", [&](float *) {
                           return launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0);
                       }, false});
-        vs.push_back({"x3 pack only (wide 64 px)", [&](float *) {
-                          return launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, 64);
+        vs.push_back({"x3 mfma persist", [&](float *o) {
+                          return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1);
                       }, false});
-        vs.push_back({"x3 pack only (256-thread)", [&](float *) {
-                          return launch_split_pack_256(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0);
+        vs.push_back({"x3 mfma persist 2/CU", [&](float *o) {
+                          return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 512);
                       }, false});
-        vs.push_back({"x3 mfma only", [&](float *o) {
+        vs.push_back({"x3 mfma persist 1/CU", [&](float *o) {
+                          return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 256);
+                      }, false});
+        vs.push_back({"x3 mfma 1-tile", [&](float *o) {
                           return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
                       }, false});
-        vs.push_back({"x3 mfma NOSTORE", [&](float *o) {
+        vs.push_back({"x3 mfma 1-tile NOSTORE", [&](float *o) {
                           return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), ws, 0);
-                      }, false});
-        vs.push_back({"x3 mfma persistent (legacy)", [&](float *o) {
-                          return launch_split_mfma_ps(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
-                      }, false});
-        vs.push_back({"x3 mfma elem L1/2", [&](float *o) {
-                          return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, false);
-                      }, false});
-        vs.push_back({"x3 mfma L0tiled", [&](float *o) {
-                          return launch_split_mfma<4>(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
-                      }, false});
-        vs.push_back({"x3 mfma L0only", [&](float *o) {
-                          return launch_split_mfma<8>(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
-                      }, false});
-        vs.push_back({"x3 mfma L0tiled only", [&](float *o) {
-                          return launch_split_mfma<12>(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
-                      }, false});
-        vs.push_back({"x3 mfma NOSTORE noDMA", [&](float *o) {
-                          return launch_split_mfma<1>(NQ, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), ws, 0);
-                      }, false});
-        vs.push_back({"x3 mfma NOSTORE noQ", [&](float *o) {
-                          return launch_split_mfma<2>(NQ, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), ws, 0);
-                      }, false});
-        vs.push_back({"x3 mfma NOSTORE noDMA noQ", [&](float *o) {
-                          return launch_split_mfma<3>(NQ, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), ws, 0);
                       }, false});
         for (float sc : {1.0f, 1e-3f, 300.0f}) {
             hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f1, fe, 1u, sc);
@@ -179,22 +150,6 @@ int main(int argc, char **argv) {
                 printf("%-10s scale %-6g %-28s max|x-f32|/max|f32| = %.3e\n", sh.name, sc, vs[k].name.c_str(), dm / rm);
             }
         }
-        {  // the wide pack against the 256-thread pack: the whole workspace bitwise
-            std::vector<unsigned char> ha(wsb), hb(wsb);
-            CK(hipMemset(ws, 0x5a, wsb));
-            CK(launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0));
-            CK(hipMemcpy(ha.data(), ws, wsb, hipMemcpyDeviceToHost));
-            CK(hipMemset(ws, 0x5a, wsb));
-            CK(launch_split_pack_256(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0));
-            CK(hipMemcpy(hb.data(), ws, wsb, hipMemcpyDeviceToHost));
-            printf("%-10s wide pack vs 256-thread pack, workspace: %s\n", sh.name,
-                   std::memcmp(ha.data(), hb.data(), wsb) ? "DIFFER" : "bit-identical");
-            CK(hipMemset(ws, 0x5a, wsb));
-            CK(launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, 64));
-            CK(hipMemcpy(ha.data(), ws, wsb, hipMemcpyDeviceToHost));
-            printf("%-10s wide pack (64 px) vs 256-thread pack, workspace: %s\n", sh.name,
-                   std::memcmp(ha.data(), hb.data(), wsb) ? "DIFFER" : "bit-identical");
-        }
         {  // kernel variants against the one-tile-per-workgroup kernel (level-1/2 element stores): every level bitwise
             auto same = [&](const char *what, std::function<hipError_t(float *)> fa) {
                 CK(launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0));
@@ -211,8 +166,10 @@ int main(int argc, char **argv) {
                 printf("%-10s %s vs 1-tile element stores, all levels: %s (%zu mismatches)\n", sh.name, what,
                        bad ? "DIFFER" : "bit-identical", bad);
             };
-            same("persistent (legacy)", [&](float *o) { return launch_split_mfma_ps(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
             same("16-B level 1/2 stores", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
+            same("persistent", [&](float *o) { return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1); });
+            same("persistent 2/CU", [&](float *o) { return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 512); });
+            same("persistent 1/CU", [&](float *o) { return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 256); });
         }
         {  // pooling of the new kernel: every level bit-identical to avg_pool2d of its own level 0
             CK(launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), ws, 0));
@@ -264,7 +221,6 @@ int main(int argc, char **argv) {
         CK(hipFree(ref));
         CK(hipFree(out));
         CK(hipFree(ws));
-        CK(hipFree(ws1));
     }
     return 0;
 }
