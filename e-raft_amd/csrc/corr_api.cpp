@@ -346,6 +346,30 @@ int corr_convex_upsample(const float *flow, const float *mask, int N, int h, int
     return hip_status(launch_convex_upsample(flow, mask, N, h, w, out, (hipStream_t)stream), fn);
 }
 
+size_t corr_convex_upsample_bwd_workspace(int N, int h, int w) {
+    if (N < 1 || h < 1 || w < 1) return 0;
+    return convex_upsample_bwd_workspace(N, h, w);
+}
+
+int corr_convex_upsample_bwd(const float *flow, const float *mask, const float *grad_out, int N, int h, int w,
+                             float *dflow, float *dmask, void *workspace, size_t workspace_bytes, void *stream) {
+    static const char *fn = "corr_convex_upsample_bwd";
+    g_err[0] = 0;
+    if (N < 1 || h < 1 || w < 1)
+        return fail(CORR_EINVAL, "%s: N, h, w must be >= 1 (got %d, %d, %d)", fn, N, h, w);
+    int rc;
+    if ((rc = check_ptr(fn, flow, "flow")) || (rc = check_ptr(fn, mask, "mask")) ||
+        (rc = check_ptr(fn, grad_out, "grad_out")) || (rc = check_ptr(fn, dflow, "dflow")) ||
+        (rc = check_ptr(fn, dmask, "dmask")) || (rc = check_ptr(fn, workspace, "workspace")))
+        return rc;
+    const size_t need = convex_upsample_bwd_workspace(N, h, w);
+    if (workspace_bytes < need)
+        return fail(CORR_EINVAL, "%s: workspace of %zu bytes, %zu needed", fn, workspace_bytes, need);
+    return hip_status(launch_convex_upsample_bwd(flow, mask, grad_out, N, h, w, dflow, dmask, workspace,
+                                                 (hipStream_t)stream),
+                      fn);
+}
+
 size_t corr_voxel_grid_workspace(int n_events, int C, int H, int W) {
     if (n_events < 0 || C < 1 || H < 1 || W < 1) return 0;
     return voxel_workspace(n_events, C, H, W);

@@ -94,8 +94,7 @@ struct PackArgs {
 // PX = 64 a lane holds its pixel's 4 k octets of a step, with PX = 32 two of them.  Every load
 // instruction reads whole feature rows of the PX pixels (PX * 4-B runs where the blocks are
 // contiguous), the pixel maxima meet in LDS, and each lane writes its own 16-B pieces of the
-// records.  Same exponents and halves as the round-1 256-thread pack (tools/legacy/pack_256.hip),
-// bit for bit.
+// records.
 template <int SPW, int PX>
 __global__ __launch_bounds__(512) void split_pack_wide_kernel(PackArgs a) {
     constexpr int OPL = 4 * PX / 64;  // k octets per lane and step
@@ -252,10 +251,7 @@ __device__ __forceinline__ void store2(float *row, int X, int Wl, float a, float
 
 // SS > 0: S = SS K steps, fully unrolled (straight-line code: the compiler's own waits on the
 // query registers are then exact and never drain the prefetch).  SS = 0: any S, runtime loop.
-// PROBE (measurement builds only, tools/kbench_build.hip; the library uses 0): bit 0 = no target
-// DMA after the prologue, bit 1 = no query loads after the prologue, bit 2 = level 0 stored to
-// patch-tiled addresses, bit 3 = no level 1-3 stores (wrong results, timing only).
-template <int SS, int PROBE = 0>
+template <int SS>
 __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
     extern __shared__ __attribute__((aligned(16))) char smem_build[];
     char *smem = smem_build;
@@ -361,8 +357,8 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
             else wait_vmcnt_barrier<0>();
             const int qs = s & 3;
             asm volatile("" : "+v"(qv[qs][0][0]), "+v"(qv[qs][0][1]), "+v"(qv[qs][1][0]), "+v"(qv[qs][1][1]));
-            if (!(PROBE & 2) && s + 3 < SS) issue_q(s + 3, (s + 3) & 3);
-            if (!(PROBE & 1) && s + 2 < SS) issue_t(s + 2, (s + 2) % kRing);
+            if (s + 3 < SS) issue_q(s + 3, (s + 3) & 3);
+            if (s + 2 < SS) issue_t(s + 2, (s + 2) % kRing);
             compute(s % kRing, qs);
         }
     } else {
@@ -405,17 +401,9 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
             }
         if (qok && nlev > 0) {
             float *row0 = p.lvl[0] + qrow * N;
-            if constexpr (PROBE & 4) {  // tiled-layout store addresses (timing probe)
 #pragma unroll
-                for (int r = 0; r < kPatchRows; ++r)
-                    if (y0 + r < H)
-                        *reinterpret_cast<float4 *>(row0 + ((tl.py * p.CB + tl.cb) * 128 + r * 16 + 4 * grp) % N) =
-                            make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
-            } else {
-#pragma unroll
-                for (int r = 0; r < kPatchRows; ++r)
-                    if (y0 + r < H) store4(row0 + (size_t)(y0 + r) * W, X0, W, v[r], p.mode0);
-            }
+            for (int r = 0; r < kPatchRows; ++r)
+                if (y0 + r < H) store4(row0 + (size_t)(y0 + r) * W, X0, W, v[r], p.mode0);
         }
         float l1[4][2];
 #pragma unroll
@@ -439,17 +427,17 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
                 const float g0 = __shfl_xor(odd ? l1[ra][0] : l1[rb][0], 16);
                 const float g1 = __shfl_xor(odd ? l1[ra][1] : l1[rb][1], 16);
                 const float4 o = odd ? make_float4(g0, g1, l1[rb][0], l1[rb][1]) : make_float4(l1[ra][0], l1[ra][1], g0, g1);
-                if (!(PROBE & 8) && qok && nlev > 1 && (y0 >> 1) + r < H1 && X1 < W1)
+                if (qok && nlev > 1 && (y0 >> 1) + r < H1 && X1 < W1)
                     *reinterpret_cast<float4 *>(p.lvl[1] + qrow * N1 + (size_t)((y0 >> 1) + r) * W1 + X1) = o;
             }
         } else {
-            if (!(PROBE & 8) && qok && nlev > 1) {
+            if (qok && nlev > 1) {
                 float *row1 = p.lvl[1] + qrow * N1;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     if ((y0 >> 1) + r < H1) store2(row1 + (size_t)((y0 >> 1) + r) * W1, X0 >> 1, W1, l1[r][0], l1[r][1], p.mode1);
             }
-            if (!(PROBE & 8) && qok && nlev > 2) {
+            if (qok && nlev > 2) {
                 float *row2 = p.lvl[2] + qrow * N2;
 #pragma unroll
                 for (int r = 0; r < 2; ++r)
@@ -471,7 +459,7 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
         auto pick = [&](int k) { return k == 0 ? t0 : k == 1 ? t1 : k == 2 ? t2 : t3; };
         const float4 o = make_float4(pick(grp), pick(grp ^ 1), pick(grp ^ 2), pick(grp ^ 3));
         const int q = (qb0 + bl) * 16 + ci;
-        if (!(PROBE & 8) && q < NQ && nlev > 2 && (y0 >> 2) + rw < H2 && (x0 >> 2) < W2)
+        if (q < NQ && nlev > 2 && (y0 >> 2) + rw < H2 && (x0 >> 2) < W2)
             *reinterpret_cast<float4 *>(p.lvl[2] + ((size_t)b * NQ + q) * N2 + (size_t)((y0 >> 2) + rw) * W2 + (x0 >> 2)) = o;
     }
     {
@@ -482,7 +470,7 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
         const float l3 = bl == 0 ? pool4(l2s[0][0], y0v, l2s[0][1], y1v) : pool4(y0v, l2s[1][0], y1v, l2s[1][1]);
         const int q = (qb0 + bl) * 16 + ci;
         const int Y3 = y0 >> 3, X3 = X0 >> 3;
-        if (!(PROBE & 8) && q < NQ && nlev > 3 && Y3 < H3 && X3 < W3) p.lvl[3][((size_t)b * NQ + q) * N3 + Y3 * W3 + X3] = l3;
+        if (q < NQ && nlev > 3 && Y3 < H3 && X3 < W3) p.lvl[3][((size_t)b * NQ + q) * N3 + Y3 * W3 + X3] = l3;
     }
 }
 
@@ -537,7 +525,10 @@ __host__ __device__ constexpr int group_ops(int s) {
     return (s == SS - 2 ? 1 : 0) + 8;
 }
 
-template <int SS>
+// HALF: a tile whose patch has at most 4 map rows left (the last patch row when H % 8 is 1-4:
+// DSEC, train, MVSEC) runs the MFMAs of rows 0-3 only (its rows 4-7 are padding whose stores
+// are dropped anyway); same memory operations, same bits.
+template <int SS, bool HALF = true>
 __global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p) {
     static_assert(SS == 4 || SS == 8, "query register slots and ring slots assume SS % 4 == 0, SS >= 4");
     extern __shared__ __attribute__((aligned(16))) char smem_build[];
@@ -612,7 +603,7 @@ __global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p)
     };
 
     f32x4 acc[2][kPatchRows];
-    auto compute = [&](int tslot, int qslot) __attribute__((always_inline)) {
+    auto compute = [&]<int NR>(int tslot, int qslot) __attribute__((always_inline)) {
         const u32x4 *A = reinterpret_cast<const u32x4 *>(smem + tslot * kSlotBytes) + lane;
         half8 qh[2], ql[2];
 #pragma unroll
@@ -624,9 +615,9 @@ __global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p)
         fh[0] = __builtin_bit_cast(half8, A[0]);
         fl[0] = __builtin_bit_cast(half8, A[64]);
 #pragma unroll
-        for (int r = 0; r < kPatchRows; ++r) {
+        for (int r = 0; r < NR; ++r) {
             const int c = r & 1;
-            if (r + 1 < kPatchRows) {
+            if (r + 1 < NR) {
                 fh[c ^ 1] = __builtin_bit_cast(half8, A[(2 * r + 2) * 64]);
                 fl[c ^ 1] = __builtin_bit_cast(half8, A[(2 * r + 3) * 64]);
             }
@@ -756,6 +747,7 @@ __global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p)
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int r = 0; r < kPatchRows; ++r) acc[i][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const bool half = HALF && cur.y0 + kPatchRows / 2 >= p.H;  // tile-uniform
         auto step = [&]<int s>() __attribute__((always_inline)) {
             // wait for step s's target DMA (and everything older: its query loads, the exponents)
             if constexpr (s < 2) vm_wait_barrier<group_ops<SS>(s == 0 ? SS - 1 : 0) + kStoresPerTile>();
@@ -771,7 +763,10 @@ __global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p)
                 issue_q(nxt, s + 2 - SS, (s + 2) & 3);
                 issue_t(nxt, s + 2 - SS, sl);
             }
-            compute((rs0 + s) % kRing, qs);
+            // only the MFMAs branch (the memory operations above are common to both arms, so no
+            // register of an in-flight load meets a control-flow join)
+            if (half) compute.template operator()<kPatchRows / 2>((rs0 + s) % kRing, qs);
+            else compute.template operator()<kPatchRows>((rs0 + s) % kRing, qs);
         };
         [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
             (step.template operator()<S>(), ...);
@@ -859,7 +854,6 @@ hipError_t launch_split_pack(const float *f1, int NQ, const float *f2, int B, in
 // The MFMA part (operands already packed in ws).  levels == 0: the MFMAs and epilogue
 // arithmetic without stores (measurement).  cons = false: levels 1-2 as element stores (the
 // previous epilogue, kept for the A/B; same bits).
-template <int PROBE = 0>
 hipError_t launch_split_mfma(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
                              hipStream_t s, bool cons = true) {
     const SplitGeom g = split_geom(D, NQ, H, W);
@@ -889,17 +883,17 @@ hipError_t launch_split_mfma(int NQ, int B, int D, int H, int W, int levels, con
     static std::atomic<unsigned long long> lds_done[9];
     const int ss = g.S <= 8 ? g.S : 0;
     const void *fns[9] = {
-        (const void *)corr_build_split_kernel<0, PROBE>, (const void *)corr_build_split_kernel<1, PROBE>,
-        (const void *)corr_build_split_kernel<2, PROBE>, (const void *)corr_build_split_kernel<3, PROBE>,
-        (const void *)corr_build_split_kernel<4, PROBE>, (const void *)corr_build_split_kernel<5, PROBE>,
-        (const void *)corr_build_split_kernel<6, PROBE>, (const void *)corr_build_split_kernel<7, PROBE>,
-        (const void *)corr_build_split_kernel<8, PROBE>};
+        (const void *)corr_build_split_kernel<0>, (const void *)corr_build_split_kernel<1>,
+        (const void *)corr_build_split_kernel<2>, (const void *)corr_build_split_kernel<3>,
+        (const void *)corr_build_split_kernel<4>, (const void *)corr_build_split_kernel<5>,
+        (const void *)corr_build_split_kernel<6>, (const void *)corr_build_split_kernel<7>,
+        (const void *)corr_build_split_kernel<8>};
     e = ensure_lds_limit(fns[ss], kBuildLds, lds_done[ss]);
     if (e != hipSuccess) return e;
     const dim3 grid((unsigned)tiles), blk(256);
     switch (ss) {
 #define CORR_BUILD_CASE(c) \
-    case c: hipLaunchKernelGGL((corr_build_split_kernel<c, PROBE>), grid, blk, kBuildLds, s, p); break;
+    case c: hipLaunchKernelGGL((corr_build_split_kernel<c>), grid, blk, kBuildLds, s, p); break;
         CORR_BUILD_CASE(0) CORR_BUILD_CASE(1) CORR_BUILD_CASE(2) CORR_BUILD_CASE(3) CORR_BUILD_CASE(4)
         CORR_BUILD_CASE(5) CORR_BUILD_CASE(6) CORR_BUILD_CASE(7) CORR_BUILD_CASE(8)
 #undef CORR_BUILD_CASE
@@ -922,7 +916,7 @@ int persist_slots() {
     if (v > 0) return v;
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)corr_build_persist_kernel<SS>, 256, kBuildLdsP) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)corr_build_persist_kernel<SS, true>, 256, kBuildLdsP) !=
         hipSuccess)
         return 0;
     v = cus * std::max(per, 1) / 8 * 8;
@@ -940,7 +934,7 @@ constexpr int kPersistDefault = 0;  // the library's choice (measured in tools/k
 // persist: 1 = persistent kernel where it applies, 0 = the one-tile-per-workgroup
 // kernel.  slots > 0 overrides the resident-workgroup count (measurement).
 hipError_t launch_split_mfma_p(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
-                               hipStream_t s, int persist = 1, int slots = 0) {
+                               hipStream_t s, int persist = 1, int slots = 0, bool half = true) {
     const SplitGeom g = split_geom(D, NQ, H, W);
     const int mode0 = store_mode(W, pyr.p[0]);
     const int cons = levels > 2 && store_mode(W >> 1, pyr.p[1]) == 2 && store_mode(W >> 2, pyr.p[2]) == 2;
@@ -967,16 +961,22 @@ hipError_t launch_split_mfma_p(int NQ, int B, int D, int H, int W, int levels, c
     const long tiles = (long)B * p.npatch * g.NQG;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
     p.ntiles = (int)tiles;
-    static std::atomic<unsigned long long> lds_done[2];
-    const void *fn = g.S == 4 ? (const void *)corr_build_persist_kernel<4> : (const void *)corr_build_persist_kernel<8>;
-    hipError_t e = ensure_lds_limit(fn, kBuildLdsP, lds_done[g.S == 4 ? 0 : 1]);
+    static std::atomic<unsigned long long> lds_done[4];
+    const int ki = (g.S == 4 ? 0 : 2) + (half ? 0 : 1);
+    const void *fns[4] = {(const void *)corr_build_persist_kernel<4, true>, (const void *)corr_build_persist_kernel<4, false>,
+                          (const void *)corr_build_persist_kernel<8, true>, (const void *)corr_build_persist_kernel<8, false>};
+    hipError_t e = ensure_lds_limit(fns[ki], kBuildLdsP, lds_done[ki]);
     if (e != hipSuccess) return e;
     int P = slots > 0 ? slots / 8 * 8 : (g.S == 4 ? persist_slots<4>() : persist_slots<8>());
     if (P <= 0) return hipErrorInvalidValue;
     P = (int)std::min<long>(P, (tiles + 7) / 8 * 8);
     const dim3 grid((unsigned)P), blk(256);
-    if (g.S == 4) hipLaunchKernelGGL(corr_build_persist_kernel<4>, grid, blk, kBuildLdsP, s, p);
-    else hipLaunchKernelGGL(corr_build_persist_kernel<8>, grid, blk, kBuildLdsP, s, p);
+    switch (ki) {
+        case 0: hipLaunchKernelGGL((corr_build_persist_kernel<4, true>), grid, blk, kBuildLdsP, s, p); break;
+        case 1: hipLaunchKernelGGL((corr_build_persist_kernel<4, false>), grid, blk, kBuildLdsP, s, p); break;
+        case 2: hipLaunchKernelGGL((corr_build_persist_kernel<8, true>), grid, blk, kBuildLdsP, s, p); break;
+        default: hipLaunchKernelGGL((corr_build_persist_kernel<8, false>), grid, blk, kBuildLdsP, s, p); break;
+    }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (levels > kFusedLevels) return launch_pool_levels(pyr, kFusedLevels, levels, (long)B * NQ, H, W, s);

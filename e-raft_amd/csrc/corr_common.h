@@ -67,6 +67,9 @@ hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, 
                                   int W, float *df1, float *df2, void *ws, hipStream_t s);
 hipError_t launch_convex_upsample(const float *flow, const float *mask, int N, int h, int w, float *out,
                                   hipStream_t s);
+size_t convex_upsample_bwd_workspace(int N, int h, int w);
+hipError_t launch_convex_upsample_bwd(const float *flow, const float *mask, const float *dout, int N, int h, int w,
+                                      float *dflow, float *dmask, void *ws, hipStream_t s);
 size_t lookup_conv_weights_bytes();
 hipError_t launch_lookup_conv_weights(const float *w, int O, int C, void *packed, hipStream_t s);
 hipError_t launch_lookup_conv(const ConstLevelPtrs &pyr, const float *coords, int B, int NQ, int H, int W,

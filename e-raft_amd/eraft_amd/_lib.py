@@ -29,7 +29,7 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
            "corr_forward_splat", "corr_convex_upsample", "corr_voxel_grid_workspace",
            "corr_voxel_grid", "corr_lookup_conv", "corr_lookup_conv_weights", "corr_lookup_conv_weights_bytes", "corr_voxel_grid_tbilinear_workspace",
            "corr_voxel_grid_tbilinear", "corr_lookup_bwd_multi", "corr_pool_fold", "corr_backward_workspace",
-           "corr_backward")
+           "corr_backward", "corr_convex_upsample_bwd_workspace", "corr_convex_upsample_bwd")
 
 # Build algorithms (include/corr_mi355x.h).  F16X3 is the default: fp32 features split into
 # f16 hi/lo pairs, three f16 MFMAs per product, fp32 accumulate (~1e-6 of max|C| from the
@@ -94,6 +94,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.corr_forward_splat_workspace.restype = sz
     lib.corr_forward_splat.argtypes = [vp, i, i, i, vp, vp, sz, vp]
     lib.corr_convex_upsample.argtypes = [vp, vp, i, i, i, vp, vp]
+    lib.corr_convex_upsample_bwd_workspace.argtypes = [i, i, i]
+    lib.corr_convex_upsample_bwd_workspace.restype = sz
+    lib.corr_convex_upsample_bwd.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp, sz, vp]
     lib.corr_lookup_conv.argtypes = [vp, vp, i, i, i, i, i, vp, vp, i, vp, vp]
     lib.corr_lookup_conv_weights.argtypes = [vp, i, i, vp, vp]
     lib.corr_lookup_conv_weights_bytes.argtypes = []
@@ -114,7 +117,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
               "corr_build_ex", "corr_build_bwd_ex", "corr_forward_splat",
               "corr_convex_upsample", "corr_voxel_grid", "corr_lookup_conv", "corr_lookup_conv_weights",
               "corr_voxel_grid_tbilinear", "corr_lookup_bwd_multi", "corr_pool_fold", "corr_backward_workspace",
-           "corr_backward"):
+              "corr_backward", "corr_convex_upsample_bwd"):
         getattr(lib, f).restype = i
     if path is None:
         _lib = lib
@@ -307,6 +310,23 @@ def convex_upsample(flow, mask, out):
     f, m, o = _dev(flow, "flow"), _dev(mask, "mask"), _dev(out, "out")
     with torch.cuda.device(flow.device):
         _check(load().corr_convex_upsample(f, m, N, h, w, o, _stream(flow)))
+
+
+def convex_upsample_bwd(flow, mask, grad_out):
+    """corr_convex_upsample_bwd: -> (dflow [N, 2, h, w], dmask [N, 576, h, w])."""
+    N, _, h, w = flow.shape
+    if tuple(mask.shape) != (N, 576, h, w) or tuple(grad_out.shape) != (N, 2, 8 * h, 8 * w):
+        raise ValueError(f"convex_upsample_bwd: flow {tuple(flow.shape)}, mask {tuple(mask.shape)}, "
+                         f"grad_out {tuple(grad_out.shape)}")
+    lib = load()
+    dflow = torch.empty_like(flow)
+    dmask = torch.empty_like(mask)
+    ws = torch.empty(lib.corr_convex_upsample_bwd_workspace(N, h, w), dtype=torch.uint8, device=flow.device)
+    with torch.cuda.device(flow.device):
+        _check(lib.corr_convex_upsample_bwd(_dev(flow, "flow"), _dev(mask, "mask"), _dev(grad_out, "grad_out"),
+                                            N, h, w, _dev(dflow, "dflow"), _dev(dmask, "dmask"),
+                                            ws.data_ptr(), ws.numel(), _stream(flow)))
+    return dflow, dmask
 
 
 def voxel_grid(x, y, t, p, out, normalize):

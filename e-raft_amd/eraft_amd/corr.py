@@ -78,9 +78,10 @@ def _weight_pack(weight):
 class _State:
     """Per-block state shared by the build and lookup autograd nodes."""
 
-    __slots__ = ("levels", "grad_levels", "H", "W", "radius", "stash")
+    __slots__ = ("levels", "grad_levels", "H", "W", "radius", "stash", "trains")
 
     def __init__(self, H, W, radius):
+        self.trains = False      # the build is in the autograd graph (gradients reach the fmaps)
         self.levels = None
         self.grad_levels = None  # per-lookup path: the accumulated gradient pyramid
         self.stash = []          # fused path: (coords, grad_out) of every lookup backward
@@ -152,19 +153,62 @@ class _LookupFn(torch.autograd.Function):
         return out
 
     @staticmethod
-    def backward(ctx, grad_out):
-        (coords,) = ctx.saved_tensors
-        st = ctx.state
+    def stash_backward(st, coords, grad_out, radius):
         if _lib.fused_backward():
             st.stash.append((coords, grad_out.contiguous()))  # run by the build's backward
         else:
             if st.grad_levels is None:
                 B, _, H, W = coords.shape
                 st.grad_levels = _alloc_pyramid(B, H, W, len(st.levels), coords, zero=True)
-            _lib.lookup_bwd(coords, grad_out.contiguous(), ctx.radius, st.grad_levels)
+            _lib.lookup_bwd(coords, grad_out.contiguous(), radius, st.grad_levels)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        (coords,) = ctx.saved_tensors
+        _LookupFn.stash_backward(ctx.state, coords, grad_out, ctx.radius)
         # No gradient for the token: the engine still runs the build's backward, after every
         # lookup backward (it depends on all of them), and nothing is filled or summed for it.
         return None, None, None, None
+
+
+class _LookupConvFn(torch.autograd.Function):
+    """relu(convc1(lookup(coords))) (update.py:68,75) as one fused kernel in the forward; the
+    324-channel lookup output is never written.  Backward (training, config 4): g = dL/dout
+    masked by out > 0 (ReLU's threshold backward); d bias = sum of g; the lookup is recomputed
+    by the lookup kernel (bit-identical to the forward's values) for dW = g lk^T; the lookup's
+    own gradient W^T g goes into the build's stash, exactly as a plain lookup's backward does,
+    so corr_backward folds it with every other lookup."""
+
+    @staticmethod
+    def forward(ctx, coords, token, weight, bias, relu, radius, state):
+        levels = state.levels
+        B, _, H, W = coords.shape
+        out = torch.empty((B, weight.shape[0], H, W), dtype=torch.float32, device=coords.device)
+        _lib.lookup_conv(levels, coords, radius, _weight_pack(weight), bias.detach().contiguous().float(), out, relu)
+        ctx.save_for_backward(coords, weight, out)
+        ctx.relu, ctx.radius, ctx.state = relu, radius, state
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        coords, weight, out = ctx.saved_tensors
+        st = ctx.state
+        g = grad_out.contiguous()
+        if ctx.relu:
+            g = torch.where(out > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
+        B, O, H, W = g.shape
+        C = weight.shape[1]
+        gf = g.view(B, O, H * W)
+        dbias = gf.sum(dim=(0, 2)) if ctx.needs_input_grad[3] else None
+        dW = None
+        if ctx.needs_input_grad[2]:
+            lk = torch.empty((B, C, H, W), dtype=torch.float32, device=coords.device)
+            _lib.lookup(st.levels, coords, ctx.radius, lk)
+            dW = torch.bmm(gf, lk.view(B, C, H * W).transpose(1, 2)).sum(0).view_as(weight)
+        if st.trains:  # the lookup's upstream gradient, for the build's backward
+            dlk = torch.matmul(weight.view(O, C).t(), gf).view(B, C, H, W)
+            _LookupFn.stash_backward(st, coords, dlk, ctx.radius)
+        return None, None, dW, dbias, None, None, None
 
 
 class CorrBlock:
@@ -185,6 +229,7 @@ class CorrBlock:
             outs = _BuildFn.apply(fmap1, fmap2, num_levels, self._state)
             self.corr_pyramid = list(outs[:-1])
             self._token = outs[-1]
+            self._state.trains = True
         else:
             B = fmap1.shape[0]
             self.corr_pyramid = _alloc_pyramid(B, H, W, num_levels, fmap1)
@@ -213,7 +258,8 @@ class CorrBlock:
     def lookup_conv(self, coords, weight, bias, relu=True):
         """Lookup fused with the motion encoder's first layer, relu(convc1(self(coords)))
         (update.py:68,75), without materialising the lookup output.  weight: convc1.weight
-        [256, L*K, 1, 1]; bias [256].  Inference only (no autograd)."""
+        [256, L*K, 1, 1]; bias [256].  Under autograd (training) gradients reach the weight,
+        the bias and, through the build's backward, both feature maps (_LookupConvFn)."""
         self._check_coords(coords)
         B, _, H, W = coords.shape
         K = (2 * self.radius + 1) ** 2
@@ -221,9 +267,15 @@ class CorrBlock:
         if tuple(weight.shape) not in ((256, C, 1, 1), (256, C)) or tuple(bias.shape) != (256,):
             raise ValueError(f"lookup_conv needs weight [256, {C}, 1, 1] and bias [256] "
                              f"(got {tuple(weight.shape)}, {tuple(bias.shape)})")
+        coords = coords.detach().contiguous()
+        if torch.is_grad_enabled() and (self._token is not None or weight.requires_grad or bias.requires_grad):
+            token = self._token
+            if token is None:  # the pyramid is constant; gradients reach only the weight and bias
+                token = coords.new_empty(())
+            return _LookupConvFn.apply(coords, token, weight, bias, relu, self.radius, self._state)
         cached = _weight_pack(weight)  # split once per weight version (every GRU iteration reuses it)
         out = torch.empty((B, weight.shape[0], H, W), dtype=torch.float32, device=coords.device)
-        _lib.lookup_conv(self._state.levels, coords.detach().contiguous(), self.radius, cached,
+        _lib.lookup_conv(self._state.levels, coords, self.radius, cached,
                          bias.detach().contiguous().float(), out, relu)
         return out
 

@@ -108,7 +108,7 @@ class BasicMotionEncoder(nn.Module):
         self.conv = nn.Conv2d(64 + 192, 128 - 2, 3, padding=1)
 
     def forward(self, flow, corr, fused=False):
-        # fused: corr already is relu(convc1(lookup)) (CorrBlock.lookup_conv, inference)
+        # fused: corr already is relu(convc1(lookup)) (CorrBlock.lookup_conv)
         c = F.relu(self.convc2(corr if fused else F.relu(self.convc1(corr))))
         f = F.relu(self.convf2(F.relu(self.convf1(flow))))
         return torch.cat([F.relu(self.conv(torch.cat([c, f], dim=1))), flow], dim=1)
@@ -184,6 +184,28 @@ class ImagePadder:
         return image[..., self.pad_height:, self.pad_width:]
 
 
+class _ConvexUpsampleFn(torch.autograd.Function):
+    """ERAFT.upsample_flow on the MI355X: forward corr_convex_upsample, backward
+    corr_convex_upsample_bwd (softmax and unfold backward fused; the 9x-expanded product of
+    the torch composition is never materialised in either direction)."""
+
+    @staticmethod
+    def forward(ctx, flow, mask):
+        from . import _lib
+        n, _, h, w = flow.shape
+        out = torch.empty((n, 2, 8 * h, 8 * w), dtype=torch.float32, device=flow.device)
+        _lib.convex_upsample(flow, mask, out)
+        ctx.save_for_backward(flow, mask)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        from . import _lib
+        flow, mask = ctx.saved_tensors
+        dflow, dmask = _lib.convex_upsample_bwd(flow, mask, grad_out.contiguous())
+        return dflow, dmask
+
+
 class ERAFT(nn.Module):
     """E-RAFT (model/eraft.py:37-146) with the MI355X CorrBlock on its hot path."""
 
@@ -216,15 +238,12 @@ class ERAFT(nn.Module):
 
     @staticmethod
     def upsample_flow(flow, mask):
-        """Convex combination of 3x3 neighbours, x8 (eraft.py:75-86).  Inference runs the
-        one-pass HIP kernel (corr_convex_upsample); under autograd (training) the torch
-        composition below keeps the gradient (it is also what bench.py's CPU baseline runs)."""
-        if flow.is_cuda and not (torch.is_grad_enabled() and (flow.requires_grad or mask.requires_grad)):
-            from . import _lib
-            n, _, h, w = flow.shape
-            out = torch.empty((n, 2, 8 * h, 8 * w), dtype=torch.float32, device=flow.device)
-            _lib.convex_upsample(flow.float().contiguous(), mask.float().contiguous(), out)
-            return out
+        """Convex combination of 3x3 neighbours, x8 (eraft.py:75-86).  On the MI355X: the
+        one-pass HIP kernel (corr_convex_upsample), with its HIP backward under autograd
+        (_ConvexUpsampleFn); on the CPU the torch composition below (what bench.py's CPU
+        baseline runs)."""
+        if flow.is_cuda:
+            return _ConvexUpsampleFn.apply(flow.float().contiguous(), mask.float().contiguous())
         n, _, h, w = flow.shape
         mask = torch.softmax(mask.view(n, 1, 9, 8, 8, h, w), dim=2)
         up = F.unfold(8 * flow, [3, 3], padding=1).view(n, 2, 9, 1, 1, h, w)
@@ -245,9 +264,10 @@ class ERAFT(nn.Module):
         if flow_init is not None:
             coords1 = coords1 + flow_init
         predictions = []
-        # inference on the MI355X: the lookup feeds convc1 on-chip (corr_lookup_conv)
-        fuse = (self.fuse_lookup_conv and image1.is_cuda and not torch.is_grad_enabled()
-                and self.corr_radius == 4 and hasattr(corr_fn, "lookup_conv"))
+        # on the MI355X the lookup feeds convc1 on-chip (corr_lookup_conv), at inference and, with
+        # its autograd backward (corr._LookupConvFn), in training
+        fuse = (self.fuse_lookup_conv and image1.is_cuda and self.corr_radius == 4
+                and hasattr(corr_fn, "lookup_conv"))
         for _ in range(iters):
             coords1 = coords1.detach()
             if fuse:

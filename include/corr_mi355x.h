@@ -261,6 +261,16 @@ int corr_voxel_grid_tbilinear(const double *events, int n_events, int C, int H, 
  */
 int corr_convex_upsample(const float *flow, const float *mask, int N, int h, int w, float *out,
                          void *stream);
+/*
+ * Backward of corr_convex_upsample (autograd of model/eraft.py:75-86 w.r.t. flow and mask):
+ * grad_out [N][2][8h][8w] -> dflow [N][2][h][w], dmask [N][576][h][w] (both overwritten).
+ * Softmax backward p_k (dv_k - sum p dv) per sub-pixel; dflow gathers 8 * sum p_k G over the
+ * sub-pixels and taps that read each coarse pixel.  Workspace: the per-tap partial sums,
+ * corr_convex_upsample_bwd_workspace(N, h, w) bytes.  fp32, tolerance-level parity.
+ */
+size_t corr_convex_upsample_bwd_workspace(int N, int h, int w);
+int corr_convex_upsample_bwd(const float *flow, const float *mask, const float *grad_out, int N, int h, int w,
+                             float *dflow, float *dmask, void *workspace, size_t workspace_bytes, void *stream);
 int corr_forward_splat(const float *flow, int B, int H, int W, float *out, void *workspace,
                        size_t workspace_bytes, void *stream);
 

@@ -633,3 +633,70 @@ def test_lookup_conv_vs_torch_reference(B, H, W, L):
         ref = (torch.relu(pre) if relu else pre).numpy()
         out = cb.lookup_conv(c, w, bias, relu=relu).cpu().numpy()
         assert np.abs(out - ref).max() <= 1e-5 * np.abs(ref).max(), relu
+
+
+def test_lookup_conv_autograd_matches_unfused():
+    """Training through the fused lookup + convc1 (corr._LookupConvFn): gradients w.r.t. both
+    fmaps, the weight and the bias agree with the unfused autograd path (HIP lookup + conv2d +
+    relu) within 1e-4 norm-relative, over 3 summed GRU-style lookups."""
+    import torch.nn.functional as F
+    B, D, H, W, L, r = 2, 32, 16, 20, 4, 4
+    K = (2 * r + 1) ** 2
+    f1, f2 = prng.gauss(91, (B, D, H, W)), prng.gauss(92, (B, D, H, W))
+    w0 = prng.gauss(93, (256, L * K, 1, 1), 0.05)
+    b0 = prng.gauss(94, (256,), 0.1)
+    coords = [torch.from_numpy(prng.lookup_coords(95 + t, B, H, W, 3.0)).to(DEV) for t in range(3)]
+    gouts = [torch.from_numpy(prng.gauss(99 + t, (B, 256, H, W))).to(DEV) for t in range(3)]
+    grads = []
+    for fused in (True, False):
+        t1 = torch.from_numpy(f1).to(DEV).requires_grad_(True)
+        t2 = torch.from_numpy(f2).to(DEV).requires_grad_(True)
+        w = torch.from_numpy(w0).to(DEV).requires_grad_(True)
+        b = torch.from_numpy(b0).to(DEV).requires_grad_(True)
+        cb = _cb()(t1, t2, num_levels=L, radius=r)
+        loss = 0
+        for c, g in zip(coords, gouts):
+            out = cb.lookup_conv(c, w, b) if fused else F.relu(F.conv2d(cb(c), w, b))
+            loss = loss + (out * g).sum()
+        loss.backward()
+        grads.append([t.grad.detach().cpu().numpy() for t in (t1, t2, w, b)])
+    for name, a, ref in zip(("dfmap1", "dfmap2", "dweight", "dbias"), *grads):
+        assert norm_rel(a, ref) <= REL_TOL, (name, norm_rel(a, ref))
+
+
+def test_lookup_conv_weight_pack_not_aliased():
+    """The packed convc1 split is cached on the weight tensor: a second weight that reuses the
+    first one's allocation (same data_ptr, same _version) must not see the first one's pack."""
+    B, D, H, W, L, r = 1, 16, 12, 16, 4, 4
+    K = (2 * r + 1) ** 2
+    f1, f2 = prng.gauss(111, (B, D, H, W)), prng.gauss(112, (B, D, H, W))
+    cb = _cb()(torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV), num_levels=L, radius=r)
+    c = torch.from_numpy(prng.lookup_coords(113, B, H, W, 3.0)).to(DEV)
+    bias = torch.zeros(256, device=DEV)
+    outs = []
+    for seed in (114, 115):
+        w = torch.from_numpy(prng.gauss(seed, (256, L * K, 1, 1), 0.05)).to(DEV)
+        outs.append((w.data_ptr(), cb.lookup_conv(c, w, bias).cpu().numpy(),
+                     torch.relu(torch.nn.functional.conv2d(cb(c), w, bias)).cpu().numpy()))
+        del w
+    for _, out, ref in outs:
+        assert np.abs(out - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("N,h,w", [(1, 60, 80), (2, 9, 70)])
+def test_convex_upsample_backward_vs_autograd(N, h, w):
+    """corr_convex_upsample_bwd (ERAFT.upsample_flow's HIP backward) vs autograd of the
+    reference composition (eraft.py:75-86) in float64: dflow and dmask within 1e-4 of max."""
+    from eraft_amd.model import ERAFT
+    flow = prng.gauss(121, (N, 2, h, w), 3.0)
+    mask = prng.gauss(122, (N, 576, h, w), 2.0)
+    g = prng.gauss(123, (N, 2, 8 * h, 8 * w))
+    tf = torch.from_numpy(flow).to(DEV).requires_grad_(True)
+    tm = torch.from_numpy(mask).to(DEV).requires_grad_(True)
+    ERAFT.upsample_flow(tf, tm).backward(torch.from_numpy(g).to(DEV))
+    rf = torch.from_numpy(flow).double().requires_grad_(True)
+    rm = torch.from_numpy(mask).double().requires_grad_(True)
+    ERAFT.upsample_flow(rf, rm).backward(torch.from_numpy(g).double())  # CPU: the torch composition
+    for a, ref in ((tf.grad, rf.grad), (tm.grad, rm.grad)):
+        a, ref = a.cpu().double().numpy(), ref.numpy()
+        assert np.abs(a - ref).max() <= 1e-4 * np.abs(ref).max()

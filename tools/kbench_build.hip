@@ -1,5 +1,5 @@
 // kbench_build.hip — the f16x3 build (corr_build_split.hip) against the exact-fp32 MFMA build
-// (corr_build.hip) and the round-1 f16x3 kernel (tools/legacy/build_split_r01.hip):
+// (corr_build.hip), the persistent form against the one-tile-per-workgroup kernel:
 //   * accuracy: max |x - f32| / max |f32| over every pyramid level, three operand scales;
 //   * pooling: levels 1-3 bit-identical to avg_pool2d of the kernel's own level 0 (host check);
 //   * timing: interleaved rounds of every variant in one process, random data (HIP events
@@ -108,6 +108,18 @@ int main(int argc, char **argv) {
         vs.push_back({"f32 build (corr_build.hip)", [&](float *o) {
                           return launch_build_cfg<BuildDefault>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
                       }, true});
+        vs.push_back({"f32 2x2x2 BK8 occ3", [&](float *o) {
+                          return launch_build_cfg<BuildCfg<2, 2, 2, 8, 3, true, false>>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
+                      }, true});
+        vs.push_back({"f32 2x2x2 BK16 occ3", [&](float *o) {
+                          return launch_build_cfg<BuildCfg<2, 2, 2, 16, 3, true, false>>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
+                      }, true});
+        vs.push_back({"f32 4x1x1 BK16 occ4", [&](float *o) {
+                          return launch_build_cfg<BuildCfg<4, 1, 1, 16, 4, true, false>>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
+                      }, true});
+        vs.push_back({"f32 2x2x2 BK8 occ4 skip", [&](float *o) {
+                          return launch_build_cfg<BuildCfg<2, 2, 2, 8, 4, true, true>>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
+                      }, true});
         vs.push_back({"x3 pack+mfma", [&](float *o) {
                           return launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
                       }, true});
@@ -116,6 +128,9 @@ int main(int argc, char **argv) {
                       }, false});
         vs.push_back({"x3 mfma persist", [&](float *o) {
                           return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1);
+                      }, false});
+        vs.push_back({"x3 mfma persist nohalf", [&](float *o) {
+                          return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 0, false);
                       }, false});
         vs.push_back({"x3 mfma persist 2/CU", [&](float *o) {
                           return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 512);
@@ -170,6 +185,7 @@ int main(int argc, char **argv) {
             same("persistent", [&](float *o) { return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1); });
             same("persistent 2/CU", [&](float *o) { return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 512); });
             same("persistent 1/CU", [&](float *o) { return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 256); });
+            same("persistent nohalf", [&](float *o) { return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 0, false); });
         }
         {  // pooling of the new kernel: every level bit-identical to avg_pool2d of its own level 0
             CK(launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), ws, 0));

@@ -1,11 +1,11 @@
-# PMC passes over tools/_build/kbench_split (run via gpurun):  bash tools/pmc_kbench.sh <shape> <variant-substring>
+# PMC passes over tools/_build/kbench_build (run via gpurun):  bash tools/pmc_kbench.sh <shape> <variant-substring>
 set -o pipefail
-SH=${1:-dsec}; VAR=${2:-"2x2 MQ2 o2"}
+SH=${1:-dsec}; VAR=${2:-"x3 mfma persist"}
 OUT=gpurun_out/pk
 mkdir -p $OUT
 export TMPDIR=/tmp
 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
-K="./tools/_build/kbench_split 3 $SH"
+K="./tools/_build/kbench_build 3 $SH"
 i=0
 for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES" \
          "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
