@@ -490,7 +490,7 @@ __global__ __launch_bounds__(kLcNT) void lookup_conv_kernel(ConstLevelPtrs pyr, 
             for (int r = 0; r < 4; ++r) {
                 const int o = 32 * w + 16 * t + 4 * (lane >> 4) + r;
                 float v = ldexpf(acc[t][c][r], -(wshift[o] + sq)) + bias[o];
-                if (relu) v = fmaxf(v, 0.0f);
+                if (relu && v < 0.0f) v = 0.0f;  // torch.relu: a NaN stays a NaN (fmaxf would drop it)
                 out[((size_t)b * kLcO + o) * N + n] = v;
             }
     }

@@ -666,8 +666,9 @@ def test_lookup_conv_autograd_matches_unfused():
 
 def test_lookup_conv_weight_pack_not_aliased():
     """The packed convc1 split is cached on the weight tensor: a second weight that reuses the
-    first one's allocation (same data_ptr, same _version) must not see the first one's pack."""
-    B, D, H, W, L, r = 1, 16, 12, 16, 4, 4
+    first one's allocation (same data_ptr, same _version) must not see the first one's pack.
+    (16 x 16: every level at least 2 x 2, so the reference composition is finite.)"""
+    B, D, H, W, L, r = 1, 16, 16, 16, 4, 4
     K = (2 * r + 1) ** 2
     f1, f2 = prng.gauss(111, (B, D, H, W)), prng.gauss(112, (B, D, H, W))
     cb = _cb()(torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV), num_levels=L, radius=r)
@@ -681,6 +682,22 @@ def test_lookup_conv_weight_pack_not_aliased():
         del w
     for _, out, ref in outs:
         assert np.abs(out - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+def test_lookup_conv_nan_level_propagates():
+    """A degenerate 1 x 2 level makes the reference lookup NaN (utils.py:11-12), and
+    relu(conv2d(.)) of it is NaN everywhere: the fused kernel must give NaN at the same places
+    (its ReLU keeps a NaN, as torch.relu does)."""
+    B, D, H, W, L, r = 1, 16, 12, 16, 4, 4
+    K = (2 * r + 1) ** 2
+    f1, f2 = prng.gauss(116, (B, D, H, W)), prng.gauss(117, (B, D, H, W))
+    cb = _cb()(torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV), num_levels=L, radius=r)
+    c = torch.from_numpy(prng.lookup_coords(118, B, H, W, 3.0)).to(DEV)
+    w = torch.from_numpy(prng.gauss(119, (256, L * K, 1, 1), 0.05)).to(DEV)
+    bias = torch.zeros(256, device=DEV)
+    ref = torch.relu(torch.nn.functional.conv2d(cb(c), w, bias)).cpu().numpy()
+    out = cb.lookup_conv(c, w, bias).cpu().numpy()
+    assert np.array_equal(np.isnan(out), np.isnan(ref)) and np.isnan(ref).any()
 
 
 @pytest.mark.parametrize("N,h,w", [(1, 60, 80), (2, 9, 70)])
