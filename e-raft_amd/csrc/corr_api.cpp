@@ -107,7 +107,10 @@ int corr_build_ex(int algo, const float *fmap1_rows, int NQ, const float *fmap2,
     static const char *fn = "corr_build_ex";
     if (algo == CORR_BUILD_FP32) return corr_build_rows(fmap1_rows, NQ, fmap2, B, D, H, W, levels, pyr, stream);
     g_err[0] = 0;
-    if (algo != CORR_BUILD_F16X3) return fail(CORR_EINVAL, "%s: unknown algorithm %d", fn, algo);
+    const int phase = algo & (CORR_BUILD_ONLY_PACK | CORR_BUILD_ONLY_MFMA);
+    algo &= ~(CORR_BUILD_ONLY_PACK | CORR_BUILD_ONLY_MFMA);
+    if (algo != CORR_BUILD_F16X3 || phase == (CORR_BUILD_ONLY_PACK | CORR_BUILD_ONLY_MFMA))
+        return fail(CORR_EINVAL, "%s: unknown algorithm %d", fn, algo | phase);
     int rc = check_dims(fn, B, NQ, H, W, levels);
     if (rc) return rc;
     if (D < 1) return fail(CORR_EINVAL, "%s: D must be >= 1 (got %d)", fn, D);
@@ -120,7 +123,8 @@ int corr_build_ex(int algo, const float *fmap1_rows, int NQ, const float *fmap2,
         return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
     LevelPtrs lp{};
     if ((rc = check_levels(fn, pyr, levels, "pyr", lp.p))) return rc;
-    return hip_status(launch_build_split(fmap1_rows, NQ, fmap2, B, D, H, W, levels, lp, workspace, (hipStream_t)stream),
+    const int part = phase == CORR_BUILD_ONLY_PACK ? 1 : phase == CORR_BUILD_ONLY_MFMA ? 2 : 0;
+    return hip_status(launch_build_split(fmap1_rows, NQ, fmap2, B, D, H, W, levels, lp, workspace, (hipStream_t)stream, part),
                       fn);
 }
 

@@ -182,6 +182,8 @@ struct BuildArgs {
     int cons;          // levels 1 and 2 as 16-B stores (W/2, W/4 multiples of 4, 16-B aligned bases)
     float inv_s;     // 1/sqrt(D) otherwise (multiplied: within tolerance, not bitwise)
     int ntiles;      // persistent kernel: B * npatch * NQG
+    unsigned long long *stamp;  // diagnostic build only (STAMP): per-workgroup clock stamps
+    int order;       // tile order: 0 = query group fastest (groups of kGroupQ), 1 = patch column fastest
 };
 
 // Tile order (L2 reuse): per batch item, query groups in groups of kGroupQ; inside a group the
@@ -196,6 +198,20 @@ __device__ __forceinline__ Tile tile_of(const BuildArgs &p, int t) {
     const int per_b = p.npatch * p.NQG;
     o.b = t / per_b;
     const int r = t - o.b * per_b;
+    if (p.order == 1) {
+        // a patch row's patches consecutive for one query group: the 64-B row segments of
+        // horizontally adjacent patches share 128-B lines, written close in time (one XCD)
+        const int CB = p.CB, npr = p.npatch / CB;
+        const int g = r / (kGroupQ * p.npatch);
+        const int gm = min(kGroupQ, p.NQG - g * kGroupQ);
+        const int r2 = r - g * kGroupQ * p.npatch;
+        o.py = r2 / (gm * CB);
+        const int r3 = r2 - o.py * gm * CB;
+        o.qg = g * kGroupQ + r3 / CB;
+        o.cb = r3 - (r3 / CB) * CB;
+        (void)npr;
+        return o;
+    }
     const int g = r / (kGroupQ * p.npatch);
     const int gm = min(kGroupQ, p.NQG - g * kGroupQ);
     const int r2 = r - g * kGroupQ * p.npatch;
@@ -251,19 +267,26 @@ __device__ __forceinline__ void store2(float *row, int X, int Wl, float a, float
 
 // SS > 0: S = SS K steps, fully unrolled (straight-line code: the compiler's own waits on the
 // query registers are then exact and never drain the prefetch).  SS = 0: any S, runtime loop.
-template <int SS>
-__global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
+// QS: query register slots (the query prefetch distance is QS - 1 K steps).  PIPE: the target
+// fragments of map row r + 1 are read from LDS while row r's six MFMAs issue (the LDS latency
+// is hidden instead of exposed once per row); the per-accumulator product order is unchanged.
+// NR: map rows of the patch whose MFMAs run (8; 4 for a patch with at most 4 rows inside the
+// map: the last patch row when H % 8 is 1-4, i.e. DSEC, train, MVSEC — its rows 4-7 are padding
+// whose accumulators stay zero and whose stores are dropped).
+template <int SS, int QS, bool PIPE, int NR>
+__device__ __forceinline__ void build_tile(const BuildArgs &p, const Tile tl) {
+    static_assert(QS == 3 || QS == 4, "query slots (prefetch distance 2 or 3)");
     extern __shared__ __attribute__((aligned(16))) char smem_build[];
     char *smem = smem_build;
     int *lds_et = reinterpret_cast<int *>(smem + kRing * kSlotBytes);
 
-    const Tile tl = tile_of(p, xcd_swizzle(blockIdx.x, gridDim.x));
     const int b = tl.b, y0 = tl.py * kPatchRows, x0 = tl.cb * 16;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ci = lane & 15, grp = lane >> 4;
     const int qb0 = tl.qg * (kQPerWG / 16) + 2 * w;  // this wave's first 16-query block
     const int S = SS > 0 ? SS : p.S;
+    const bool qact = qb0 * 16 < p.NQ;  // wave-uniform
 
     // The patch's target exponents -> LDS by LDS-DMA (waves 0 and 1, one dword per lane) and
     // the query exponents -> registers, issued ahead of the operand stream and never waited for
@@ -293,14 +316,14 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
     const u32x4 *qsrc = p.pq + ((size_t)b * S * p.NQB + qb0) * kRecU + lane;
 
     // Issue schedule (SS > 0, fully unrolled): step k issues the wave's 4 query loads of step
-    // k + 3 (into register slot (k + 3) % 4), then its 4 LDS-DMA pieces of step k + 2 (ring slot
-    // (k + 2) % 3); the prologue plays steps -3..-1.  The DMA is inline asm, so the compiler
-    // does not make every ds_read wait for ALL outstanding DMAs (it cannot tell the ring slots
-    // apart).  At step k's barrier the loads younger than its DMA are exactly step k-1's group
-    // (vmcnt(8)), and every query load of step k is older; the query registers are then
-    // passed through an empty asm, before which the compiler's own wait (counting only the query
-    // loads it knows of: steps k+1, k+2) is vmcnt(8) as well — already satisfied, no drain.
-    u32x4 qv[4][2][2];  // [register slot][query block][hi, lo]
+    // k + QS - 1 (into register slot (k + QS - 1) % QS), then its 4 LDS-DMA pieces of step k + 2
+    // (ring slot (k + 2) % 3); the prologue plays the steps before 0.  The DMA is inline asm, so
+    // the compiler does not make every ds_read wait for ALL outstanding DMAs (it cannot tell the
+    // ring slots apart).  At step k's barrier the operations younger than its DMA are exactly
+    // the later groups (vmcnt(8) or (4)), and every query load of step k is older; the query
+    // registers are then passed through an empty asm, before which the compiler's own wait
+    // (counting only the query loads it knows of) is already satisfied: no drain.
+    u32x4 qv[QS][2][2];  // [register slot][query block][hi, lo]
     auto issue_q = [&](int s, int slot) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -329,37 +352,68 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
             qh[i] = __builtin_bit_cast(half8, qv[qslot][i][0]);
             ql[i] = __builtin_bit_cast(half8, qv[qslot][i][1]);
         }
+        if constexpr (PIPE) {
+            half8 fh[2], fl[2];
+            fh[0] = __builtin_bit_cast(half8, A[lane]);
+            fl[0] = __builtin_bit_cast(half8, A[64 + lane]);
 #pragma unroll
-        for (int r = 0; r < kPatchRows; ++r) {
-            const half8 ah = __builtin_bit_cast(half8, A[(2 * r) * 64 + lane]);
-            const half8 al = __builtin_bit_cast(half8, A[(2 * r + 1) * 64 + lane]);
+            for (int r = 0; r < NR; ++r) {
+                const int c = r & 1;
+                if (r + 1 < NR) {
+                    fh[c ^ 1] = __builtin_bit_cast(half8, A[(2 * r + 2) * 64 + lane]);
+                    fl[c ^ 1] = __builtin_bit_cast(half8, A[(2 * r + 3) * 64 + lane]);
+                }
+                acc[0][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl[c], qh[0], acc[0][r], 0, 0, 0);
+                acc[1][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl[c], qh[1], acc[1][r], 0, 0, 0);
+                acc[0][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], ql[0], acc[0][r], 0, 0, 0);
+                acc[1][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], ql[1], acc[1][r], 0, 0, 0);
+                acc[0][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], qh[0], acc[0][r], 0, 0, 0);
+                acc[1][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], qh[1], acc[1][r], 0, 0, 0);
+            }
+            // schedule: row 0's reads, then per row the next row's 2 reads ahead of its 6 MFMAs
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                acc[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, qh[i], acc[i][r], 0, 0, 0);
-                acc[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, ql[i], acc[i][r], 0, 0, 0);
-                acc[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, qh[i], acc[i][r], 0, 0, 0);
+            for (int r = 0; r < NR; ++r) {
+                if (r + 1 < NR) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const half8 ah = __builtin_bit_cast(half8, A[(2 * r) * 64 + lane]);
+                const half8 al = __builtin_bit_cast(half8, A[(2 * r + 1) * 64 + lane]);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    acc[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, qh[i], acc[i][r], 0, 0, 0);
+                    acc[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, ql[i], acc[i][r], 0, 0, 0);
+                    acc[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, qh[i], acc[i][r], 0, 0, 0);
+                }
             }
         }
     };
 
     if constexpr (SS > 0) {
+        constexpr int QD = QS - 1;  // query prefetch distance (>= 2: Q(s) is issued before T(s))
+        // prologue: Q0 Q1 T0 [Q2] T1
         issue_q(0, 0);
         if (SS > 1) issue_q(1, 1);
         issue_t(0, 0);
-        if (SS > 2) issue_q(2, 2);
+        if (QD > 2 && SS > 2) issue_q(2, 2);
         if (SS > 1) issue_t(1, 1);
 #pragma unroll
         for (int s = 0; s < SS; ++s) {
-            // loads younger than step s's DMA: step s-1's group = Q(s+2), T(s+1) where they exist
-            const int younger = (s + 2 < SS ? 4 : 0) + (s + 1 < SS ? 4 : 0);
+            // operations younger than step s's DMA T(s): at step 0 the prologue's later loads,
+            // else step s - 1's group (Q(s - 1 + QD), T(s + 1), where they exist)
+            const int younger = s == 0 ? (QD > 2 && SS > 2 ? 4 : 0) + (SS > 1 ? 4 : 0)
+                                       : (s - 1 + QD < SS ? 4 : 0) + (s + 1 < SS ? 4 : 0);
             if (younger == 8) wait_vmcnt_barrier<8>();
             else if (younger == 4) wait_vmcnt_barrier<4>();
             else wait_vmcnt_barrier<0>();
-            const int qs = s & 3;
+            const int qs = s % QS;
             asm volatile("" : "+v"(qv[qs][0][0]), "+v"(qv[qs][0][1]), "+v"(qv[qs][1][0]), "+v"(qv[qs][1][1]));
-            if (s + 3 < SS) issue_q(s + 3, (s + 3) & 3);
+            if (s + QD < SS) issue_q(s + QD, (s + QD) % QS);
             if (s + 2 < SS) issue_t(s + 2, (s + 2) % kRing);
-            compute(s % kRing, qs);
+            if (qact) compute(s % kRing, qs);  // a wave whose queries all lie past NQ skips its MFMAs
         }
     } else {
         // any S: no prefetch (one group in flight, drained every step)
@@ -474,24 +528,30 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
     }
 }
 
+template <int SS, int QS = 4, bool PIPE = false>
+__global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
+    const Tile tl = tile_of(p, xcd_swizzle(blockIdx.x, gridDim.x));
+    // two whole code paths (no value flows out of either): a half patch runs half the MFMAs
+    if (SS > 0 && tl.py * kPatchRows + kPatchRows / 2 >= p.H) build_tile<SS, QS, PIPE, kPatchRows / 2>(p, tl);
+    else build_tile<SS, QS, PIPE, kPatchRows>(p, tl);
+}
+
 // ---------------------------------------------------------------------------------------
-// Persistent form (the default wherever it applies: S = 4 or 8 K steps, 4+ levels, levels 0-2
-// stored as 16-B runs).  Same tiles, same arithmetic and the same bits as the kernel above;
-// what changes is the schedule:
-//   * a workgroup stays resident and walks a list of tiles (its XCD's contiguous share of the
-//     tile order, every P8-th tile), and the operand stream never stops at a tile boundary:
-//     the last K steps of tile k already issue the query loads and target DMA of tile k+1's
-//     first steps, so no workgroup waits out a cold prologue after the first;
+// Streaming (persistent) form.  Same tiles, same arithmetic and the same bits as the kernel
+// above; what changes is the schedule:
+//   * a workgroup stays resident (three per CU, <= 168 VGPRs) and walks a list of tiles (its
+//     XCD's contiguous share of the tile order, every P8-th tile); the operand stream never
+//     stops at a tile boundary: the last two K steps of tile k already issue the query loads
+//     and target DMA of tile k+1's first two steps, so only the first tile waits out a cold
+//     prologue;
 //   * the epilogue's pyramid stores are issued AFTER those loads and are never waited for at
 //     the tile boundary: tile k+1's first two barriers count them among the younger memory
-//     operations (vmcnt(30) = 8 loads + 22 stores), so the stores drain while the MFMAs of
-//     tile k+1 run, and the workgroups of one CU, which leave the store queue one after the
-//     other, fall out of step: one's store phase meets another's MFMA phase;
-//   * every wave issues exactly 22 store instructions per tile (buffer stores; a lane with
-//     nothing to write gets an out-of-range offset, which the hardware drops), so the
-//     hand-counted vmcnt immediates are exact.  No store is skipped by a branch.
-//   * the MFMA loop reads the next row's target fragments from LDS while the current row's
-//     six MFMAs issue, and alternates the two query blocks' accumulators.
+//     operations, so the stores drain while tile k+1's first MFMAs run, and co-resident
+//     workgroups, which the store path serves one after the other, fall out of step: one's
+//     store phase meets another's MFMA phase;
+//   * every wave issues exactly kStoresPerTile store instructions per tile (buffer stores; a
+//     lane with nothing to write gets an out-of-range offset, which the hardware drops), so
+//     the hand-counted vmcnt immediates are exact.  No store is skipped by a branch.
 // ---------------------------------------------------------------------------------------
 constexpr int kExpInts = kPatchRows * 16 + kQPerWG;  // a tile's exponents: targets, then queries
 constexpr int kBuildLdsP = kRing * kSlotBytes + 2 * kExpInts * 4;  // exponents double-buffered
@@ -525,11 +585,8 @@ __host__ __device__ constexpr int group_ops(int s) {
     return (s == SS - 2 ? 1 : 0) + 8;
 }
 
-// HALF: a tile whose patch has at most 4 map rows left (the last patch row when H % 8 is 1-4:
-// DSEC, train, MVSEC) runs the MFMAs of rows 0-3 only (its rows 4-7 are padding whose stores
-// are dropped anyway); same memory operations, same bits.
-template <int SS, bool HALF = true>
-__global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p) {
+template <int SS, bool STAMP = false>
+__global__ __launch_bounds__(256, 3) void corr_build_stream_kernel(BuildArgs p) {
     static_assert(SS == 4 || SS == 8, "query register slots and ring slots assume SS % 4 == 0, SS >= 4");
     extern __shared__ __attribute__((aligned(16))) char smem_build[];
     char *smem = smem_build;
@@ -539,7 +596,6 @@ __global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p)
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ci = lane & 15, grp = lane >> 4;
 
     // This workgroup's tiles: XCD x (= blockIdx % 8 under round-robin dispatch; speed only)
     // owns a contiguous range of the tile order, and its P8 workgroups deal it out.
@@ -550,36 +606,63 @@ __global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p)
     const int nmine = jj < len ? (len - 1 - jj) / P8 + 1 : 0;
     if (nmine == 0) return;
 
+    // STAMP (kbench diagnostic build only): wave 0 records s_memtime per tile (first 4 tiles):
+    // tile start, after step 0's barrier, after the K loop, after the epilogue; and realtime at
+    // the kernel start and end, into p.stamp (nothing reads it).
+    // (kept in LDS, past the exponents, so that no stamp is a vector-memory operation)
+    unsigned long long *stv = reinterpret_cast<unsigned long long *>(smem + kBuildLdsP);
+    auto stamp = [&](int i) __attribute__((always_inline)) {
+        if constexpr (STAMP) {
+            unsigned long long t;
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if (w == 0 && lane == 0) stv[i] = t;
+        }
+    };
+    if constexpr (STAMP) {
+        unsigned long long rt;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt)::"memory");
+        if (w == 0 && lane < 20) stv[lane] = lane == 0 ? rt : 0;
+    }
+
     const int H = p.H, W = p.W, N = p.N, NQ = p.NQ;
     const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
     const int N1 = H1 * W1, N2 = H2 * W2, N3 = H3 * W3;
     const size_t trowB = (size_t)p.CB * kRecU * 16;  // bytes per patch row of the target image
+    const size_t qstepB = (size_t)p.NQB * kRecU * 16;  // bytes per K step of the query image
 
     struct TA {
         int b, y0, x0, qb0;
     };
     auto tile_addr = [&](int k) __attribute__((always_inline)) {
         const Tile tl = tile_of(p, t0 + jj + k * P8);
-        return TA{tl.b, tl.py * kPatchRows, tl.cb * 16, tl.qg * (kQPerWG / 16) + 2 * w};
+        return TA{__builtin_amdgcn_readfirstlane(tl.b), __builtin_amdgcn_readfirstlane(tl.py * kPatchRows),
+                  __builtin_amdgcn_readfirstlane(tl.cb * 16),
+                  __builtin_amdgcn_readfirstlane(tl.qg * (kQPerWG / 16) + 2 * w)};
     };
 
     u32x4 qv[4][2][2];  // [register slot][query block][hi, lo]
+    // lane * 16, recomputed inside the tile loop from an opaque copy (so that no lane-dependent
+    // value is hoisted out of the loop and held, or spilled, across it)
+    uint32_t l16;
+    // the query image as one buffer resource (wave-uniform base, per-lane offset l16)
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void *)p.pq, 0, (int)((size_t)p.B * SS * qstepB), 0x00020000);
     auto issue_q = [&](const TA &a, int s, int slot) __attribute__((always_inline)) {
-        const u32x4 *q = p.pq + ((size_t)(a.b * SS + s) * p.NQB + a.qb0) * kRecU + lane;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            qv[slot][i][0] = q[i * kRecU];
-            qv[slot][i][1] = q[i * kRecU + 64];
-        }
+        const int so = __builtin_amdgcn_readfirstlane((int)(((a.b * SS + s) * p.NQB + a.qb0) * kRecU * 16));
+        qv[slot][0][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, l16, so, 0));
+        qv[slot][0][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, l16 + 1024, so, 0));
+        qv[slot][1][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, l16 + 2048, so, 0));
+        qv[slot][1][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, l16 + 3072, so, 0));
     };
     // the 4 DMA pieces of this wave: piece pc = w + 4 m = (patch row pc >> 1, half pc & 1)
     auto issue_t = [&](const TA &a, int s, int slot) __attribute__((always_inline)) {
         const uint32_t base = lds_base + slot * kSlotBytes;
-        const char *t = (const char *)(p.pt + (((size_t)(a.b * SS + s) * p.Hp + a.y0) * p.CB + (a.x0 >> 4)) * kRecU);
+        const char *t = (const char *)p.pt + (((size_t)(a.b * SS + s) * p.Hp + a.y0) * p.CB + (a.x0 >> 4)) * kRecU * 16;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             const int pc = w + 4 * m;
-            dma16s(sgpr_ptr(t + (pc >> 1) * trowB + (pc & 1) * 1024), lane * 16, base + pc * 1024);
+            dma16s(sgpr_ptr(t + (pc >> 1) * trowB + (pc & 1) * 1024), l16, base + pc * 1024);
         }
     };
     // A tile's exponents, one LDS-DMA dword per lane: waves 0, 1 the patch's 128 target
@@ -603,7 +686,7 @@ __global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p)
     };
 
     f32x4 acc[2][kPatchRows];
-    auto compute = [&]<int NR>(int tslot, int qslot) __attribute__((always_inline)) {
+    auto compute = [&](int tslot, int qslot) __attribute__((always_inline)) {
         const u32x4 *A = reinterpret_cast<const u32x4 *>(smem + tslot * kSlotBytes) + lane;
         half8 qh[2], ql[2];
 #pragma unroll
@@ -611,29 +694,25 @@ __global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p)
             qh[i] = __builtin_bit_cast(half8, qv[qslot][i][0]);
             ql[i] = __builtin_bit_cast(half8, qv[qslot][i][1]);
         }
-        half8 fh[2], fl[2];
-        fh[0] = __builtin_bit_cast(half8, A[0]);
-        fl[0] = __builtin_bit_cast(half8, A[64]);
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const int c = r & 1;
-            if (r + 1 < NR) {
-                fh[c ^ 1] = __builtin_bit_cast(half8, A[(2 * r + 2) * 64]);
-                fl[c ^ 1] = __builtin_bit_cast(half8, A[(2 * r + 3) * 64]);
+        for (int r = 0; r < kPatchRows; ++r) {
+            const half8 ah = __builtin_bit_cast(half8, A[(2 * r) * 64]);
+            const half8 al = __builtin_bit_cast(half8, A[(2 * r + 1) * 64]);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                acc[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, qh[i], acc[i][r], 0, 0, 0);
+                acc[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, ql[i], acc[i][r], 0, 0, 0);
+                acc[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, qh[i], acc[i][r], 0, 0, 0);
             }
-            // per accumulator the product order of the kernel above (lo_t hi_q, hi_t lo_q, hi_t hi_q)
-            acc[0][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl[c], qh[0], acc[0][r], 0, 0, 0);
-            acc[1][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fl[c], qh[1], acc[1][r], 0, 0, 0);
-            acc[0][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], ql[0], acc[0][r], 0, 0, 0);
-            acc[1][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], ql[1], acc[1][r], 0, 0, 0);
-            acc[0][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], qh[0], acc[0][r], 0, 0, 0);
-            acc[1][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fh[c], qh[1], acc[1][r], 0, 0, 0);
         }
     };
 
     // Epilogue: exactly kStoresPerTile buffer stores per wave.  Resources are per wave and
-    // level, based at the wave's first query row, sized to its valid queries.
-    auto epilogue = [&](const TA &a, int buf) __attribute__((always_inline)) {
+    // level, based at the wave's first query row, sized to its valid queries.  Every store
+    // offset is computed unconditionally and then replaced by kOOB where the lane has nothing
+    // to write (a select, never a branch).
+    auto epilogue = [&](const TA &a, int buf, int ln) __attribute__((always_inline)) {
+        const int ci = ln & 15, grp = ln >> 4;
         const int q0 = a.qb0 * 16;
         const int nq = min(max(NQ - q0, 0), 32);
         const size_t qrow0 = (size_t)a.b * NQ + q0;
@@ -642,87 +721,81 @@ __global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p)
         const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc(p.lvl[2] + qrow0 * N2, 0, nq * N2 * 4, 0x00020000);
         const __amdgpu_buffer_rsrc_t r3 = __builtin_amdgcn_make_buffer_rsrc(p.lvl[3] + qrow0 * N3, 0, nq * N3 * 4, 0x00020000);
         const int *etb = lds_et + buf * kExpInts;
-        int eqv[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) eqv[i] = etb[kPatchRows * 16 + (2 * w + i) * 16 + ci] + p.eshift;
-        int et[kPatchRows][4];
-#pragma unroll
-        for (int r = 0; r < kPatchRows; ++r) {
-            const int4 e4 = reinterpret_cast<const int4 *>(etb)[r * 4 + grp];
-            et[r][0] = e4.x, et[r][1] = e4.y, et[r][2] = e4.z, et[r][3] = e4.w;
-        }
         const int y0 = a.y0, x0 = a.x0, X0 = x0 + 4 * grp;
+        auto sel_off = [&](bool ok, uint32_t o) __attribute__((always_inline)) {
+            o = opq(o);
+            return opq(ok ? o : kOOB);
+        };
         float l2s[2][2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
+            const int eqv = etb[kPatchRows * 16 + (2 * w + i) * 16 + ci] + p.eshift;
             const int qq = i * 16 + ci;  // query row within the wave's resources
-            float v[kPatchRows][4];
-#pragma unroll
-            for (int r = 0; r < kPatchRows; ++r)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    float x = ldexpf(acc[i][r][g], eqv[i] + et[r][g]);
-                    if (!p.exact) x = x * p.inv_s;
-                    v[r][g] = x;
-                }
-            {
-                const uint32_t o = (uint32_t)(qq * N + y0 * W + X0) * 4u;
-                const bool xok = X0 < W;
-#pragma unroll
-                for (int r = 0; r < kPatchRows; ++r) {
-                    const bool ok = xok && y0 + r < H;
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{v[r][0], v[r][1], v[r][2], v[r][3]}),
-                                                           r0, opq(ok ? o + (uint32_t)(r * W * 4) : kOOB), 0, 0);
-                }
-            }
+            const uint32_t o0 = (uint32_t)(qq * N + y0 * W + X0) * 4u;
+            const bool xok = X0 < W;
             float l1[4][2];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                l1[r][0] = pool4(v[2 * r][0], v[2 * r][1], v[2 * r + 1][0], v[2 * r + 1][1]);
-                l1[r][1] = pool4(v[2 * r][2], v[2 * r][3], v[2 * r + 1][2], v[2 * r + 1][3]);
+            for (int r = 0; r < kPatchRows; ++r) {
+                const int4 e4 = reinterpret_cast<const int4 *>(etb)[r * 4 + grp];
+                const int et[4] = {e4.x, e4.y, e4.z, e4.w};
+                f32x4 v;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    float x = ldexpf(acc[i][r][g], eqv + et[g]);
+                    if (!p.exact) x = x * p.inv_s;
+                    v[g] = x;
+                }
+                acc[i][r] = v;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r0,
+                                                       sel_off(xok && y0 + r < H, o0 + (uint32_t)(r * W * 4)), 0, 0);
+                if (r & 1) {
+                    const f32x4 u = acc[i][r - 1];
+                    l1[r >> 1][0] = pool4(u[0], u[1], v[0], v[1]);
+                    l1[r >> 1][1] = pool4(u[2], u[3], v[2], v[3]);
+                }
             }
 #pragma unroll
             for (int r = 0; r < 2; ++r) l2s[i][r] = pool4(l1[2 * r][0], l1[2 * r][1], l1[2 * r + 1][0], l1[2 * r + 1][1]);
-            // Level 1 as 16-B stores: lanes grp 2m, 2m + 1 swap one row's column pair (see above).
+            // Level 1 as 16-B stores: lanes grp 2m, 2m + 1 swap one row's column pair (lanes 16
+            // apart), so that the even lane stores rows 0, 2 and the odd lane rows 1, 3.
             const bool odd = grp & 1;
             const int X1 = (x0 >> 1) + 4 * (grp >> 1);
 #pragma unroll
             for (int rp = 0; rp < 2; ++rp) {
-                const int ra = 2 * rp, rb = ra + 1, r = odd ? rb : ra;
+                const int ra = 2 * rp, rb = ra + 1;
                 const float g0 = __shfl_xor(odd ? l1[ra][0] : l1[rb][0], 16);
                 const float g1 = __shfl_xor(odd ? l1[ra][1] : l1[rb][1], 16);
-                const f32x4 o4 = odd ? f32x4{g0, g1, l1[rb][0], l1[rb][1]} : f32x4{l1[ra][0], l1[ra][1], g0, g1};
-                const int Y1 = (y0 >> 1) + r;
-                const bool ok = Y1 < H1 && X1 < W1;
+                const f32x4 o4 = f32x4{odd ? g0 : l1[ra][0], odd ? g1 : l1[ra][1], odd ? l1[rb][0] : g0, odd ? l1[rb][1] : g1};
+                const int Y1 = (y0 >> 1) + ra + (odd ? 1 : 0);
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o4), r1,
-                                                       opq(ok ? (uint32_t)(qq * N1 + Y1 * W1 + X1) * 4u : kOOB), 0, 0);
+                                                       sel_off(Y1 < H1 && X1 < W1, (uint32_t)(qq * N1 + Y1 * W1 + X1) * 4u), 0, 0);
             }
         }
         {  // Level 2 of both blocks in one store (lane g gathers row g & 1 of block g >> 1).
             const int bl = grp >> 1, rw = grp & 1;
-            // value k = 2 * block + row of this lane, by bit selects (no dynamic register index, no branch)
             auto sel = [&](int k) { return fsel(k & 2, fsel(k & 1, l2s[1][1], l2s[1][0]), fsel(k & 1, l2s[0][1], l2s[0][0])); };
             const float t0v = sel(grp);
             const float t1 = __shfl_xor(sel(grp ^ 1), 16), t2 = __shfl_xor(sel(grp ^ 2), 32), t3 = __shfl_xor(sel(grp ^ 3), 48);
             auto pick = [&](int k) { return fsel(k & 2, fsel(k & 1, t3, t2), fsel(k & 1, t1, t0v)); };
             const f32x4 o4 = f32x4{pick(grp), pick(grp ^ 1), pick(grp ^ 2), pick(grp ^ 3)};
             const int Y2 = (y0 >> 2) + rw, X2 = x0 >> 2;
-            const bool ok = Y2 < H2 && X2 < W2;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o4), r2,
-                                                   opq(ok ? (uint32_t)((bl * 16 + ci) * N2 + Y2 * W2 + X2) * 4u : kOOB), 0, 0);
+                                                   sel_off(Y2 < H2 && X2 < W2, (uint32_t)((bl * 16 + ci) * N2 + Y2 * W2 + X2) * 4u), 0, 0);
         }
-        {  // Level 3: even lanes pool block 0, odd lanes block 1.
+        {  // Level 3: even lanes pool block 0, odd lanes block 1, in ((a + b) + c) + d order.
             const int bl = grp & 1;
-            const float y0v = __shfl_xor(bl ? l2s[0][0] : l2s[1][0], 16), y1v = __shfl_xor(bl ? l2s[0][1] : l2s[1][1], 16);
-            const float l3 = bl == 0 ? pool4(l2s[0][0], y0v, l2s[0][1], y1v) : pool4(y0v, l2s[1][0], y1v, l2s[1][1]);
+            const float y0v = __shfl_xor(fsel(bl, l2s[0][0], l2s[1][0]), 16), y1v = __shfl_xor(fsel(bl, l2s[0][1], l2s[1][1]), 16);
+            const float a0 = fsel(bl, y0v, l2s[0][0]), a1 = fsel(bl, l2s[1][0], y0v);
+            const float a2 = fsel(bl, y1v, l2s[0][1]), a3 = fsel(bl, l2s[1][1], y1v);
+            const float l3 = pool4(a0, a1, a2, a3);
             const int Y3 = y0 >> 3, X3 = X0 >> 3;
-            const bool ok = Y3 < H3 && X3 < W3;
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, l3), r3,
-                                                  opq(ok ? (uint32_t)((bl * 16 + ci) * N3 + Y3 * W3 + X3) * 4u : kOOB), 0, 0);
+                                                  sel_off(Y3 < H3 && X3 < W3, (uint32_t)((bl * 16 + ci) * N3 + Y3 * W3 + X3) * 4u), 0, 0);
         }
     };
 
     // ---- prologue of the first tile ----
+    l16 = (uint32_t)lane * 16u;
     TA cur = tile_addr(0);
     issue_e(cur, 0);
     issue_q(cur, 0, 0);
@@ -732,8 +805,7 @@ __global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p)
     {
         // kStoresPerTile dropped stores (num_records 0): every tile, the first included, then
         // starts with the same memory operations in flight, so the vmcnt immediates of steps 0
-        // and 1 are one constant each, and so are the compiler's own waits for the query
-        // registers (its loop-header merge would otherwise fall back to the prologue's count).
+        // and 1 are one constant each.
         const __amdgpu_buffer_rsrc_t nul = __builtin_amdgcn_make_buffer_rsrc(p.lvl[0], 0, 0, 0x00020000);
 #pragma unroll
         for (int i = 0; i < kStoresPerTile; ++i) __builtin_amdgcn_raw_buffer_store_b32(0u, nul, opq(kOOB), 0, 0);
@@ -743,15 +815,20 @@ __global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p)
         // the tile whose first steps are prefetched at the end of this one (the last tile
         // prefetches itself: every group is issued, so every count below is a constant)
         const TA nxt = tile_addr(k + 1 < nmine ? k + 1 : k);
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        l16 = (uint32_t)ln * 16u;
+        if (k < 4) stamp(2 + 4 * k);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
             for (int r = 0; r < kPatchRows; ++r) acc[i][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const bool half = HALF && cur.y0 + kPatchRows / 2 >= p.H;  // tile-uniform
         auto step = [&]<int s>() __attribute__((always_inline)) {
             // wait for step s's target DMA (and everything older: its query loads, the exponents)
             if constexpr (s < 2) vm_wait_barrier<group_ops<SS>(s == 0 ? SS - 1 : 0) + kStoresPerTile>();
             else vm_wait_barrier<group_ops<SS>(s - 1)>();
+            if constexpr (s == 0)
+                if (k < 4) stamp(3 + 4 * k);
             const int qs = s & 3;
             asm volatile("" : "+v"(qv[qs][0][0]), "+v"(qv[qs][0][1]), "+v"(qv[qs][1][0]), "+v"(qv[qs][1][1]));
             if constexpr (s == SS - 2) issue_e(nxt, (k + 1) & 1);
@@ -763,21 +840,31 @@ __global__ __launch_bounds__(256, 2) void corr_build_persist_kernel(BuildArgs p)
                 issue_q(nxt, s + 2 - SS, (s + 2) & 3);
                 issue_t(nxt, s + 2 - SS, sl);
             }
-            // only the MFMAs branch (the memory operations above are common to both arms, so no
-            // register of an in-flight load meets a control-flow join)
-            if (half) compute.template operator()<kPatchRows / 2>((rs0 + s) % kRing, qs);
-            else compute.template operator()<kPatchRows>((rs0 + s) % kRing, qs);
+            compute((rs0 + s) % kRing, qs);
         };
         [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
             (step.template operator()<S>(), ...);
         }(std::make_integer_sequence<int, SS>{});
-        epilogue(cur, k & 1);
+        if (k < 4) stamp(4 + 4 * k);
+        epilogue(cur, k & 1, ln);
+        if (k < 4) stamp(5 + 4 * k);
         cur = nxt;
         rs0 = (rs0 + SS) % kRing;
     }
     // the last tile's self-prefetch is still landing in LDS: drain it before the workgroup's
     // LDS can be handed to another workgroup
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (STAMP) {
+        unsigned long long rt;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt)::"memory");
+        if (w == 0 && lane == 0) {
+            stv[1] = rt;
+            stv[18] = nmine | ((unsigned long long)blockIdx.x << 32);
+            stv[19] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (w == 0 && lane < 20) p.stamp[(size_t)blockIdx.x * 20 + lane] = stv[lane];
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -851,11 +938,26 @@ hipError_t launch_split_pack(const float *f1, int NQ, const float *f2, int B, in
     }
 }
 
+// One instantiation of the one-tile-per-workgroup kernel, its dynamic-LDS limit raised once.
+template <int SS, int QS, bool PIPE>
+hipError_t launch_build_kernel(dim3 grid, const BuildArgs &p, hipStream_t s) {
+    static std::atomic<unsigned long long> lds_done{0};
+    const hipError_t e = ensure_lds_limit((const void *)corr_build_split_kernel<SS, QS, PIPE>, kBuildLds, lds_done);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((corr_build_split_kernel<SS, QS, PIPE>), grid, dim3(256), kBuildLds, s, p);
+    return hipGetLastError();
+}
+
 // The MFMA part (operands already packed in ws).  levels == 0: the MFMAs and epilogue
 // arithmetic without stores (measurement).  cons = false: levels 1-2 as element stores (the
 // previous epilogue, kept for the A/B; same bits).
+// Tile order of the build (BuildArgs::order): 1 = a patch row's patches consecutive for one
+// query group (the default: 1280x960 1006 -> 948 us, DSEC / train / MVSEC 1-4 % faster,
+// profiles/r03b_kbench_build_order.txt); tools/kbench_build.hip overrides it for the A/B.
+int g_tile_order = 1;
+
 hipError_t launch_split_mfma(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
-                             hipStream_t s, bool cons = true) {
+                             hipStream_t s, bool cons = true, int variant = 0) {
     const SplitGeom g = split_geom(D, NQ, H, W);
     const SplitWs w = split_ws(ws, B, g);
     BuildArgs p{};
@@ -877,37 +979,38 @@ hipError_t launch_split_mfma(int NQ, int B, int D, int H, int W, int levels, con
     p.mode0 = p.nlev > 0 ? store_mode(W, pyr.p[0]) : 0;
     p.mode1 = p.nlev > 1 ? store_mode(W >> 1, pyr.p[1]) : 0;
     p.cons = cons && p.mode1 == 2 && (p.nlev <= 2 || store_mode(W >> 2, pyr.p[2]) == 2);
+    p.order = g_tile_order;
     const long tiles = (long)B * p.npatch * g.NQG;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
-    hipError_t e;
-    static std::atomic<unsigned long long> lds_done[9];
+    const dim3 grid((unsigned)tiles);
     const int ss = g.S <= 8 ? g.S : 0;
-    const void *fns[9] = {
-        (const void *)corr_build_split_kernel<0>, (const void *)corr_build_split_kernel<1>,
-        (const void *)corr_build_split_kernel<2>, (const void *)corr_build_split_kernel<3>,
-        (const void *)corr_build_split_kernel<4>, (const void *)corr_build_split_kernel<5>,
-        (const void *)corr_build_split_kernel<6>, (const void *)corr_build_split_kernel<7>,
-        (const void *)corr_build_split_kernel<8>};
-    e = ensure_lds_limit(fns[ss], kBuildLds, lds_done[ss]);
-    if (e != hipSuccess) return e;
-    const dim3 grid((unsigned)tiles), blk(256);
-    switch (ss) {
+    hipError_t e;
+    if (variant != 0 && ss == 8) {
+        switch (variant) {
+            case 1: e = launch_build_kernel<8, 4, false>(grid, p, s); break;
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (ss) {
 #define CORR_BUILD_CASE(c) \
-    case c: hipLaunchKernelGGL((corr_build_split_kernel<c>), grid, blk, kBuildLds, s, p); break;
-        CORR_BUILD_CASE(0) CORR_BUILD_CASE(1) CORR_BUILD_CASE(2) CORR_BUILD_CASE(3) CORR_BUILD_CASE(4)
-        CORR_BUILD_CASE(5) CORR_BUILD_CASE(6) CORR_BUILD_CASE(7) CORR_BUILD_CASE(8)
+    case c: e = launch_build_kernel<c, 4, true>(grid, p, s); break;
+            CORR_BUILD_CASE(0) CORR_BUILD_CASE(1) CORR_BUILD_CASE(2) CORR_BUILD_CASE(3) CORR_BUILD_CASE(4)
+            CORR_BUILD_CASE(5) CORR_BUILD_CASE(6) CORR_BUILD_CASE(7) CORR_BUILD_CASE(8)
 #undef CORR_BUILD_CASE
+            default: return hipErrorInvalidValue;
+        }
     }
+    if (e != hipSuccess) return e;
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (levels > kFusedLevels) return launch_pool_levels(pyr, kFusedLevels, levels, (long)B * NQ, H, W, s);
     return hipSuccess;
 }
 
-// Resident workgroups of the persistent kernel per device: CUs x blocks per CU (occupancy API),
+// Resident workgroups of the streaming kernel per device: CUs x blocks per CU (occupancy API),
 // rounded down to a multiple of 8 (one share per XCD).
 template <int SS>
-int persist_slots() {
+int stream_slots() {
     static std::atomic<int> cache[64];
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
@@ -916,7 +1019,7 @@ int persist_slots() {
     if (v > 0) return v;
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)corr_build_persist_kernel<SS, true>, 256, kBuildLdsP) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)corr_build_stream_kernel<SS, false>, 256, kBuildLdsP) !=
         hipSuccess)
         return 0;
     v = cus * std::max(per, 1) / 8 * 8;
@@ -924,21 +1027,21 @@ int persist_slots() {
     return v;
 }
 
-// The persistent form applies: S in {4, 8}, >= 4 levels, levels 0-2 as 16-B runs.
-bool persist_applies(int S, int levels, int mode0, int cons) {
+// The streaming form applies: S in {4, 8}, >= 4 levels, levels 0-2 stored as 16-B runs.
+bool stream_applies(int S, int levels, int mode0, int cons) {
     return (S == 4 || S == 8) && levels >= kFusedLevels && mode0 == 2 && cons;
 }
 
-constexpr int kPersistDefault = 0;  // the library's choice (measured in tools/kbench_build.hip)
+constexpr int kStreamDefault = 0;  // the library's choice (measured in tools/kbench_build.hip)
 
-// persist: 1 = persistent kernel where it applies, 0 = the one-tile-per-workgroup
-// kernel.  slots > 0 overrides the resident-workgroup count (measurement).
-hipError_t launch_split_mfma_p(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
-                               hipStream_t s, int persist = 1, int slots = 0, bool half = true) {
+// stream: 1 = the streaming kernel where it applies, 0 = the one-tile-per-workgroup kernel.
+// slots > 0 overrides the resident-workgroup count; stamp: diagnostic build (measurement).
+hipError_t launch_split_mfma_s(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
+                               hipStream_t s, int stream = 1, int slots = 0, unsigned long long *stamp = nullptr) {
     const SplitGeom g = split_geom(D, NQ, H, W);
     const int mode0 = store_mode(W, pyr.p[0]);
     const int cons = levels > 2 && store_mode(W >> 1, pyr.p[1]) == 2 && store_mode(W >> 2, pyr.p[2]) == 2;
-    if (!persist || !persist_applies(g.S, levels, mode0, cons))
+    if (!stream || !stream_applies(g.S, levels, mode0, cons))
         return launch_split_mfma(NQ, B, D, H, W, levels, pyr, ws, s);
     const SplitWs w = split_ws(ws, B, g);
     BuildArgs p{};
@@ -958,24 +1061,27 @@ hipError_t launch_split_mfma_p(int NQ, int B, int D, int H, int W, int levels, c
         p.eshift = e - 1;
     }
     p.mode0 = 2, p.mode1 = 2, p.cons = 1;
+    p.stamp = stamp;
+    p.order = g_tile_order;
     const long tiles = (long)B * p.npatch * g.NQG;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
     p.ntiles = (int)tiles;
     static std::atomic<unsigned long long> lds_done[4];
-    const int ki = (g.S == 4 ? 0 : 2) + (half ? 0 : 1);
-    const void *fns[4] = {(const void *)corr_build_persist_kernel<4, true>, (const void *)corr_build_persist_kernel<4, false>,
-                          (const void *)corr_build_persist_kernel<8, true>, (const void *)corr_build_persist_kernel<8, false>};
-    hipError_t e = ensure_lds_limit(fns[ki], kBuildLdsP, lds_done[ki]);
+    const int ki = (g.S == 4 ? 0 : 2) + (stamp ? 1 : 0);
+    const void *fns[4] = {(const void *)corr_build_stream_kernel<4, false>, (const void *)corr_build_stream_kernel<4, true>,
+                          (const void *)corr_build_stream_kernel<8, false>, (const void *)corr_build_stream_kernel<8, true>};
+    const int lds = kBuildLdsP + (stamp ? 160 : 0);
+    hipError_t e = ensure_lds_limit(fns[ki], lds, lds_done[ki]);
     if (e != hipSuccess) return e;
-    int P = slots > 0 ? slots / 8 * 8 : (g.S == 4 ? persist_slots<4>() : persist_slots<8>());
+    int P = slots > 0 ? slots / 8 * 8 : (g.S == 4 ? stream_slots<4>() : stream_slots<8>());
     if (P <= 0) return hipErrorInvalidValue;
     P = (int)std::min<long>(P, (tiles + 7) / 8 * 8);
     const dim3 grid((unsigned)P), blk(256);
     switch (ki) {
-        case 0: hipLaunchKernelGGL((corr_build_persist_kernel<4, true>), grid, blk, kBuildLdsP, s, p); break;
-        case 1: hipLaunchKernelGGL((corr_build_persist_kernel<4, false>), grid, blk, kBuildLdsP, s, p); break;
-        case 2: hipLaunchKernelGGL((corr_build_persist_kernel<8, true>), grid, blk, kBuildLdsP, s, p); break;
-        default: hipLaunchKernelGGL((corr_build_persist_kernel<8, false>), grid, blk, kBuildLdsP, s, p); break;
+        case 0: hipLaunchKernelGGL((corr_build_stream_kernel<4, false>), grid, blk, lds, s, p); break;
+        case 1: hipLaunchKernelGGL((corr_build_stream_kernel<4, true>), grid, blk, lds, s, p); break;
+        case 2: hipLaunchKernelGGL((corr_build_stream_kernel<8, false>), grid, blk, lds, s, p); break;
+        default: hipLaunchKernelGGL((corr_build_stream_kernel<8, true>), grid, blk, lds, s, p); break;
     }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -983,11 +1089,15 @@ hipError_t launch_split_mfma_p(int NQ, int B, int D, int H, int W, int levels, c
     return hipSuccess;
 }
 
+// part: 0 = pack + MFMA; 1 = the pack alone; 2 = the MFMA kernel alone (measurement: the
+// workspace must already hold this pair's pack).
 hipError_t launch_build_split(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, int levels,
-                              const LevelPtrs &pyr, void *ws, hipStream_t s) {
-    hipError_t e = launch_split_pack(f1, NQ, f2, B, D, H, W, ws, s);
-    if (e != hipSuccess) return e;
-    return launch_split_mfma_p(NQ, B, D, H, W, levels, pyr, ws, s, kPersistDefault);
+                              const LevelPtrs &pyr, void *ws, hipStream_t s, int part) {
+    if (part != 2) {
+        const hipError_t e = launch_split_pack(f1, NQ, f2, B, D, H, W, ws, s);
+        if (e != hipSuccess || part == 1) return e;
+    }
+    return launch_split_mfma_s(NQ, B, D, H, W, levels, pyr, ws, s, kStreamDefault);
 }
 
 }  // namespace corr

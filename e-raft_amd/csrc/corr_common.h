@@ -61,7 +61,7 @@ hipError_t launch_backward(int algo, const float *const *coords, const float *co
 size_t build_split_workspace(int B, int D, int NQ, int H, int W);
 bool build_split_supported(int D);
 hipError_t launch_build_split(const float *f1, int NQ, const float *f2, int B, int D, int H, int W,
-                              int levels, const LevelPtrs &pyr, void *ws, hipStream_t s);
+                              int levels, const LevelPtrs &pyr, void *ws, hipStream_t s, int part = 0);
 size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W);
 hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, const float *f2, int B, int D, int H,
                                   int W, float *df1, float *df2, void *ws, hipStream_t s);

@@ -37,6 +37,8 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
 # selects the fp32-operand MFMA build instead.
 BUILD_FP32 = 0
 BUILD_F16X3 = 1
+BUILD_ONLY_PACK = 0x100  # measurement: OR into BUILD_F16X3 to run only the operand pack
+BUILD_ONLY_MFMA = 0x200  # ... or only the MFMA kernel (the workspace holds this pair's pack)
 _ALGOS = {"fp32": BUILD_FP32, "f16x3": BUILD_F16X3}
 
 
@@ -180,7 +182,7 @@ def build(fmap1, fmap2, levels, algo=None, workspace=None):
     B, D, H, W = fmap2.shape
     a, b, pp = _dev(fmap1, "fmap1"), _dev(fmap2, "fmap2"), _ptrs(levels, "pyr")
     if workspace is None:
-        workspace = build_workspace(fmap1, fmap2, algo)
+        workspace = build_workspace(fmap1, fmap2, algo & 0xff)
     wp = 0 if workspace is None else workspace.data_ptr()
     wn = 0 if workspace is None else workspace.numel() * workspace.element_size()
     with torch.cuda.device(fmap1.device):

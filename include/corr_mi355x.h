@@ -72,6 +72,11 @@ int corr_build(const float *fmap1, const float *fmap2, int B, int D, int H, int 
  */
 #define CORR_BUILD_FP32 0
 #define CORR_BUILD_F16X3 1
+/* Measurement only (OR-ed into CORR_BUILD_F16X3): run just one of its two kernels — the
+ * operand pack, or the MFMA build from a workspace that already holds this pair's pack — so a
+ * benchmark can time each kernel on its own.  The pyramid is complete only after both. */
+#define CORR_BUILD_ONLY_PACK 0x100
+#define CORR_BUILD_ONLY_MFMA 0x200
 
 /* Bytes of device workspace corr_build_ex(algo, ...) needs (0 for CORR_BUILD_FP32;
  * (size_t)-1 if the algorithm does not support D). */

@@ -126,23 +126,26 @@ int main(int argc, char **argv) {
         vs.push_back({"x3 pack only", [&](float *) {
                           return launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0);
                       }, false});
-        vs.push_back({"x3 mfma persist", [&](float *o) {
-                          return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1);
-                      }, false});
-        vs.push_back({"x3 mfma persist nohalf", [&](float *o) {
-                          return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 0, false);
-                      }, false});
-        vs.push_back({"x3 mfma persist 2/CU", [&](float *o) {
-                          return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 512);
-                      }, false});
-        vs.push_back({"x3 mfma persist 1/CU", [&](float *o) {
-                          return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 256);
-                      }, false});
-        vs.push_back({"x3 mfma 1-tile", [&](float *o) {
-                          return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
+        auto with_order = [&](int ord, std::function<hipError_t()> f) {
+            g_tile_order = ord;
+            const hipError_t e = f();
+            g_tile_order = 1;
+            return e;
+        };
+        vs.push_back({"x3 mfma 1-tile order0", [&](float *o) {
+                          return with_order(0, [&] { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
                       }, false});
         vs.push_back({"x3 mfma 1-tile NOSTORE", [&](float *o) {
                           return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), ws, 0);
+                      }, false});
+        vs.push_back({"x3 mfma 1-tile order1", [&](float *o) {
+                          return with_order(1, [&] { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
+                      }, false});
+        vs.push_back({"x3 mfma 1-tile nopipe (206 VGPR)", [&](float *o) {
+                          return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 1);
+                      }, false});
+        vs.push_back({"x3 mfma stream", [&](float *o) {
+                          return launch_split_mfma_s(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1);
                       }, false});
         for (float sc : {1.0f, 1e-3f, 300.0f}) {
             hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f1, fe, 1u, sc);
@@ -182,10 +185,13 @@ int main(int argc, char **argv) {
                        bad ? "DIFFER" : "bit-identical", bad);
             };
             same("16-B level 1/2 stores", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
-            same("persistent", [&](float *o) { return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1); });
-            same("persistent 2/CU", [&](float *o) { return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 512); });
-            same("persistent 1/CU", [&](float *o) { return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 256); });
-            same("persistent nohalf", [&](float *o) { return launch_split_mfma_p(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 0, false); });
+            same("1-tile order0", [&](float *o) {
+                return with_order(0, [&] { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
+            });
+            same("1-tile nopipe", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 1); });
+            same("stream", [&](float *o) { return launch_split_mfma_s(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1); });
+
+            same("stream 1/CU", [&](float *o) { return launch_split_mfma_s(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 256); });
         }
         {  // pooling of the new kernel: every level bit-identical to avg_pool2d of its own level 0
             CK(launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), ws, 0));
@@ -206,6 +212,68 @@ int main(int argc, char **argv) {
             }
             printf("%-10s pooling levels 1-3 vs own level 0: %s (%zu mismatches)\n", sh.name,
                    bad ? "DIFFER" : "bit-identical", bad);
+        }
+        if (vfilter && !strcmp(vfilter, "stamp")) {  // diagnostic: per-tile clock stamps of the streaming kernel
+            {  // the streaming kernel: per tile (first 4) start, after step 0, after the loop, after the epilogue
+                const int P = stream_slots<8>();
+                unsigned long long *ss;
+                CK(hipMalloc(&ss, (size_t)P * 20 * 8));
+                CK(hipMemset(ss, 0, (size_t)P * 20 * 8));
+                for (int i = 0; i < 20; ++i) CK(launch_split_mfma_s(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), ws, 0, 1, 0, ss));
+                CK(hipDeviceSynchronize());
+                std::vector<unsigned long long> h((size_t)P * 20);
+                CK(hipMemcpy(h.data(), ss, h.size() * 8, hipMemcpyDeviceToHost));
+                unsigned long long r0 = ~0ull, r1 = 0;
+                double dm = 0, dr = 0;
+                int nwg = 0;
+                double ph[4][4] = {}, tl[4] = {};
+                int nt[4] = {}, hist[8] = {};
+                for (int j = 0; j < P; ++j) {
+                    const unsigned long long *o = &h[(size_t)j * 20];
+                    if (!o[0]) continue;
+                    ++nwg;
+                    r0 = std::min(r0, o[0]), r1 = std::max(r1, o[1]);
+                    const int nm = (int)(o[18] & 0xffffffff);
+                    ++hist[std::min(nm, 7)];
+                    const int kl = std::min(nm, 4) - 1;
+                    dm += (double)(o[5 + 4 * kl] - o[2]), dr += (double)(o[1] - o[0]);
+                    for (int k = 0; k < std::min(nm, 4); ++k) {
+                        const unsigned long long *t = o + 2 + 4 * k;
+                        ph[k][0] += (double)(t[1] - t[0]);
+                        ph[k][1] += (double)(t[2] - t[1]);
+                        ph[k][2] += (double)(t[3] - t[2]);
+                        if (k + 1 < std::min(nm, 4)) ph[k][3] += (double)(t[4] - t[3]);
+                        ++nt[k];
+                        tl[k] += (double)(t[3] - t[0]);
+                    }
+                }
+                {  // which blocks share a CU (HW_ID bits 15:8), first 6 CUs
+                    std::vector<std::vector<int>> cu(256);
+                    for (int j = 0; j < P; ++j) {
+                        const unsigned long long *o = &h[(size_t)j * 20];
+                        if (o[0]) cu[(o[19] >> 8) & 0xff].push_back((int)(o[18] >> 32));
+                    }
+                    printf("%-10s co-resident blocks:", sh.name);
+                    for (int c = 0, shown = 0; c < 256 && shown < 8; ++c)
+                        if (!cu[c].empty()) {
+                            printf(" [");
+                            for (int b : cu[c]) printf(" %d", b);
+                            printf(" ]");
+                            ++shown;
+                        }
+                    printf("\n");
+                }
+                const double clk = dm / dr * 100.0;
+                printf("%-10s stream stamp: %d WGs, clock ~%.0f MHz (memtime/realtime over the stamped part), span %.2f us; tiles/WG:", sh.name, nwg, clk,
+                       (r1 - r0) / 100.0);
+                for (int k = 0; k < 8; ++k)
+                    if (hist[k]) printf(" %d:%d", k, hist[k]);
+                printf("\n   tile   n   to-step0-barrier  K-loop  epilogue  (cycles)\n");
+                for (int k = 0; k < 4; ++k)
+                    if (nt[k]) printf("   %d %5d %10.0f %10.0f %8.0f\n", k, nt[k], ph[k][0] / nt[k], ph[k][1] / nt[k], ph[k][2] / nt[k]);
+                CK(hipFree(ss));
+            }
+            vfilter = "x3 mfma";
         }
         if (vfilter) {
             std::vector<Variant> keep;
