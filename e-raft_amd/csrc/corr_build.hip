@@ -43,7 +43,7 @@ struct BuildCfg {
 };
 
 // Default geometry (selected by tools/kbench_build.hip measurements).
-using BuildDefault = BuildCfg<2, 2, 2, 8, 4, true, false>;
+using BuildDefault = BuildCfg<2, 2, 2, 8, 4, true, true>;
 
 struct BuildParams {
     const float *f1;

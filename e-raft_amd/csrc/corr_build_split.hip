@@ -394,7 +394,8 @@ __device__ __forceinline__ void build_tile(const BuildArgs &p, const Tile tl) {
 
     if constexpr (SS > 0) {
         constexpr int QD = QS - 1;  // query prefetch distance (>= 2: Q(s) is issued before T(s))
-        // prologue: Q0 Q1 T0 [Q2] T1
+        // prologue: Q0 Q1 T0 [Q2] T1 (Q0 T0 Q1 T1 Q2 with the query loads hidden from the
+        // compiler's vmcnt accounting measured no faster: profiles/r03c_kbench_build_early_dropped.txt)
         issue_q(0, 0);
         if (SS > 1) issue_q(1, 1);
         issue_t(0, 0);

@@ -36,6 +36,14 @@ __global__ void fill_coords(float *c, int B, int H, int W, unsigned seed) {
     }
 }
 
+__global__ void fill_grid(float *c, int B, int H, int W) {  // the integer pixel grid (cold start)
+    const int N = H * W;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B * 2 * N; i += gridDim.x * blockDim.x) {
+        const int n = i % N, axis = (i / N) % 2;
+        c[i] = axis == 0 ? (float)(n % W) : (float)(n / W);
+    }
+}
+
 __global__ void fill(float *p, size_t n, unsigned seed) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         unsigned x = (unsigned)i * 2654435761u ^ seed;
@@ -76,15 +84,21 @@ int main(int argc, char **argv) {
         std::function<void()> run;
         std::vector<float> us;
     };
-    auto launch = [&](auto kern, int t_count) {
+    float *cgrid;
+    CK(hipMalloc(&cgrid, (size_t)B * 2 * N * 4));
+    hipLaunchKernelGGL(fill_grid, dim3(256), dim3(256), 0, 0, cgrid, B, H, W);
+    auto launch = [&](auto kern, int t_count, bool grid0 = false) {
         BwdLookups l2 = lk;
         l2.T = t_count;
+        if (grid0) l2.coords[0] = cgrid;
         CK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
         hipLaunchKernelGGL(kern, dim3((unsigned)(G * B)), dim3(64 * kFusedLv), bytes, 0, l2, o);
     };
     std::vector<V> vs;
     vs.push_back({"full T=12", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12); }, {}});
     vs.push_back({"full T=1", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 1); }, {}});
+    vs.push_back({"full T=12, lookup 0 on the integer grid", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12, true); }, {}});
+    vs.push_back({"full T=1 on the integer grid", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 1, true); }, {}});
     vs.push_back({"no lookups (zero + fold)", [&] { launch(lookup_bwd_fold_kernel<S, 1>, 12); }, {}});
     vs.push_back({"no fold T=12", [&] { launch(lookup_bwd_fold_kernel<S, 2>, 12); }, {}});
     vs.push_back({"zero-init only", [&] { launch(lookup_bwd_fold_kernel<S, 3>, 12); }, {}});
@@ -107,7 +121,7 @@ int main(int argc, char **argv) {
         }
     for (auto &v : vs) {
         std::sort(v.us.begin(), v.us.end());
-        printf("%-28s median %8.2f us  min %8.2f us\n", v.name.c_str(), v.us[v.us.size() / 2], v.us[0]);
+        printf("%-42s median %8.2f us  min %8.2f us\n", v.name.c_str(), v.us[v.us.size() / 2], v.us[0]);
     }
     return 0;
 }
