@@ -181,8 +181,6 @@ struct BuildArgs {
     int mode0, mode1;  // store width of levels 0 / 1: 2 = 16 B, 1 = 8 B, 0 = elements
     int cons;          // levels 1 and 2 as 16-B stores (W/2, W/4 multiples of 4, 16-B aligned bases)
     float inv_s;     // 1/sqrt(D) otherwise (multiplied: within tolerance, not bitwise)
-    int ntiles;      // persistent kernel: B * npatch * NQG
-    unsigned long long *stamp;  // diagnostic build only (STAMP): per-workgroup clock stamps
     int order;       // tile order: 0 = query group fastest (groups of kGroupQ), 1 = patch column fastest
 };
 
@@ -538,337 +536,6 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Streaming (persistent) form.  Same tiles, same arithmetic and the same bits as the kernel
-// above; what changes is the schedule:
-//   * a workgroup stays resident (three per CU, <= 168 VGPRs) and walks a list of tiles (its
-//     XCD's contiguous share of the tile order, every P8-th tile); the operand stream never
-//     stops at a tile boundary: the last two K steps of tile k already issue the query loads
-//     and target DMA of tile k+1's first two steps, so only the first tile waits out a cold
-//     prologue;
-//   * the epilogue's pyramid stores are issued AFTER those loads and are never waited for at
-//     the tile boundary: tile k+1's first two barriers count them among the younger memory
-//     operations, so the stores drain while tile k+1's first MFMAs run, and co-resident
-//     workgroups, which the store path serves one after the other, fall out of step: one's
-//     store phase meets another's MFMA phase;
-//   * every wave issues exactly kStoresPerTile store instructions per tile (buffer stores; a
-//     lane with nothing to write gets an out-of-range offset, which the hardware drops), so
-//     the hand-counted vmcnt immediates are exact.  No store is skipped by a branch.
-// ---------------------------------------------------------------------------------------
-constexpr int kExpInts = kPatchRows * 16 + kQPerWG;  // a tile's exponents: targets, then queries
-constexpr int kBuildLdsP = kRing * kSlotBytes + 2 * kExpInts * 4;  // exponents double-buffered
-constexpr int kStoresPerTile = 22;  // per wave: level 0 16, level 1 4, level 2 1, level 3 1
-constexpr uint32_t kOOB = 0x7ffffff0u;  // a buffer offset beyond every num_records (dropped store)
-
-__device__ __forceinline__ const void *sgpr_ptr(const void *p) {
-    const uint64_t v = (uint64_t)p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return (const void *)(((uint64_t)hi << 32) | lo);
-}
-
-template <int N>
-__device__ __forceinline__ void vm_wait_barrier() {
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
-}
-
-// One LDS-DMA piece with a wave-uniform (SGPR) source base: 16 B per lane from base + voff.
-__device__ __forceinline__ void dma16s(const void *base, uint32_t voff, uint32_t lds) {
-    asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(base), "{m0}"(lds) : "memory");
-}
-
-// Group(s') = the vector-memory operations a wave issues at step s': [1 at s' = SS-2: the next
-// tile's exponent DMA] + 4 query loads + 4 DMA pieces of flat step s'+2 (this tile's or the
-// next one's; the last tile prefetches itself again, so every group is issued).  At step s's
-// barrier the operations younger than step s's DMA (the last issue of Group(s-2)) are
-// Group(s-1), and at steps 0 and 1 also the previous tile's kStoresPerTile stores.
-template <int SS>
-__host__ __device__ constexpr int group_ops(int s) {
-    return (s == SS - 2 ? 1 : 0) + 8;
-}
-
-template <int SS, bool STAMP = false>
-__global__ __launch_bounds__(256, 3) void corr_build_stream_kernel(BuildArgs p) {
-    static_assert(SS == 4 || SS == 8, "query register slots and ring slots assume SS % 4 == 0, SS >= 4");
-    extern __shared__ __attribute__((aligned(16))) char smem_build[];
-    char *smem = smem_build;
-    int *lds_et = reinterpret_cast<int *>(smem + kRing * kSlotBytes);  // [2][kExpInts]
-    const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_void_t *)smem;
-    const uint32_t lds_et_base = (uint32_t)(uintptr_t)(lds_void_t *)lds_et;
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-
-    // This workgroup's tiles: XCD x (= blockIdx % 8 under round-robin dispatch; speed only)
-    // owns a contiguous range of the tile order, and its P8 workgroups deal it out.
-    const int xcd = blockIdx.x & 7, jj = blockIdx.x >> 3, P8 = gridDim.x >> 3;
-    const int T = p.ntiles, qT = T >> 3, rT = T & 7;
-    const int t0 = xcd < rT ? xcd * (qT + 1) : rT * (qT + 1) + (xcd - rT) * qT;
-    const int len = qT + (xcd < rT ? 1 : 0);
-    const int nmine = jj < len ? (len - 1 - jj) / P8 + 1 : 0;
-    if (nmine == 0) return;
-
-    // STAMP (kbench diagnostic build only): wave 0 records s_memtime per tile (first 4 tiles):
-    // tile start, after step 0's barrier, after the K loop, after the epilogue; and realtime at
-    // the kernel start and end, into p.stamp (nothing reads it).
-    // (kept in LDS, past the exponents, so that no stamp is a vector-memory operation)
-    unsigned long long *stv = reinterpret_cast<unsigned long long *>(smem + kBuildLdsP);
-    auto stamp = [&](int i) __attribute__((always_inline)) {
-        if constexpr (STAMP) {
-            unsigned long long t;
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-            __builtin_amdgcn_sched_barrier(0);
-            if (w == 0 && lane == 0) stv[i] = t;
-        }
-    };
-    if constexpr (STAMP) {
-        unsigned long long rt;
-        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt)::"memory");
-        if (w == 0 && lane < 20) stv[lane] = lane == 0 ? rt : 0;
-    }
-
-    const int H = p.H, W = p.W, N = p.N, NQ = p.NQ;
-    const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
-    const int N1 = H1 * W1, N2 = H2 * W2, N3 = H3 * W3;
-    const size_t trowB = (size_t)p.CB * kRecU * 16;  // bytes per patch row of the target image
-    const size_t qstepB = (size_t)p.NQB * kRecU * 16;  // bytes per K step of the query image
-
-    struct TA {
-        int b, y0, x0, qb0;
-    };
-    auto tile_addr = [&](int k) __attribute__((always_inline)) {
-        const Tile tl = tile_of(p, t0 + jj + k * P8);
-        return TA{__builtin_amdgcn_readfirstlane(tl.b), __builtin_amdgcn_readfirstlane(tl.py * kPatchRows),
-                  __builtin_amdgcn_readfirstlane(tl.cb * 16),
-                  __builtin_amdgcn_readfirstlane(tl.qg * (kQPerWG / 16) + 2 * w)};
-    };
-
-    u32x4 qv[4][2][2];  // [register slot][query block][hi, lo]
-    // lane * 16, recomputed inside the tile loop from an opaque copy (so that no lane-dependent
-    // value is hoisted out of the loop and held, or spilled, across it)
-    uint32_t l16;
-    // the query image as one buffer resource (wave-uniform base, per-lane offset l16)
-    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void *)p.pq, 0, (int)((size_t)p.B * SS * qstepB), 0x00020000);
-    auto issue_q = [&](const TA &a, int s, int slot) __attribute__((always_inline)) {
-        const int so = __builtin_amdgcn_readfirstlane((int)(((a.b * SS + s) * p.NQB + a.qb0) * kRecU * 16));
-        qv[slot][0][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, l16, so, 0));
-        qv[slot][0][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, l16 + 1024, so, 0));
-        qv[slot][1][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, l16 + 2048, so, 0));
-        qv[slot][1][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, l16 + 3072, so, 0));
-    };
-    // the 4 DMA pieces of this wave: piece pc = w + 4 m = (patch row pc >> 1, half pc & 1)
-    auto issue_t = [&](const TA &a, int s, int slot) __attribute__((always_inline)) {
-        const uint32_t base = lds_base + slot * kSlotBytes;
-        const char *t = (const char *)p.pt + (((size_t)(a.b * SS + s) * p.Hp + a.y0) * p.CB + (a.x0 >> 4)) * kRecU * 16;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int pc = w + 4 * m;
-            dma16s(sgpr_ptr(t + (pc >> 1) * trowB + (pc & 1) * 1024), l16, base + pc * 1024);
-        }
-    };
-    // A tile's exponents, one LDS-DMA dword per lane: waves 0, 1 the patch's 128 target
-    // exponents, waves 2, 3 the workgroup's 128 query exponents.
-    auto issue_e = [&](const TA &a, int buf) __attribute__((always_inline)) {
-        const int idx = (w & 1) * 64 + lane;
-        const int *src = w < 2 ? p.et + ((size_t)a.b * p.Hp + a.y0 + (idx >> 4)) * p.Wp + a.x0 + (idx & 15)
-                               : p.eq + (size_t)a.b * p.NQp + (a.qb0 - 2 * w) * 16 + idx;
-        dma4(src, lds_et_base + buf * (kExpInts * 4) + w * 256);
-    };
-    // c ? a : b without control flow
-    auto fsel = [](int c, float a, float b) __attribute__((always_inline)) {
-        const uint32_t m = c ? 0xffffffffu : 0u;
-        return __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, a) & m) | (__builtin_bit_cast(uint32_t, b) & ~m));
-    };
-    // A store's offset, opaque to the compiler: it must not split the store into one per value
-    // (that would make the number of issued stores data-dependent).
-    auto opq = [](uint32_t o) __attribute__((always_inline)) {
-        asm volatile("" : "+v"(o));
-        return o;
-    };
-
-    f32x4 acc[2][kPatchRows];
-    auto compute = [&](int tslot, int qslot) __attribute__((always_inline)) {
-        const u32x4 *A = reinterpret_cast<const u32x4 *>(smem + tslot * kSlotBytes) + lane;
-        half8 qh[2], ql[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            qh[i] = __builtin_bit_cast(half8, qv[qslot][i][0]);
-            ql[i] = __builtin_bit_cast(half8, qv[qslot][i][1]);
-        }
-#pragma unroll
-        for (int r = 0; r < kPatchRows; ++r) {
-            const half8 ah = __builtin_bit_cast(half8, A[(2 * r) * 64]);
-            const half8 al = __builtin_bit_cast(half8, A[(2 * r + 1) * 64]);
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                acc[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, qh[i], acc[i][r], 0, 0, 0);
-                acc[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, ql[i], acc[i][r], 0, 0, 0);
-                acc[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, qh[i], acc[i][r], 0, 0, 0);
-            }
-        }
-    };
-
-    // Epilogue: exactly kStoresPerTile buffer stores per wave.  Resources are per wave and
-    // level, based at the wave's first query row, sized to its valid queries.  Every store
-    // offset is computed unconditionally and then replaced by kOOB where the lane has nothing
-    // to write (a select, never a branch).
-    auto epilogue = [&](const TA &a, int buf, int ln) __attribute__((always_inline)) {
-        const int ci = ln & 15, grp = ln >> 4;
-        const int q0 = a.qb0 * 16;
-        const int nq = min(max(NQ - q0, 0), 32);
-        const size_t qrow0 = (size_t)a.b * NQ + q0;
-        const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(p.lvl[0] + qrow0 * N, 0, nq * N * 4, 0x00020000);
-        const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(p.lvl[1] + qrow0 * N1, 0, nq * N1 * 4, 0x00020000);
-        const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc(p.lvl[2] + qrow0 * N2, 0, nq * N2 * 4, 0x00020000);
-        const __amdgpu_buffer_rsrc_t r3 = __builtin_amdgcn_make_buffer_rsrc(p.lvl[3] + qrow0 * N3, 0, nq * N3 * 4, 0x00020000);
-        const int *etb = lds_et + buf * kExpInts;
-        const int y0 = a.y0, x0 = a.x0, X0 = x0 + 4 * grp;
-        auto sel_off = [&](bool ok, uint32_t o) __attribute__((always_inline)) {
-            o = opq(o);
-            return opq(ok ? o : kOOB);
-        };
-        float l2s[2][2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int eqv = etb[kPatchRows * 16 + (2 * w + i) * 16 + ci] + p.eshift;
-            const int qq = i * 16 + ci;  // query row within the wave's resources
-            const uint32_t o0 = (uint32_t)(qq * N + y0 * W + X0) * 4u;
-            const bool xok = X0 < W;
-            float l1[4][2];
-#pragma unroll
-            for (int r = 0; r < kPatchRows; ++r) {
-                const int4 e4 = reinterpret_cast<const int4 *>(etb)[r * 4 + grp];
-                const int et[4] = {e4.x, e4.y, e4.z, e4.w};
-                f32x4 v;
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    float x = ldexpf(acc[i][r][g], eqv + et[g]);
-                    if (!p.exact) x = x * p.inv_s;
-                    v[g] = x;
-                }
-                acc[i][r] = v;
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r0,
-                                                       sel_off(xok && y0 + r < H, o0 + (uint32_t)(r * W * 4)), 0, 0);
-                if (r & 1) {
-                    const f32x4 u = acc[i][r - 1];
-                    l1[r >> 1][0] = pool4(u[0], u[1], v[0], v[1]);
-                    l1[r >> 1][1] = pool4(u[2], u[3], v[2], v[3]);
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < 2; ++r) l2s[i][r] = pool4(l1[2 * r][0], l1[2 * r][1], l1[2 * r + 1][0], l1[2 * r + 1][1]);
-            // Level 1 as 16-B stores: lanes grp 2m, 2m + 1 swap one row's column pair (lanes 16
-            // apart), so that the even lane stores rows 0, 2 and the odd lane rows 1, 3.
-            const bool odd = grp & 1;
-            const int X1 = (x0 >> 1) + 4 * (grp >> 1);
-#pragma unroll
-            for (int rp = 0; rp < 2; ++rp) {
-                const int ra = 2 * rp, rb = ra + 1;
-                const float g0 = __shfl_xor(odd ? l1[ra][0] : l1[rb][0], 16);
-                const float g1 = __shfl_xor(odd ? l1[ra][1] : l1[rb][1], 16);
-                const f32x4 o4 = f32x4{odd ? g0 : l1[ra][0], odd ? g1 : l1[ra][1], odd ? l1[rb][0] : g0, odd ? l1[rb][1] : g1};
-                const int Y1 = (y0 >> 1) + ra + (odd ? 1 : 0);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o4), r1,
-                                                       sel_off(Y1 < H1 && X1 < W1, (uint32_t)(qq * N1 + Y1 * W1 + X1) * 4u), 0, 0);
-            }
-        }
-        {  // Level 2 of both blocks in one store (lane g gathers row g & 1 of block g >> 1).
-            const int bl = grp >> 1, rw = grp & 1;
-            auto sel = [&](int k) { return fsel(k & 2, fsel(k & 1, l2s[1][1], l2s[1][0]), fsel(k & 1, l2s[0][1], l2s[0][0])); };
-            const float t0v = sel(grp);
-            const float t1 = __shfl_xor(sel(grp ^ 1), 16), t2 = __shfl_xor(sel(grp ^ 2), 32), t3 = __shfl_xor(sel(grp ^ 3), 48);
-            auto pick = [&](int k) { return fsel(k & 2, fsel(k & 1, t3, t2), fsel(k & 1, t1, t0v)); };
-            const f32x4 o4 = f32x4{pick(grp), pick(grp ^ 1), pick(grp ^ 2), pick(grp ^ 3)};
-            const int Y2 = (y0 >> 2) + rw, X2 = x0 >> 2;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o4), r2,
-                                                   sel_off(Y2 < H2 && X2 < W2, (uint32_t)((bl * 16 + ci) * N2 + Y2 * W2 + X2) * 4u), 0, 0);
-        }
-        {  // Level 3: even lanes pool block 0, odd lanes block 1, in ((a + b) + c) + d order.
-            const int bl = grp & 1;
-            const float y0v = __shfl_xor(fsel(bl, l2s[0][0], l2s[1][0]), 16), y1v = __shfl_xor(fsel(bl, l2s[0][1], l2s[1][1]), 16);
-            const float a0 = fsel(bl, y0v, l2s[0][0]), a1 = fsel(bl, l2s[1][0], y0v);
-            const float a2 = fsel(bl, y1v, l2s[0][1]), a3 = fsel(bl, l2s[1][1], y1v);
-            const float l3 = pool4(a0, a1, a2, a3);
-            const int Y3 = y0 >> 3, X3 = X0 >> 3;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, l3), r3,
-                                                  sel_off(Y3 < H3 && X3 < W3, (uint32_t)((bl * 16 + ci) * N3 + Y3 * W3 + X3) * 4u), 0, 0);
-        }
-    };
-
-    // ---- prologue of the first tile ----
-    l16 = (uint32_t)lane * 16u;
-    TA cur = tile_addr(0);
-    issue_e(cur, 0);
-    issue_q(cur, 0, 0);
-    issue_t(cur, 0, 0);
-    issue_q(cur, 1, 1);
-    issue_t(cur, 1, 1);
-    {
-        // kStoresPerTile dropped stores (num_records 0): every tile, the first included, then
-        // starts with the same memory operations in flight, so the vmcnt immediates of steps 0
-        // and 1 are one constant each.
-        const __amdgpu_buffer_rsrc_t nul = __builtin_amdgcn_make_buffer_rsrc(p.lvl[0], 0, 0, 0x00020000);
-#pragma unroll
-        for (int i = 0; i < kStoresPerTile; ++i) __builtin_amdgcn_raw_buffer_store_b32(0u, nul, opq(kOOB), 0, 0);
-    }
-    int rs0 = 0;  // ring slot of the current tile's step 0
-    for (int k = 0; k < nmine; ++k) {
-        // the tile whose first steps are prefetched at the end of this one (the last tile
-        // prefetches itself: every group is issued, so every count below is a constant)
-        const TA nxt = tile_addr(k + 1 < nmine ? k + 1 : k);
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        l16 = (uint32_t)ln * 16u;
-        if (k < 4) stamp(2 + 4 * k);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int r = 0; r < kPatchRows; ++r) acc[i][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-        auto step = [&]<int s>() __attribute__((always_inline)) {
-            // wait for step s's target DMA (and everything older: its query loads, the exponents)
-            if constexpr (s < 2) vm_wait_barrier<group_ops<SS>(s == 0 ? SS - 1 : 0) + kStoresPerTile>();
-            else vm_wait_barrier<group_ops<SS>(s - 1)>();
-            if constexpr (s == 0)
-                if (k < 4) stamp(3 + 4 * k);
-            const int qs = s & 3;
-            asm volatile("" : "+v"(qv[qs][0][0]), "+v"(qv[qs][0][1]), "+v"(qv[qs][1][0]), "+v"(qv[qs][1][1]));
-            if constexpr (s == SS - 2) issue_e(nxt, (k + 1) & 1);
-            const int sl = (rs0 + s + 2) % kRing;
-            if constexpr (s + 2 < SS) {
-                issue_q(cur, s + 2, (s + 2) & 3);
-                issue_t(cur, s + 2, sl);
-            } else {
-                issue_q(nxt, s + 2 - SS, (s + 2) & 3);
-                issue_t(nxt, s + 2 - SS, sl);
-            }
-            compute((rs0 + s) % kRing, qs);
-        };
-        [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
-            (step.template operator()<S>(), ...);
-        }(std::make_integer_sequence<int, SS>{});
-        if (k < 4) stamp(4 + 4 * k);
-        epilogue(cur, k & 1, ln);
-        if (k < 4) stamp(5 + 4 * k);
-        cur = nxt;
-        rs0 = (rs0 + SS) % kRing;
-    }
-    // the last tile's self-prefetch is still landing in LDS: drain it before the workgroup's
-    // LDS can be handed to another workgroup
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (STAMP) {
-        unsigned long long rt;
-        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rt)::"memory");
-        if (w == 0 && lane == 0) {
-            stv[1] = rt;
-            stv[18] = nmine | ((unsigned long long)blockIdx.x << 32);
-            stv[19] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        if (w == 0 && lane < 20) p.stamp[(size_t)blockIdx.x * 20 + lane] = stv[lane];
-    }
-}
-
-// ---------------------------------------------------------------------------------------
 // Host side.
 // ---------------------------------------------------------------------------------------
 namespace {
@@ -1008,88 +675,6 @@ hipError_t launch_split_mfma(int NQ, int B, int D, int H, int W, int levels, con
     return hipSuccess;
 }
 
-// Resident workgroups of the streaming kernel per device: CUs x blocks per CU (occupancy API),
-// rounded down to a multiple of 8 (one share per XCD).
-template <int SS>
-int stream_slots() {
-    static std::atomic<int> cache[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    std::atomic<int> &c = cache[dev & 63];
-    int v = c.load(std::memory_order_acquire);
-    if (v > 0) return v;
-    int cus = 0, per = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)corr_build_stream_kernel<SS, false>, 256, kBuildLdsP) !=
-        hipSuccess)
-        return 0;
-    v = cus * std::max(per, 1) / 8 * 8;
-    c.store(v, std::memory_order_release);
-    return v;
-}
-
-// The streaming form applies: S in {4, 8}, >= 4 levels, levels 0-2 stored as 16-B runs.
-bool stream_applies(int S, int levels, int mode0, int cons) {
-    return (S == 4 || S == 8) && levels >= kFusedLevels && mode0 == 2 && cons;
-}
-
-constexpr int kStreamDefault = 0;  // the library's choice (measured in tools/kbench_build.hip)
-
-// stream: 1 = the streaming kernel where it applies, 0 = the one-tile-per-workgroup kernel.
-// slots > 0 overrides the resident-workgroup count; stamp: diagnostic build (measurement).
-hipError_t launch_split_mfma_s(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
-                               hipStream_t s, int stream = 1, int slots = 0, unsigned long long *stamp = nullptr) {
-    const SplitGeom g = split_geom(D, NQ, H, W);
-    const int mode0 = store_mode(W, pyr.p[0]);
-    const int cons = levels > 2 && store_mode(W >> 1, pyr.p[1]) == 2 && store_mode(W >> 2, pyr.p[2]) == 2;
-    if (!stream || !stream_applies(g.S, levels, mode0, cons))
-        return launch_split_mfma(NQ, B, D, H, W, levels, pyr, ws, s);
-    const SplitWs w = split_ws(ws, B, g);
-    BuildArgs p{};
-    p.pq = w.pq, p.pt = w.pt, p.eq = w.eq, p.et = w.et;
-    p.B = B, p.H = H, p.W = W, p.N = H * W, p.NQ = NQ, p.S = g.S;
-    p.nlev = kFusedLevels;
-    for (int l = 0; l < kFusedLevels; ++l) p.lvl[l] = pyr.p[l];
-    p.NQp = g.NQp, p.NQB = g.NQB, p.NQG = g.NQG, p.Hp = g.Hp, p.CB = g.CB, p.Wp = g.Wp;
-    p.npatch = (g.Hp / kPatchRows) * g.CB;
-    const float sD = std::sqrt((float)D);
-    p.inv_s = 1.0f / sD;
-    p.exact = is_pow2(sD);
-    p.eshift = 0;
-    if (p.exact) {
-        int e;
-        std::frexp(p.inv_s, &e);
-        p.eshift = e - 1;
-    }
-    p.mode0 = 2, p.mode1 = 2, p.cons = 1;
-    p.stamp = stamp;
-    p.order = g_tile_order;
-    const long tiles = (long)B * p.npatch * g.NQG;
-    if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
-    p.ntiles = (int)tiles;
-    static std::atomic<unsigned long long> lds_done[4];
-    const int ki = (g.S == 4 ? 0 : 2) + (stamp ? 1 : 0);
-    const void *fns[4] = {(const void *)corr_build_stream_kernel<4, false>, (const void *)corr_build_stream_kernel<4, true>,
-                          (const void *)corr_build_stream_kernel<8, false>, (const void *)corr_build_stream_kernel<8, true>};
-    const int lds = kBuildLdsP + (stamp ? 160 : 0);
-    hipError_t e = ensure_lds_limit(fns[ki], lds, lds_done[ki]);
-    if (e != hipSuccess) return e;
-    int P = slots > 0 ? slots / 8 * 8 : (g.S == 4 ? stream_slots<4>() : stream_slots<8>());
-    if (P <= 0) return hipErrorInvalidValue;
-    P = (int)std::min<long>(P, (tiles + 7) / 8 * 8);
-    const dim3 grid((unsigned)P), blk(256);
-    switch (ki) {
-        case 0: hipLaunchKernelGGL((corr_build_stream_kernel<4, false>), grid, blk, lds, s, p); break;
-        case 1: hipLaunchKernelGGL((corr_build_stream_kernel<4, true>), grid, blk, lds, s, p); break;
-        case 2: hipLaunchKernelGGL((corr_build_stream_kernel<8, false>), grid, blk, lds, s, p); break;
-        default: hipLaunchKernelGGL((corr_build_stream_kernel<8, true>), grid, blk, lds, s, p); break;
-    }
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    if (levels > kFusedLevels) return launch_pool_levels(pyr, kFusedLevels, levels, (long)B * NQ, H, W, s);
-    return hipSuccess;
-}
-
 // part: 0 = pack + MFMA; 1 = the pack alone; 2 = the MFMA kernel alone (measurement: the
 // workspace must already hold this pair's pack).
 hipError_t launch_build_split(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, int levels,
@@ -1098,7 +683,7 @@ hipError_t launch_build_split(const float *f1, int NQ, const float *f2, int B, i
         const hipError_t e = launch_split_pack(f1, NQ, f2, B, D, H, W, ws, s);
         if (e != hipSuccess || part == 1) return e;
     }
-    return launch_split_mfma_s(NQ, B, D, H, W, levels, pyr, ws, s, kStreamDefault);
+    return launch_split_mfma(NQ, B, D, H, W, levels, pyr, ws, s);
 }
 
 }  // namespace corr

@@ -1,5 +1,5 @@
 // kbench_build.hip — the f16x3 build (corr_build_split.hip) against the exact-fp32 MFMA build
-// (corr_build.hip), the persistent form against the one-tile-per-workgroup kernel:
+// (corr_build.hip), and variants of the MFMA kernel (tile order, fragment pipelining):
 //   * accuracy: max |x - f32| / max |f32| over every pyramid level, three operand scales;
 //   * pooling: levels 1-3 bit-identical to avg_pool2d of the kernel's own level 0 (host check);
 //   * timing: interleaved rounds of every variant in one process, random data (HIP events
@@ -144,9 +144,6 @@ int main(int argc, char **argv) {
         vs.push_back({"x3 mfma 1-tile nopipe (206 VGPR)", [&](float *o) {
                           return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 1);
                       }, false});
-        vs.push_back({"x3 mfma stream", [&](float *o) {
-                          return launch_split_mfma_s(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1);
-                      }, false});
         for (float sc : {1.0f, 1e-3f, 300.0f}) {
             hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f1, fe, 1u, sc);
             hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f2, fe, 2u, sc);
@@ -189,9 +186,7 @@ int main(int argc, char **argv) {
                 return with_order(0, [&] { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
             });
             same("1-tile nopipe", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 1); });
-            same("stream", [&](float *o) { return launch_split_mfma_s(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1); });
 
-            same("stream 1/CU", [&](float *o) { return launch_split_mfma_s(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, 1, 256); });
         }
         {  // pooling of the new kernel: every level bit-identical to avg_pool2d of its own level 0
             CK(launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), ws, 0));
@@ -212,68 +207,6 @@ int main(int argc, char **argv) {
             }
             printf("%-10s pooling levels 1-3 vs own level 0: %s (%zu mismatches)\n", sh.name,
                    bad ? "DIFFER" : "bit-identical", bad);
-        }
-        if (vfilter && !strcmp(vfilter, "stamp")) {  // diagnostic: per-tile clock stamps of the streaming kernel
-            {  // the streaming kernel: per tile (first 4) start, after step 0, after the loop, after the epilogue
-                const int P = stream_slots<8>();
-                unsigned long long *ss;
-                CK(hipMalloc(&ss, (size_t)P * 20 * 8));
-                CK(hipMemset(ss, 0, (size_t)P * 20 * 8));
-                for (int i = 0; i < 20; ++i) CK(launch_split_mfma_s(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), ws, 0, 1, 0, ss));
-                CK(hipDeviceSynchronize());
-                std::vector<unsigned long long> h((size_t)P * 20);
-                CK(hipMemcpy(h.data(), ss, h.size() * 8, hipMemcpyDeviceToHost));
-                unsigned long long r0 = ~0ull, r1 = 0;
-                double dm = 0, dr = 0;
-                int nwg = 0;
-                double ph[4][4] = {}, tl[4] = {};
-                int nt[4] = {}, hist[8] = {};
-                for (int j = 0; j < P; ++j) {
-                    const unsigned long long *o = &h[(size_t)j * 20];
-                    if (!o[0]) continue;
-                    ++nwg;
-                    r0 = std::min(r0, o[0]), r1 = std::max(r1, o[1]);
-                    const int nm = (int)(o[18] & 0xffffffff);
-                    ++hist[std::min(nm, 7)];
-                    const int kl = std::min(nm, 4) - 1;
-                    dm += (double)(o[5 + 4 * kl] - o[2]), dr += (double)(o[1] - o[0]);
-                    for (int k = 0; k < std::min(nm, 4); ++k) {
-                        const unsigned long long *t = o + 2 + 4 * k;
-                        ph[k][0] += (double)(t[1] - t[0]);
-                        ph[k][1] += (double)(t[2] - t[1]);
-                        ph[k][2] += (double)(t[3] - t[2]);
-                        if (k + 1 < std::min(nm, 4)) ph[k][3] += (double)(t[4] - t[3]);
-                        ++nt[k];
-                        tl[k] += (double)(t[3] - t[0]);
-                    }
-                }
-                {  // which blocks share a CU (HW_ID bits 15:8), first 6 CUs
-                    std::vector<std::vector<int>> cu(256);
-                    for (int j = 0; j < P; ++j) {
-                        const unsigned long long *o = &h[(size_t)j * 20];
-                        if (o[0]) cu[(o[19] >> 8) & 0xff].push_back((int)(o[18] >> 32));
-                    }
-                    printf("%-10s co-resident blocks:", sh.name);
-                    for (int c = 0, shown = 0; c < 256 && shown < 8; ++c)
-                        if (!cu[c].empty()) {
-                            printf(" [");
-                            for (int b : cu[c]) printf(" %d", b);
-                            printf(" ]");
-                            ++shown;
-                        }
-                    printf("\n");
-                }
-                const double clk = dm / dr * 100.0;
-                printf("%-10s stream stamp: %d WGs, clock ~%.0f MHz (memtime/realtime over the stamped part), span %.2f us; tiles/WG:", sh.name, nwg, clk,
-                       (r1 - r0) / 100.0);
-                for (int k = 0; k < 8; ++k)
-                    if (hist[k]) printf(" %d:%d", k, hist[k]);
-                printf("\n   tile   n   to-step0-barrier  K-loop  epilogue  (cycles)\n");
-                for (int k = 0; k < 4; ++k)
-                    if (nt[k]) printf("   %d %5d %10.0f %10.0f %8.0f\n", k, nt[k], ph[k][0] / nt[k], ph[k][1] / nt[k], ph[k][2] / nt[k]);
-                CK(hipFree(ss));
-            }
-            vfilter = "x3 mfma";
         }
         if (vfilter) {
             std::vector<Variant> keep;
