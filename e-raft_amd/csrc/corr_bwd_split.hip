@@ -606,7 +606,10 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
 // 436 us with 5 splits = 560 workgroups, 401 us with 3).
 constexpr long kGemmSlots = 512;
 
+int g_gemm_splits = 0;  // measurement override of the split count (tools/kbench_gemm.hip); 0 = plan
+
 int plan_split_k(int NI, int NJ, int nkc, int batch) {
+    if (g_gemm_splits > 0) return g_gemm_splits;
     const long tiles = (long)((NI + kTI - 1) / kTI) * ((NJ + kTJ - 1) / kTJ) * batch;
     long splits = std::max(1L, kGemmSlots / tiles);
     splits = std::min<long>(splits, std::max(1, nkc / 8));  // >= 128 k per split

@@ -1,0 +1,136 @@
+// kbench_gemm.hip — the backward split GEMMs (corr_bwd_split.hip) at the train shape (B 8,
+// D 256, 36x48): dF1 = F2 dC^T (row operands) and dF2 = F1 dC (dC columns), each with its
+// split-K reduce, for several split counts (HIP events around back-to-back launches).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++20 -ffp-contract=off -o tools/_build/kbench_gemm tools/kbench_gemm.hip \
+//         e-raft_amd/csrc/corr_bwd.hip e-raft_amd/csrc/corr_build.hip e-raft_amd/csrc/corr_lookup.hip
+#include <algorithm>
+#include <cstring>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../e-raft_amd/csrc/corr_bwd_split.hip"
+
+using namespace corr;
+
+#define CK(x)                                                                                 \
+    do {                                                                                      \
+        hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) {                                                               \
+            fprintf(stderr, "%s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                          \
+        }                                                                                     \
+    } while (0)
+
+__global__ void fill(float *p, size_t n, unsigned seed) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        unsigned x = (unsigned)i * 2654435761u ^ seed;
+        x ^= x >> 13;
+        x *= 0x5bd1e995u;
+        x ^= x >> 15;
+        p[i] = ((x >> 8) * (1.0f / 16777216.0f)) * 2.0f - 1.0f;
+    }
+}
+
+__global__ void maxdiff(const float *a, const float *b, size_t n, unsigned *dmax, unsigned *rmax) {
+    float d = 0.f, r = 0.f;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        d = fmaxf(d, fabsf(a[i] - b[i]));
+        r = fmaxf(r, fabsf(a[i]));
+    }
+    atomicMax(dmax, __float_as_uint(d));
+    atomicMax(rmax, __float_as_uint(r));
+}
+
+int main(int argc, char **argv) {
+    const int rounds = argc > 1 ? atoi(argv[1]) : 10;
+    const int B = 8, D = 256, H = 36, W = 48, N = H * W, NQ = N;
+    float *f1, *f2, *dc, *o1, *o2, *r1, *r2;
+    CK(hipMalloc(&f1, (size_t)B * D * N * 4));
+    CK(hipMalloc(&f2, (size_t)B * D * N * 4));
+    CK(hipMalloc(&dc, (size_t)B * NQ * N * 4));
+    CK(hipMalloc(&o1, (size_t)B * D * N * 4));
+    CK(hipMalloc(&o2, (size_t)B * D * N * 4));
+    CK(hipMalloc(&r1, (size_t)B * D * N * 4));
+    CK(hipMalloc(&r2, (size_t)B * D * N * 4));
+    hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f1, (size_t)B * D * N, 1u);
+    hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f2, (size_t)B * D * N, 2u);
+    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, dc, (size_t)B * NQ * N, 3u);
+    g_gemm_splits = 16;  // the largest slab the variants need
+    const size_t wsb = build_bwd_split_workspace(B, D, NQ, H, W);
+    g_gemm_splits = 0;
+    void *ws;
+    CK(hipMalloc(&ws, wsb));
+    const BwdWs w = carve(ws, B, D, NQ, N);
+    CK(hipMemset(w.mx0, 0, w.mx_bytes));
+    CK(absmax(dc, B, NQ, N, w.mxB, w.mxC, 0));
+    CK(rowmax2(f2, N, w.mxA, f1, NQ, w.mxA2, B, D, 0));
+    const float sD = 16.0f;
+    auto g1 = [&](float *out) {
+        return gemm_f32<false>(f2, (long)D * N, N, dc, (long)NQ * N, N, 1, w.mxA, w.mxB, B, D, NQ, N, sD, out, w.slab, 0);
+    };
+    auto g2 = [&](float *out) {
+        return gemm_f32<true>(f1, (long)D * NQ, NQ, dc, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, out, w.slab, 0);
+    };
+    CK(g1(r1));
+    CK(g2(r2));
+    struct V {
+        std::string name;
+        std::function<hipError_t()> run;
+        float *out, *ref;
+        std::vector<float> us;
+    };
+    std::vector<V> vs;
+    for (int sp : {0, 1, 2, 3, 4, 6, 8}) {
+        vs.push_back({"dF1 (rows) splits " + std::string(sp ? std::to_string(sp) : "plan"), [&, sp] {
+                          g_gemm_splits = sp;
+                          const hipError_t e = g1(o1);
+                          g_gemm_splits = 0;
+                          return e;
+                      }, o1, r1, {}});
+        vs.push_back({"dF2 (cols) splits " + std::string(sp ? std::to_string(sp) : "plan"), [&, sp] {
+                          g_gemm_splits = sp;
+                          const hipError_t e = g2(o2);
+                          g_gemm_splits = 0;
+                          return e;
+                      }, o2, r2, {}});
+    }
+    for (auto &v : vs) {
+        CK(v.run());
+        unsigned *d;
+        unsigned hv[2] = {0, 0};
+        CK(hipMalloc(&d, 8));
+        CK(hipMemset(d, 0, 8));
+        hipLaunchKernelGGL(maxdiff, dim3(2048), dim3(256), 0, 0, v.ref, v.out, (size_t)B * D * N, d, d + 1);
+        CK(hipMemcpy(hv, d, 8, hipMemcpyDeviceToHost));
+        CK(hipFree(d));
+        float dm, rm;
+        std::memcpy(&dm, &hv[0], 4);
+        std::memcpy(&rm, &hv[1], 4);
+        printf("%-28s max|x - plan| / max|plan| = %.3e\n", v.name.c_str(), dm / rm);
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    constexpr int PER = 4;
+    for (int r = 0; r < rounds; ++r)
+        for (auto &v : vs) {
+            CK(hipEventRecord(e0, 0));
+            for (int i = 0; i < PER; ++i) CK(v.run());
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            v.us.push_back(ms * 1e3f / PER);
+        }
+    const double fl = 2.0 * B * (double)D * N * NQ;
+    for (auto &v : vs) {
+        std::sort(v.us.begin(), v.us.end());
+        const float med = v.us[v.us.size() / 2];
+        printf("%-28s median %8.2f us  min %8.2f us  %6.3f of 2.5 PF f16 pipe (x3)\n", v.name.c_str(), med, v.us[0],
+               3.0 * fl / (med * 1e-6) / 2.5e15);
+    }
+    return 0;
+}
