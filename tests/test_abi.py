@@ -91,6 +91,10 @@ def test_build_ex_workspace_and_validation(lib):
     assert rc == -1 and "unknown algorithm" in lib.corr_last_error().decode()
     rc = lib.corr_build_ex(1, 256, 4800, 256, 1, 256, 60, 80, 4, pyr, 260, 1 << 40, None)
     assert rc == -1 and "256-byte aligned" in lib.corr_last_error().decode()
+    # measurement phase flags: one at a time, and only on the f16x3 build
+    for algo in (0x100 | 0x200 | 1, 0x100 | 0, 0x200 | 0):
+        rc = lib.corr_build_ex(algo, 256, 4800, 256, 1, 256, 60, 80, 4, pyr, 256, 1 << 40, None)
+        assert rc == -1 and "unknown algorithm" in lib.corr_last_error().decode(), hex(algo)
 
 
 def test_build_algo_env(monkeypatch):

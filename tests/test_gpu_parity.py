@@ -87,6 +87,28 @@ def test_split_build_shapes_deterministic(shape, monkeypatch):
         assert bit_equal(oracle.avg_pool2x2(pyrs[0][l - 1]), pyrs[0][l]), l
 
 
+@pytest.mark.parametrize("shape", [(1, 256, 60, 80), (2, 200, 17, 23)])
+def test_split_build_phases_compose(shape):
+    """The measurement flags CORR_BUILD_ONLY_PACK then CORR_BUILD_ONLY_MFMA (bench.py times the
+    two kernels separately with them) write the same pyramid, bit for bit, as one full build."""
+    from eraft_amd import _lib
+    B, D, H, W = shape
+    t1 = torch.from_numpy(prng.gauss(21, (B, D, H, W))).to(DEV)
+    t2 = torch.from_numpy(prng.gauss(22, (B, D, H, W))).to(DEV)
+    L = min(4, int(np.log2(min(H, W))) + 1)
+    shapes = [(B * H * W, 1, H >> l, W >> l) for l in range(L)]
+    full = [torch.empty(s, device=DEV) for s in shapes]
+    split = [torch.full(s, float("nan"), device=DEV) for s in shapes]
+    ws = _lib.build_workspace(t1, t2, _lib.BUILD_F16X3)
+    _lib.build(t1, t2, full, _lib.BUILD_F16X3, ws)
+    ws.zero_()
+    _lib.build(t1, t2, split, _lib.BUILD_F16X3 | _lib.BUILD_ONLY_PACK, ws)
+    _lib.build(t1, t2, split, _lib.BUILD_F16X3 | _lib.BUILD_ONLY_MFMA, ws)
+    torch.cuda.synchronize()
+    for l in range(L):
+        assert bit_equal(full[l].cpu().numpy(), split[l].cpu().numpy()), l
+
+
 @pytest.mark.parametrize("name", BUILD_CASES)
 def test_lookup_bitexact_on_reference_pyramid(name):
     g = load(name)
