@@ -27,10 +27,11 @@ namespace corr {
 // Tile geometry.  WQ x WT waves; each wave QT query tiles of 32 x one 8x8 target sub-patch.
 // PF: read all of a chunk's MFMA operands from LDS before issuing its MFMAs.
 // SKIP: skip the MFMAs of a 4-row target tile that lies entirely below the map.
-template <int WQ_, int WT_, int QT_, int BK_, int OCC_, bool PF_ = false, bool SKIP_ = true>
+// NOSTORE: measurement instantiation only (tools/kbench_build.hip): no pyramid stores.
+template <int WQ_, int WT_, int QT_, int BK_, int OCC_, bool PF_ = false, bool SKIP_ = true, bool NOSTORE_ = false>
 struct BuildCfg {
     static constexpr int WQ = WQ_, WT = WT_, QT = QT_, BK = BK_, OCC = OCC_;
-    static constexpr bool PF = PF_, SKIP = SKIP_;
+    static constexpr bool PF = PF_, SKIP = SKIP_, NOSTORE = NOSTORE_;
     static constexpr int NT = 64 * WQ * WT;  // threads
     static constexpr int BQ = 32 * QT * WQ;  // queries per tile
     static constexpr int PW = 8 * WT;        // target patch columns (8 rows)
@@ -42,8 +43,10 @@ struct BuildCfg {
     static_assert(NT % (BQ / 4) == 0 && NT % (BT / 4) == 0, "fixed staging column per thread");
 };
 
-// Default geometry (selected by tools/kbench_build.hip measurements).
-using BuildDefault = BuildCfg<2, 2, 2, 8, 4, true, true>;
+// Default geometry (selected by tools/kbench_build.hip measurements).  No SKIP:
+// the second (half-tile) kernel body costs more than the MFMAs it skips (DSEC 126 -> 123 us,
+// train 139 -> 137 us; profiles/r03f_kbench_build_fp32.txt).
+using BuildDefault = BuildCfg<2, 2, 2, 8, 4, true, false>;
 
 struct BuildParams {
     const float *f1;
@@ -62,7 +65,10 @@ struct BuildParams {
 // Epilogue: scale, level 0, in-register pyramid.
 // acc[qt][tt][r]: query qw + qt*32 + l32, target (y, x) of the wave's 8x8 sub-patch at
 // (py*8, xw) with y = tt*4 + (r >> 2), x = 4h + (r & 3)   (32x32 C/D map).
-template <int QT, bool VEC>
+// VEC1 (W % 8 == 0, 16-B aligned levels): the two lane halves (h = 0, 1: the same query, target
+// columns 0-3 / 4-7) swap half of their level-1 rows, so a lane writes 2 level-1 rows of 4
+// columns as two 16-B stores (instead of 8 element stores), and one 8-B level-2 pair.
+template <int QT, bool VEC, bool VEC1>
 __device__ __forceinline__ void store_pyramid(const BuildParams &p, f32x16 (&acc)[QT][2], const int b,
                                               const int qw, const int xw, const int py, const int h,
                                               const int l32) {
@@ -110,7 +116,30 @@ __device__ __forceinline__ void store_pyramid(const BuildParams &p, f32x16 (&acc
             for (int x = 0; x < 2; ++x)
                 l1[y][x] = pool4(v[2 * y][2 * x], v[2 * y][2 * x + 1], v[2 * y + 1][2 * x],
                                  v[2 * y + 1][2 * x + 1]);
-        if (qok) {
+        if (VEC1) {
+            // h = 0 keeps rows 0-1 and receives columns 2-3 of them; h = 1 keeps rows 2-3 and
+            // receives columns 0-1 of them
+            float r[2][4];
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+#pragma unroll
+                for (int x = 0; x < 2; ++x) {
+                    const float give = h ? l1[y][x] : l1[y + 2][x];
+                    const float got = __shfl_xor(give, 32);
+                    const float mine = h ? l1[y + 2][x] : l1[y][x];
+                    r[y][2 * h + x] = mine;
+                    r[y][2 * (1 - h) + x] = got;
+                }
+            if (qok && xw < W) {
+                float *o = p.lvl[1] + qrow * (size_t)(H1 * W1) + (xw >> 1);
+#pragma unroll
+                for (int y = 0; y < 2; ++y) {
+                    const int Y = py * 4 + 2 * h + y;
+                    if (Y < H1)
+                        *reinterpret_cast<float4 *>(o + (size_t)Y * W1) = make_float4(r[y][0], r[y][1], r[y][2], r[y][3]);
+                }
+            }
+        } else if (qok) {
             float *o = p.lvl[1] + qrow * (size_t)(H1 * W1);
 #pragma unroll
             for (int y = 0; y < 4; ++y)
@@ -125,7 +154,15 @@ __device__ __forceinline__ void store_pyramid(const BuildParams &p, f32x16 (&acc
         float l2[2];
 #pragma unroll
         for (int y = 0; y < 2; ++y) l2[y] = pool4(l1[2 * y][0], l1[2 * y][1], l1[2 * y + 1][0], l1[2 * y + 1][1]);
-        if (qok) {
+        // the partner half's level-2 pair (x = 1 - h): for the 8-B level-2 stores and level 3
+        const float o0 = __shfl_xor(l2[0], 32);
+        const float o1 = __shfl_xor(l2[1], 32);
+        if (VEC1) {  // h = 0 writes row 0 (x = 0, 1), h = 1 row 1
+            const int Y = py * 2 + h;
+            if (qok && xw < W && Y < H2)
+                *reinterpret_cast<float2 *>(p.lvl[2] + qrow * (size_t)(H2 * W2) + (size_t)Y * W2 + (xw >> 2)) =
+                    h ? make_float2(o1, l2[1]) : make_float2(l2[0], o0);
+        } else if (qok) {
             float *o = p.lvl[2] + qrow * (size_t)(H2 * W2);
             const int X = X0 >> 2;
 #pragma unroll
@@ -136,8 +173,6 @@ __device__ __forceinline__ void store_pyramid(const BuildParams &p, f32x16 (&acc
         }
         if (p.nlev < 4) continue;
         // level 3: the 2x2 level-2 block is split across lane halves h = 0 (x = 0), 1 (x = 1)
-        const float o0 = __shfl_xor(l2[0], 32);
-        const float o1 = __shfl_xor(l2[1], 32);
         if (h == 0 && qok) {
             const float l3 = pool4(l2[0], o0, l2[1], o1);
             const int Y = py, X = X0 >> 3;
@@ -147,7 +182,9 @@ __device__ __forceinline__ void store_pyramid(const BuildParams &p, f32x16 (&acc
 }
 
 // One output tile.  smem: [stage][BK][BQ + BT].
-template <class Cfg, bool VEC, bool TT1>
+// VM: 0 = element loads / stores, 1 = 16-B staging loads and level-0 stores, 2 = also 16-B
+// level-1 and 8-B level-2 stores (store_pyramid's VEC1).
+template <class Cfg, int VM, bool TT1>
 __device__ __forceinline__ void build_tile(const BuildParams &p, float *smem, const int tile) {
     constexpr int NT = Cfg::NT, BQ = Cfg::BQ, BT = Cfg::BT, BK = Cfg::BK, QT = Cfg::QT;
     constexpr int PW = Cfg::PW, QPT = Cfg::QPT, TPT = Cfg::TPT;
@@ -183,7 +220,7 @@ __device__ __forceinline__ void build_tile(const BuildParams &p, float *smem, co
 #pragma unroll
         for (int i = 0; i < QPT; ++i) {
             const int k = k0 + qk + QKSTEP * i;
-            if (VEC) {
+            if (VM >= 1) {
                 rq[i] = (k < D && qidx < NQ) ? *reinterpret_cast<const float4 *>(f1b + (size_t)k * NQ + qidx)
                                             : make_float4(0.f, 0.f, 0.f, 0.f);
             } else {
@@ -196,7 +233,7 @@ __device__ __forceinline__ void build_tile(const BuildParams &p, float *smem, co
 #pragma unroll
         for (int i = 0; i < TPT; ++i) {
             const int k = k0 + tk + TKSTEP * i;
-            if (VEC) {
+            if (VM >= 1) {
                 rt[i] = (k < D && tvalid) ? *reinterpret_cast<const float4 *>(f2b + (size_t)k * N + tOff)
                                           : make_float4(0.f, 0.f, 0.f, 0.f);
             } else {
@@ -277,10 +314,17 @@ __device__ __forceinline__ void build_tile(const BuildParams &p, float *smem, co
         __syncthreads();
     }
 
-    store_pyramid<QT, VEC>(p, acc, b, q0 + wq * 32 * QT, px * PW + wt * 8, py, h, l32);
+    if constexpr (Cfg::NOSTORE) {  // keep the MFMAs live without writing the pyramid
+        float x = 0.f;
+#pragma unroll
+        for (int i = 0; i < QT; ++i) x += acc[i][0][0] + acc[i][1][15];
+        if (x == 1234.5f) p.lvl[0][tid] = x;
+    } else {
+        store_pyramid<QT, (VM >= 1), (VM == 2)>(p, acc, b, q0 + wq * 32 * QT, px * PW + wt * 8, py, h, l32);
+    }
 }
 
-template <class Cfg, bool VEC>
+template <class Cfg, int VM>
 __global__ __launch_bounds__(Cfg::NT, Cfg::OCC) void corr_build_kernel(BuildParams p) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int tile = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -288,9 +332,9 @@ __global__ __launch_bounds__(Cfg::NT, Cfg::OCC) void corr_build_kernel(BuildPara
     // one tile-uniform branch between two complete bodies (register pressure = the max of the
     // two, not their union)
     if (!Cfg::SKIP || py * 8 + 4 < p.H)
-        build_tile<Cfg, VEC, true>(p, smem, tile);
+        build_tile<Cfg, VM, true>(p, smem, tile);
     else
-        build_tile<Cfg, VEC, false>(p, smem, tile);
+        build_tile<Cfg, VM, false>(p, smem, tile);
 }
 
 namespace {
@@ -329,6 +373,9 @@ hipError_t launch_pool_levels(const LevelPtrs &pyr, int l_from, int levels, long
     return hipSuccess;
 }
 
+// 16-B level-1 stores when the shape allows (tools/kbench_build.hip turns them off for its A/B).
+bool g_build_vec1 = true;
+
 // Launch one build with tile geometry Cfg (exposed for tools/kbench_build.hip).
 template <class Cfg>
 hipError_t launch_build_cfg(const float *f1, int NQ, const float *f2, int B, int D, int H, int W,
@@ -356,18 +403,21 @@ hipError_t launch_build_cfg(const float *f1, int NQ, const float *f2, int B, int
                      ((uintptr_t)f1 % 16 == 0) && ((uintptr_t)f2 % 16 == 0);
     const long tiles = (long)p.nq * p.npx * p.npy * B;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
-    static std::atomic<unsigned long long> lds_done[2];
-    if (vec) {
-        hipError_t e = ensure_lds_limit((const void *)corr_build_kernel<Cfg, true>, (int)Cfg::LDS, lds_done[1]);
+    // 16-B level-1 / 8-B level-2 stores: whole 8-column sub-patches and aligned level bases
+    const bool vec1 = g_build_vec1 && vec && W % 8 == 0 && (p.nlev < 2 || (uintptr_t)pyr.p[1] % 16 == 0) &&
+                      (p.nlev < 3 || (uintptr_t)pyr.p[2] % 8 == 0);
+    static std::atomic<unsigned long long> lds_done[3];
+    auto go = [&](auto vm_tag) {
+        constexpr int VM = decltype(vm_tag)::value;
+        hipError_t e = ensure_lds_limit((const void *)corr_build_kernel<Cfg, VM>, (int)Cfg::LDS, lds_done[VM]);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((corr_build_kernel<Cfg, true>), dim3((unsigned)tiles), dim3(Cfg::NT),
-                           Cfg::LDS, s, p);
-    } else {
-        hipError_t e = ensure_lds_limit((const void *)corr_build_kernel<Cfg, false>, (int)Cfg::LDS, lds_done[0]);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((corr_build_kernel<Cfg, false>), dim3((unsigned)tiles), dim3(Cfg::NT),
-                           Cfg::LDS, s, p);
-    }
+        hipLaunchKernelGGL((corr_build_kernel<Cfg, VM>), dim3((unsigned)tiles), dim3(Cfg::NT), Cfg::LDS, s, p);
+        return hipSuccess;
+    };
+    hipError_t e0 = vec1 ? go(std::integral_constant<int, 2>{})
+                  : vec  ? go(std::integral_constant<int, 1>{})
+                         : go(std::integral_constant<int, 0>{});
+    if (e0 != hipSuccess) return e0;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (levels > kFusedLevels) return launch_pool_levels(pyr, kFusedLevels, levels, (long)B * NQ, H, W, s);

@@ -108,18 +108,24 @@ int main(int argc, char **argv) {
         vs.push_back({"f32 build (corr_build.hip)", [&](float *o) {
                           return launch_build_cfg<BuildDefault>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
                       }, true});
-        vs.push_back({"f32 2x2x2 BK8 occ3", [&](float *o) {
+        vs.push_back({"f32 noskip occ3", [&](float *o) {
                           return launch_build_cfg<BuildCfg<2, 2, 2, 8, 3, true, false>>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
                       }, true});
-        vs.push_back({"f32 2x2x2 BK16 occ3", [&](float *o) {
-                          return launch_build_cfg<BuildCfg<2, 2, 2, 16, 3, true, false>>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
-                      }, true});
-        vs.push_back({"f32 4x1x1 BK16 occ4", [&](float *o) {
-                          return launch_build_cfg<BuildCfg<4, 1, 1, 16, 4, true, false>>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
-                      }, true});
-        vs.push_back({"f32 2x2x2 BK8 occ4 skip", [&](float *o) {
+        vs.push_back({"f32 skip occ4 (round-2 default)", [&](float *o) {
                           return launch_build_cfg<BuildCfg<2, 2, 2, 8, 4, true, true>>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
                       }, true});
+        vs.push_back({"f32 element level-1/2 stores", [&](float *o) {
+                          g_build_vec1 = false;
+                          const hipError_t e = launch_build_cfg<BuildDefault>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
+                          g_build_vec1 = true;
+                          return e;
+                      }, true});
+        vs.push_back({"f32 level 0 only", [&](float *o) {
+                          return launch_build_cfg<BuildDefault>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 1, lp_of(o), 0);
+                      }, false});
+        vs.push_back({"f32 default NOSTORE", [&](float *o) {
+                          return launch_build_cfg<BuildCfg<2, 2, 2, 8, 4, true, false, true>>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
+                      }, false});
         vs.push_back({"x3 pack+mfma", [&](float *o) {
                           return launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
                       }, true});
