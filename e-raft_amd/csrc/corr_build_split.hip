@@ -527,11 +527,12 @@ __device__ __forceinline__ void build_tile(const BuildArgs &p, const Tile tl) {
     }
 }
 
-template <int SS, int QS = 4, bool PIPE = false>
+// HALF = false: measurement instantiation (one body; half patches compute their padding rows).
+template <int SS, int QS = 4, bool PIPE = false, bool HALF = true>
 __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
     const Tile tl = tile_of(p, xcd_swizzle(blockIdx.x, gridDim.x));
     // two whole code paths (no value flows out of either): a half patch runs half the MFMAs
-    if (SS > 0 && tl.py * kPatchRows + kPatchRows / 2 >= p.H) build_tile<SS, QS, PIPE, kPatchRows / 2>(p, tl);
+    if (HALF && SS > 0 && tl.py * kPatchRows + kPatchRows / 2 >= p.H) build_tile<SS, QS, PIPE, kPatchRows / 2>(p, tl);
     else build_tile<SS, QS, PIPE, kPatchRows>(p, tl);
 }
 
@@ -607,12 +608,12 @@ hipError_t launch_split_pack(const float *f1, int NQ, const float *f2, int B, in
 }
 
 // One instantiation of the one-tile-per-workgroup kernel, its dynamic-LDS limit raised once.
-template <int SS, int QS, bool PIPE>
+template <int SS, int QS, bool PIPE, bool HALF = true>
 hipError_t launch_build_kernel(dim3 grid, const BuildArgs &p, hipStream_t s) {
     static std::atomic<unsigned long long> lds_done{0};
-    const hipError_t e = ensure_lds_limit((const void *)corr_build_split_kernel<SS, QS, PIPE>, kBuildLds, lds_done);
+    const hipError_t e = ensure_lds_limit((const void *)corr_build_split_kernel<SS, QS, PIPE, HALF>, kBuildLds, lds_done);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((corr_build_split_kernel<SS, QS, PIPE>), grid, dim3(256), kBuildLds, s, p);
+    hipLaunchKernelGGL((corr_build_split_kernel<SS, QS, PIPE, HALF>), grid, dim3(256), kBuildLds, s, p);
     return hipGetLastError();
 }
 
@@ -656,6 +657,7 @@ hipError_t launch_split_mfma(int NQ, int B, int D, int H, int W, int levels, con
     if (variant != 0 && ss == 8) {
         switch (variant) {
             case 1: e = launch_build_kernel<8, 4, false>(grid, p, s); break;
+            case 2: e = launch_build_kernel<8, 4, true, false>(grid, p, s); break;
             default: return hipErrorInvalidValue;
         }
     } else {

@@ -147,6 +147,9 @@ int main(int argc, char **argv) {
         vs.push_back({"x3 mfma 1-tile order1", [&](float *o) {
                           return with_order(1, [&] { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
                       }, false});
+        vs.push_back({"x3 mfma 1-tile no half path", [&](float *o) {
+                          return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 2);
+                      }, false});
         vs.push_back({"x3 mfma 1-tile nopipe (206 VGPR)", [&](float *o) {
                           return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 1);
                       }, false});
@@ -191,6 +194,7 @@ int main(int argc, char **argv) {
             same("1-tile order0", [&](float *o) {
                 return with_order(0, [&] { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
             });
+            same("1-tile no half path", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 2); });
             same("1-tile nopipe", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 1); });
 
         }
