@@ -87,16 +87,23 @@ int main(int argc, char **argv) {
     float *cgrid;
     CK(hipMalloc(&cgrid, (size_t)B * 2 * N * 4));
     hipLaunchKernelGGL(fill_grid, dim3(256), dim3(256), 0, 0, cgrid, B, H, W);
-    auto launch = [&](auto kern, int t_count, bool grid0 = false) {
+    // lds > bytes: the same kernel with its LDS padded, i.e. fewer workgroups per CU (the
+    // occupancy sensitivity of the lookup loop)
+    auto launch = [&](auto kern, int t_count, bool grid0 = false, size_t lds = 0) {
         BwdLookups l2 = lk;
         l2.T = t_count;
         if (grid0) l2.coords[0] = cgrid;
-        CK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-        hipLaunchKernelGGL(kern, dim3((unsigned)(G * B)), dim3(64 * kFusedLv), bytes, 0, l2, o);
+        const size_t b = lds ? lds : bytes;
+        CK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b));
+        hipLaunchKernelGGL(kern, dim3((unsigned)(G * B)), dim3(64 * kFusedLv), b, 0, l2, o);
     };
     std::vector<V> vs;
     vs.push_back({"full T=12", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12); }, {}});
     vs.push_back({"full T=1", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 1); }, {}});
+    vs.push_back({"full T=12, 2 WG/CU (LDS padded to 64 KB)", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12, false, 64 * 1024); }, {}});
+    vs.push_back({"full T=1, 2 WG/CU", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 1, false, 64 * 1024); }, {}});
+    vs.push_back({"full T=12, 1 WG/CU (LDS padded to 96 KB)", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12, false, 96 * 1024); }, {}});
+    vs.push_back({"full T=1, 1 WG/CU", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 1, false, 96 * 1024); }, {}});
     vs.push_back({"full T=12, lookup 0 on the integer grid", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12, true); }, {}});
     vs.push_back({"full T=1 on the integer grid", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 1, true); }, {}});
     vs.push_back({"no lookups (zero + fold)", [&] { launch(lookup_bwd_fold_kernel<S, 1>, 12); }, {}});
