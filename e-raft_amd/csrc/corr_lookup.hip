@@ -764,11 +764,14 @@ __global__ __launch_bounds__(lookup_bwd_threads(S, BQ)) void lookup_bwd_kernel(B
 // per query, so BQ = 64 / SLOTS queries (4 at r = 4).  A wave touches only its own level's maps
 // and staging, so the lookup loop has NO workgroup barrier: each wave streams through the T
 // lookups on its own (the next lookup's loads in flight), and the workgroup meets once, before
-// the fold.  Per lookup: lanes cx < S compute tap cx of both axes and stage it with the upstream
-// gradients of x-tap cx (wave-private LDS); then lane cx produces its column's cells — closed
-// form (regular taps), contiguous hit ranges (irregular), or, when a corner leaves the (S+2)^2
-// neighbourhood, lookup_bwd_kernel's sequential scatter into a zeroed window scratch — and adds
-// them to the map (branchless: out-of-map cells go to a per-lane dump slot).
+// the fold.  Per lookup: lanes cx < S compute tap cx of both axes; the closed form takes the
+// group's other taps by DPP (row_newbcast for the y-taps and the anchors, row_shr for x-tap
+// cx - 1 and its gradients), so a regular lookup touches LDS only for its cells.  Lane cx then
+// produces its column's cells — closed form (regular taps), contiguous hit ranges (irregular),
+// or, when a corner leaves the (S+2)^2 neighbourhood, lookup_bwd_kernel's sequential scatter
+// into a zeroed window scratch (these two read every tap and gradient from the wave's LDS
+// staging, written only when some group of the wave needs it) — and adds them to the map
+// (branchless: out-of-map cells go to a per-lane dump slot).
 constexpr int kFusedLv = 4;  // level slots (= waves) per workgroup
 
 constexpr int fused_slots(int S) { return S + 2 <= 4 ? 4 : S + 2 <= 8 ? 8 : S + 2 <= 16 ? 16 : 32; }
@@ -850,6 +853,25 @@ __device__ __forceinline__ float lane_prev(float x, int cx) {
     }
 }
 
+// Lane J of this lane's SLOTS-lane group.  Groups of 16 lanes are DPP rows: row_newbcast:J (one
+// VALU move, no LDS); other group sizes use a bpermute.
+template <int SLOTS, int J>
+__device__ __forceinline__ float group_lane(float x, int lane) {
+    if constexpr (SLOTS == 16) {
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x150 + J, 0xF, 0xF, false));
+    } else {
+        return __shfl(x, (lane & ~(SLOTS - 1)) + J, 64);
+    }
+}
+
+template <int SLOTS, int N, int J = 0>
+__device__ __forceinline__ void group_lanes(float x, int lane, float (&out)[N]) {
+    if constexpr (J < N) {
+        out[J] = group_lane<SLOTS, J>(x, lane);
+        group_lanes<SLOTS, N, J + 1>(x, lane, out);
+    }
+}
+
 // Orders this wave's LDS traffic (LDS executes one wave's operations in issue order; the asm
 // also keeps the compiler from moving LDS accesses across it).
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -921,7 +943,7 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     if (act) prefetch(0);
 
     for (int t = 0; !(PROBE & 1) && act && t < lk.T; ++t) {  // absent levels (l >= L) only join the fold
-        // ---- 1. tap cx of both axes and the upstream gradients of x-tap cx -> staging ----
+        // ---- 1. tap cx of both axes; the group's taps reach the other lanes by DPP ----
         const float cxv = loader ? pcx : 0.0f, cyv = loader ? pcy : 0.0f;
         float v[S];
 #pragma unroll
@@ -929,31 +951,26 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         prefetch(min(t + 1, lk.T - 1));
         const Axis a = tap_axis(cxv, inv_scale, cxl, R, Wl);
         const Axis c = tap_axis(cyv, inv_scale, cxl, R, Hl);
-        if (cx < S) {
-            tx(0, cx) = a.f, tx(1, cx) = a.lo, tx(2, cx) = a.hi;
-            ty(0, cx) = c.f, ty(1, cx) = c.lo, ty(2, cx) = c.hi;
-            if (cx == 0) {
-                reinterpret_cast<int *>(st)[ST::AX + q] = anchor_of(a.f);
-                reinterpret_cast<int *>(st)[ST::AY + q] = anchor_of(c.f);
-            }
-        }
-        wave_lds_sync();
         // ---- 2. the (query, level) group's form, decided per group ----
-        const float fx0 = tx(0, 0), fy0 = ty(0, 0);
+        const float fx0 = group_lane<SLOTS, 0>(a.f, lane), fy0 = group_lane<SLOTS, 0>(c.f, lane);
         const bool bad = cx < S && !(a.f - fx0 == (float)cx && c.f - fy0 == (float)cx);
         const unsigned long long gmask = (SLOTS == 64 ? ~0ull : ((1ull << SLOTS) - 1)) << (q * SLOTS);
         const bool irregular = (__ballot(bad) & gmask) != 0;
-        const bool far = anchor_of(fx0) == kFarAnchor || anchor_of(fy0) == kFarAnchor;
-        const bool unc = qok && !window_covers<S>(fx0, tx(0, S - 1), fy0, ty(0, S - 1));
-        // the range form and the sequential scatter read any tap's gradients: stage them only
-        // when some group of the wave takes one of those paths
+        const int ax = anchor_of(fx0), ay = anchor_of(fy0);
+        const bool far = ax == kFarAnchor || ay == kFarAnchor;
+        const bool unc = qok && !window_covers<S>(fx0, group_lane<SLOTS, S - 1>(a.f, lane), fy0,
+                                                  group_lane<SLOTS, S - 1>(c.f, lane));
+        // the range form and the sequential scatter read any tap and any tap's gradients from the
+        // wave's staging: written only when some group of the wave takes one of those paths
         if (__ballot(irregular || unc)) {
-            if (cx < S)
+            if (cx < S) {
+                tx(0, cx) = a.f, tx(1, cx) = a.lo, tx(2, cx) = a.hi;
+                ty(0, cx) = c.f, ty(1, cx) = c.lo, ty(2, cx) = c.hi;
 #pragma unroll
                 for (int u = 0; u < S; ++u) gg(cx * S + u) = v[u];
+            }
             wave_lds_sync();
         }
-        const int ax = reinterpret_cast<int *>(st)[ST::AX + q], ay = reinterpret_cast<int *>(st)[ST::AY + q];
         const int X = ax + cx;
         const bool colok = qok && !unc && !far && cx < WIN && X >= 0 && X < Wl;
         // cell (cx, cy) of the window -> its map address, or the lane's dump slot when the cell
@@ -967,9 +984,14 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
             // in the reference's order (se, ne, sw, nw) with the same bits.  Arrays are indexed
             // by y-tap j + 1 with zero sentinels at j = -1 and j = S, and two cells (cy, cy + 1)
             // go through each packed-fp32 instruction (v_pk_mul_f32 / v_pk_add_f32, IEEE per lane).
-            const float wlo = cx < S ? tx(1, cx) : 0.f;
-            const float whi = cx >= 1 && cx <= S ? tx(2, cx - 1) : 0.f;
-            auto yv = [&](int c, int j) { return j >= 0 && j < S ? ty(c, j) : 0.f; };
+            // x-tap cx is this lane's own, x-tap cx - 1 the previous lane's; y-tap j is lane j's.
+            const float wlo = cx < S ? a.lo : 0.f;
+            const float hprev = lane_prev<SLOTS>(a.hi, cx);
+            const float whi = cx >= 1 && cx <= S ? hprev : 0.f;
+            float ylo_[S], yhi_[S];
+            group_lanes<SLOTS, S>(c.lo, lane, ylo_);
+            group_lanes<SLOTS, S>(c.hi, lane, yhi_);
+            auto yv = [&](int cc, int j) { return j >= 0 && j < S ? (cc == 1 ? ylo_[j] : yhi_[j]) : 0.f; };
             // the gradients of x-tap cx are this lane's own loads (v: zero for cx >= S and for
             // absent queries), those of x-tap cx - 1 the previous lane's (lane_prev: zero at cx = 0)
             float gpr[S];

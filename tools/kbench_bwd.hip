@@ -111,6 +111,12 @@ int main(int argc, char **argv) {
     vs.push_back({"zero-init only", [&] { launch(lookup_bwd_fold_kernel<S, 3>, 12); }, {}});
     vs.push_back({"fold only (no zero)", [&] { launch(lookup_bwd_fold_kernel<S, 5>, 12); }, {}});
     vs.push_back({"empty (no zero, no fold)", [&] { launch(lookup_bwd_fold_kernel<S, 7>, 12); }, {}});
+    if (argc > 2) {  // time only the variant named exactly argv[2] (for PMC passes)
+        std::vector<V> keep;
+        for (auto &v : vs)
+            if (v.name == argv[2]) keep.push_back(v);
+        vs = keep;
+    }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
