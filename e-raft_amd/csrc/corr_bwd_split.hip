@@ -362,10 +362,40 @@ struct FGemmParams {
     int direct, vec;  // vec: 16-B loads legal (strides / bases / K multiples of 4)
 };
 
-template <bool BCOL>
+typedef __attribute__((address_space(3))) void gemm_lds_t;
+
+// One LDS-DMA piece: 16 B per lane from g into LDS at lds + 16 * lane (global_load_lds_dwordx4,
+// M0 = the wave-uniform LDS byte address); counted in vmcnt like any vector load.
+__device__ __forceinline__ void gemm_dma16(const void *g, uint32_t lds) {
+    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(lds) : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void gemm_wait_vm_barrier() {
+    static_assert(N == 0 || N == 6, "vmcnt immediates of the DMA ring (6 pieces per wave per chunk)");
+    if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Dynamic LDS of the GEMM: the hi/lo staging (2 stages; DMA: 1), the row exponents, and (DMA)
+// a 2-slot ring of raw fp32 chunks (kRows rows x 16 k; BCOL: B as 16 k-rows x 256 columns).
+constexpr int kRawFloats = kRows * kBK;  // per ring slot
+template <bool DMA>
+constexpr int gemm_lds_bytes() {
+    return (DMA ? 1 : 2) * kRows * 4 * (int)sizeof(u32x4) + kRows * (int)sizeof(int) +
+           (DMA ? 2 * kRawFloats * (int)sizeof(float) : 0);
+}
+
+// DMA = true: the raw fp32 chunks arrive by LDS-DMA two chunks ahead (no register staging, so a
+// chunk's loads have two MFMA phases to land); each chunk is then split LDS -> registers -> the
+// hi/lo staging (the same split and layout as the register path, so the same bits).  Needs 16-B
+// aligned operands, K % 16 == 0 and (BCOL) NJ % 4 == 0.
+template <bool BCOL, bool DMA = false>
 __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
-    __shared__ __attribute__((aligned(16))) u32x4 lds[2 * kRows * 4];
-    __shared__ int lex[kRows];
+    extern __shared__ __attribute__((aligned(16))) u32x4 gemm_smem[];
+    u32x4 *lds = gemm_smem;
+    int *lex = reinterpret_cast<int *>(gemm_smem + (DMA ? 1 : 2) * kRows * 4);
+    float *raw = reinterpret_cast<float *>(lex + kRows);
     int id = xcd_swizzle(blockIdx.x, gridDim.x);
     const int tj = id % p.tj;
     id /= p.tj;
@@ -544,7 +574,67 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
 #pragma unroll
             for (int n = 0; n < kNJ; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh[n], acc[m][n], 0, 0, 0);
     };
-    if constexpr (!BCOL) {  // row operands: one set (two would spill at 256 VGPRs)
+    if constexpr (DMA) {
+        const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const uint32_t raw_base = (uint32_t)(uintptr_t)(gemm_lds_t *)raw;
+        // this wave's pieces of a chunk: A rows 16 (2w + q) + lane / 4, 16-B piece lane % 4;
+        // B rows 16 (4w + q) + lane / 4 (BCOL: k-row 4w + q, columns 4 lane .. 4 lane + 3)
+        const float *asrc[2], *bsrc[4];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int row = 16 * (2 * w + q) + (lane >> 2);
+            asrc[q] = p.A + (size_t)b * p.a_sb + (size_t)min(i0 + row, p.NI - 1) * p.a_sr + (lane & 3) * 4;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (!BCOL) {
+                const int row = 16 * (4 * w + q) + (lane >> 2);
+                bsrc[q] = p.Bm + (size_t)b * p.b_sb + (size_t)min(j0 + row, p.NJ - 1) * p.b_sr + (lane & 3) * 4;
+            } else {
+                bsrc[q] = p.Bm + (size_t)b * p.b_sb + (size_t)(4 * w + q) * p.b_sk + min(j0 + 4 * lane, p.NJ - 4);
+            }
+        }
+        auto issue = [&](int kc, int slot) __attribute__((always_inline)) {
+            const uint32_t base = raw_base + slot * kRawFloats * 4;
+            const size_t ka = (size_t)kc * kBK, kb = BCOL ? (size_t)kc * kBK * p.b_sk : ka;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) gemm_dma16(asrc[q] + ka, base + (2 * w + q) * 1024);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gemm_dma16(bsrc[q] + kb, base + kTI * kBK * 4 + (4 * w + q) * 1024);
+        };
+        auto read_raw = [&](int slot) __attribute__((always_inline)) {
+            const float *R = raw + slot * kRawFloats;
+            const float4 *ar = reinterpret_cast<const float4 *>(R + arow * kBK + aoct * 8);
+            const float4 x0 = ar[0], x1 = ar[1];
+            ra0[0] = x0.x, ra0[1] = x0.y, ra0[2] = x0.z, ra0[3] = x0.w;
+            ra0[4] = x1.x, ra0[5] = x1.y, ra0[6] = x1.z, ra0[7] = x1.w;
+            const float *RB = R + kTI * kBK;
+            if (!BCOL) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const float4 *br = reinterpret_cast<const float4 *>(RB + brow[u] * kBK + aoct * 8);
+                    const float4 y0 = br[0], y1 = br[1];
+                    rb0[8 * u + 0] = y0.x, rb0[8 * u + 1] = y0.y, rb0[8 * u + 2] = y0.z, rb0[8 * u + 3] = y0.w;
+                    rb0[8 * u + 4] = y1.x, rb0[8 * u + 5] = y1.y, rb0[8 * u + 6] = y1.z, rb0[8 * u + 7] = y1.w;
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < 16; ++t) rb0[t] = RB[t * kTJ + tid];
+            }
+        };
+        if (kc0 < kc1) issue(kc0, 0);
+        if (kc0 + 1 < kc1) issue(kc0 + 1, 1);
+        for (int kc = kc0; kc < kc1; ++kc) {
+            const int slot = (kc - kc0) & 1;
+            if (kc + 1 < kc1) gemm_wait_vm_barrier<6>();  // chunk kc landed (every wave's pieces)
+            else gemm_wait_vm_barrier<0>();
+            read_raw(slot);
+            store_chunk(0, ra0, rb0);
+            __syncthreads();  // staging complete, ring slot read
+            if (kc + 2 < kc1) issue(kc + 2, slot);
+            mfma_chunk(0);
+        }
+    } else if constexpr (!BCOL) {  // row operands: one set (two would spill at 256 VGPRs)
         if (kc0 < kc1) {
             load_chunk(kc0, ra0, rb0);
             store_chunk(0, ra0, rb0);
@@ -607,6 +697,7 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
 constexpr long kGemmSlots = 512;
 
 int g_gemm_splits = 0;  // measurement override of the split count (tools/kbench_gemm.hip); 0 = plan
+int g_gemm_dma = 1;     // LDS-DMA operand ring when the shape allows (tools/kbench_gemm.hip A/B)
 
 int plan_split_k(int NI, int NJ, int nkc, int batch) {
     if (g_gemm_splits > 0) return g_gemm_splits;
@@ -705,8 +796,17 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     p.vec = al16(A) && al16(Bm) && a_sb % 4 == 0 && a_sr % 4 == 0 && b_sb % 4 == 0 &&
             (BCOL ? b_sk % 4 == 0 : b_sr % 4 == 0);
     const long grid = (long)p.ti * p.tj * p.splits * B;
-    hipLaunchKernelGGL(split_gemm_f32_kernel<BCOL>, dim3((unsigned)grid), dim3(kNT), 0, s, p);
-    hipError_t e = hipGetLastError();
+    const bool dma = g_gemm_dma && p.vec && K % kBK == 0 && (!BCOL || NJ % 4 == 0);
+    hipError_t e;
+    if (dma) {
+        static std::atomic<unsigned long long> done{0};
+        e = ensure_lds_limit((const void *)split_gemm_f32_kernel<BCOL, true>, gemm_lds_bytes<true>(), done);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, true>), dim3((unsigned)grid), dim3(kNT), gemm_lds_bytes<true>(), s, p);
+    } else {
+        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, false>), dim3((unsigned)grid), dim3(kNT), gemm_lds_bytes<false>(), s, p);
+    }
+    e = hipGetLastError();
     if (e != hipSuccess || p.direct) return e;
     return launch_splitk_reduce(slab, C, p.splits, (size_t)B * NI * NJ, sD, s);
 }

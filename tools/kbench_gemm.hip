@@ -1,6 +1,7 @@
 // kbench_gemm.hip — the backward split GEMMs (corr_bwd_split.hip) at the train shape (B 8,
 // D 256, 36x48): dF1 = F2 dC^T (row operands) and dF2 = F1 dC (dC columns), each with its
-// split-K reduce, for several split counts (HIP events around back-to-back launches).
+// split-K reduce, for several split counts, register-staged vs LDS-DMA operand ring (HIP events
+// around back-to-back launches; results against the register-staged plan, which must match bitwise).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++20 -ffp-contract=off -o tools/_build/kbench_gemm tools/kbench_gemm.hip \
 //         e-raft_amd/csrc/corr_bwd.hip e-raft_amd/csrc/corr_build.hip e-raft_amd/csrc/corr_lookup.hip
 #include <algorithm>
@@ -74,8 +75,10 @@ int main(int argc, char **argv) {
     auto g2 = [&](float *out) {
         return gemm_f32<true>(f1, (long)D * NQ, NQ, dc, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, out, w.slab, 0);
     };
+    g_gemm_dma = 0;  // reference: the register-staged kernel
     CK(g1(r1));
     CK(g2(r2));
+    g_gemm_dma = 1;
     struct V {
         std::string name;
         std::function<hipError_t()> run;
@@ -83,19 +86,27 @@ int main(int argc, char **argv) {
         std::vector<float> us;
     };
     std::vector<V> vs;
-    for (int sp : {0, 1, 2, 3, 4, 6, 8}) {
-        vs.push_back({"dF1 (rows) splits " + std::string(sp ? std::to_string(sp) : "plan"), [&, sp] {
-                          g_gemm_splits = sp;
-                          const hipError_t e = g1(o1);
-                          g_gemm_splits = 0;
-                          return e;
-                      }, o1, r1, {}});
-        vs.push_back({"dF2 (cols) splits " + std::string(sp ? std::to_string(sp) : "plan"), [&, sp] {
-                          g_gemm_splits = sp;
-                          const hipError_t e = g2(o2);
-                          g_gemm_splits = 0;
-                          return e;
-                      }, o2, r2, {}});
+    for (int dma : {0, 1})
+        for (int sp : {0, 2, 3, 4, 6}) {
+            const std::string tag = std::string(dma ? "DMA " : "reg ") + "splits " + (sp ? std::to_string(sp) : "plan");
+            vs.push_back({"dF1 (rows) " + tag, [&, sp, dma] {
+                              g_gemm_splits = sp, g_gemm_dma = dma;
+                              const hipError_t e = g1(o1);
+                              g_gemm_splits = 0, g_gemm_dma = 1;
+                              return e;
+                          }, o1, r1, {}});
+            vs.push_back({"dF2 (cols) " + tag, [&, sp, dma] {
+                              g_gemm_splits = sp, g_gemm_dma = dma;
+                              const hipError_t e = g2(o2);
+                              g_gemm_splits = 0, g_gemm_dma = 1;
+                              return e;
+                          }, o2, r2, {}});
+        }
+    if (argc > 2) {  // only the variant named exactly argv[2] (PMC passes)
+        std::vector<V> keep;
+        for (auto &v : vs)
+            if (v.name == argv[2]) keep.push_back(v);
+        vs = keep;
     }
     for (auto &v : vs) {
         CK(v.run());
@@ -109,7 +120,7 @@ int main(int argc, char **argv) {
         float dm, rm;
         std::memcpy(&dm, &hv[0], 4);
         std::memcpy(&rm, &hv[1], 4);
-        printf("%-28s max|x - plan| / max|plan| = %.3e\n", v.name.c_str(), dm / rm);
+        printf("%-32s max|x - reg plan| / max|reg plan| = %.3e\n", v.name.c_str(), dm / rm);
     }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -129,7 +140,7 @@ int main(int argc, char **argv) {
     for (auto &v : vs) {
         std::sort(v.us.begin(), v.us.end());
         const float med = v.us[v.us.size() / 2];
-        printf("%-28s median %8.2f us  min %8.2f us  %6.3f of 2.5 PF f16 pipe (x3)\n", v.name.c_str(), med, v.us[0],
+        printf("%-32s median %8.2f us  min %8.2f us  %6.3f of 2.5 PF f16 pipe (x3)\n", v.name.c_str(), med, v.us[0],
                3.0 * fl / (med * 1e-6) / 2.5e15);
     }
     return 0;
