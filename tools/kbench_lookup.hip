@@ -115,21 +115,19 @@ int main(int argc, char **argv) {
         vs.push_back({"prod launch_lookup", [=](float *o) { return launch_lookup(lp, coords, B, H * W, H, W, 4, 4, o, 0); }, {}});
         vs.push_back({"QB16", [=](float *o) { return launch_qb<16>(lp, coords, B, H, W, o); }, {}});
         vs.push_back({"QB32", [=](float *o) { return launch_qb<32>(lp, coords, B, H, W, o); }, {}});
-        vs.push_back({"QB64", [=](float *o) { return launch_qb<64>(lp, coords, B, H, W, o); }, {}});
-        vs.push_back({"QB8", [=](float *o) { return launch_qb<8>(lp, coords, B, H, W, o); }, {}});
-        // thread counts that fill whole waves (QB * 9 just below a multiple of 64)
-        vs.push_back({"QB7", [=](float *o) { return launch_qb<7>(lp, coords, B, H, W, o); }, {}});
-        vs.push_back({"QB14", [=](float *o) { return launch_qb<14>(lp, coords, B, H, W, o); }, {}});
-        vs.push_back({"QB28", [=](float *o) { return launch_qb<28>(lp, coords, B, H, W, o); }, {}});
-        vs.push_back({"QB56", [=](float *o) { return launch_qb<56>(lp, coords, B, H, W, o); }, {}});
+        // persistent workgroups walking the blocks, next block's coords prefetched (x1 / x2 the
+        // resident workgroup count)
+        for (int pm : {1, 2})
+            vs.push_back({"persist x" + std::to_string(pm), [=](float *o) {
+                              g_lookup_persist = pm;
+                              const hipError_t e = launch_lookup(lp, coords, B, H * W, H, W, 4, 4, o, 0);
+                              g_lookup_persist = 0;
+                              return e;
+                          }, {}});
         vs.push_back({"prod smooth-flow", [=](float *o) { return launch_lookup(lp, coords_s, B, H * W, H, W, 4, 4, o, 0); }, {}});
         vs.push_back({"prod grid (integer)", [=](float *o) { return launch_lookup(lp, coords_g, B, H * W, H, W, 4, 4, o, 0); }, {}});
         vs.push_back({"QB16 smooth-flow", [=](float *o) { return launch_qb<16>(lp, coords_s, B, H, W, o); }, {}});
         vs.push_back({"abl QB32 noload", [=](float *o) { return launch_qb<32, 1>(lp, coords, B, H, W, o); }, {}});
-        vs.push_back({"abl QB32 nostore", [=](float *o) { return launch_qb<32, 2>(lp, coords, B, H, W, o); }, {}});
-        vs.push_back({"abl QB32 nocoords", [=](float *o) { return launch_qb<32, 4>(lp, coords, B, H, W, o); }, {}});
-        vs.push_back({"abl QB32 load only", [=](float *o) { return launch_qb<32, 6>(lp, coords, B, H, W, o); }, {}});
-        vs.push_back({"abl QB32 nothing", [=](float *o) { return launch_qb<32, 7>(lp, coords, B, H, W, o); }, {}});
         CK(vs[0].launch(ref));
         for (auto &v : vs) {
             CK(hipMemset(out, 0, n_out * 4));
