@@ -340,38 +340,6 @@ __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
                                  [&](int j, float acc) { o[(size_t)j * N] = acc; });
 }
 
-// Persistent form (measurement A/B, tools/kbench_lookup.hip): gridDim.x workgroups walk the
-// blocks t = blockIdx.x + k gridDim.x (level-major, as lookup_kernel's grid is dispatched); the
-// next block's coords are loaded while this block gathers, so a workgroup's second block starts
-// without the coords round trip.  Same bits as lookup_kernel.
-template <int S, int QB>
-__global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_persist_kernel(
-    ConstLevelPtrs pyr, const float *__restrict__ coords, int B, int NQ, int H, int W, int L,
-    float *__restrict__ out, int nblk) {
-    constexpr int K = S * S, NT = lookup_threads(S, QB);
-    __shared__ LookupSmem<S, QB> sm;
-    const int N = NQ, nqb = (N + QB - 1) / QB, per = nqb * B;
-    const int tid = threadIdx.x, i = tid / QB, q = tid % QB;
-    auto load_coords = [&](int t, float &cx, float &cy) {
-        const int x = t % per, b = x / nqb, n = (x - b * nqb) * QB + q;
-        const bool ok = i < S && n < N;
-        cx = ok ? coords[((size_t)b * 2 + 0) * N + n] : 0.0f;
-        cy = ok ? coords[((size_t)b * 2 + 1) * N + n] : 0.0f;
-    };
-    float cx = 0.f, cy = 0.f;
-    if ((int)blockIdx.x < nblk) load_coords(blockIdx.x, cx, cy);
-    for (int t = blockIdx.x; t < nblk; t += gridDim.x) {
-        float ncx = 0.f, ncy = 0.f;
-        if (t + (int)gridDim.x < nblk) load_coords(t + gridDim.x, ncx, ncy);
-        const int l = t / per, x = t - l * per, b = x / nqb, n0 = (x - b * nqb) * QB;
-        float *o = out + (((size_t)b * L + l) * K + (size_t)i * S) * N + n0 + q;
-        lookup_block_v<S, QB, NT, 0>(sm, pyr.p[l], cx, cy, b, n0, N, H, W, l, tid,
-                                     [&](int j, float acc) { o[(size_t)j * N] = acc; });
-        __syncthreads();  // the next block rewrites the shared taps and windows
-        cx = ncx, cy = ncy;
-    }
-}
-
 // Lookup fused with the consumer's 1x1 convolution (BasicMotionEncoder.convc1, update.py:68,75:
 // cor = relu(convc1(corr)), L*K = 324 -> 256 channels), on the f16 MFMA pipe with the same
 // fp32-accurate split as the build: x = 2^-s (hi + lo), products lo.hi + hi.lo + hi.hi into an
@@ -1272,10 +1240,6 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const float *__restrict__
     }
 }
 
-// > 0: the persistent lookup on g_lookup_persist x the resident workgroups (tools/kbench_lookup.hip
-// A/B; 0 = one workgroup per block, the library default)
-int g_lookup_persist = 0;
-
 template <int S>
 hipError_t launch_lookup_s(const ConstLevelPtrs &pyr, const float *coords, int B, int NQ, int H,
                            int W, int L, float *out, hipStream_t s) {
@@ -1283,31 +1247,14 @@ hipError_t launch_lookup_s(const ConstLevelPtrs &pyr, const float *coords, int B
     // <= 2048 cells, where the smaller workgroups pack the CUs better (same bits; tools/kbench_lookup:
     // train 36x48 12.5 vs 12.8 us, MVSEC 36x44 B16 19.6 vs 20.3, DSEC 60x80 equal, 1280x960 23.8
     // vs 22.4)
-    auto persist = [&](auto qb_tag) {
-        constexpr int QB = decltype(qb_tag)::value;
-        const int nblk = (NQ + QB - 1) / QB * B * L;
-        int per_cu = 0, cus = 0, dev = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e == hipSuccess)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)lookup_persist_kernel<S, QB>,
-                                                            lookup_threads(S, QB), 0);
-        if (e != hipSuccess) return e;
-        const int grid = std::min(nblk, std::max(1, per_cu * cus * g_lookup_persist));
-        hipLaunchKernelGGL((lookup_persist_kernel<S, QB>), dim3(grid), dim3(lookup_threads(S, QB)), 0, s, pyr, coords,
-                           B, NQ, H, W, L, out, nblk);
-        return hipGetLastError();
-    };
     if (S == 9 && H * W <= 2048) {
         constexpr int QB = 16;
-        if (g_lookup_persist) return persist(std::integral_constant<int, QB>{});
         const int nqb = (NQ + QB - 1) / QB;
         hipLaunchKernelGGL((lookup_kernel<S, QB>), dim3(nqb * B, L), dim3(lookup_threads(S, QB)), 0, s,
                            pyr, coords, B, NQ, H, W, L, out);
         return hipGetLastError();
     }
     constexpr int QB = 32;
-    if (g_lookup_persist) return persist(std::integral_constant<int, QB>{});
     const int nqb = (NQ + QB - 1) / QB;
     hipLaunchKernelGGL((lookup_kernel<S, QB>), dim3(nqb * B, L), dim3(lookup_threads(S, QB)), 0, s,
                        pyr, coords, B, NQ, H, W, L, out);

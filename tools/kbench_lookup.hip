@@ -115,15 +115,6 @@ int main(int argc, char **argv) {
         vs.push_back({"prod launch_lookup", [=](float *o) { return launch_lookup(lp, coords, B, H * W, H, W, 4, 4, o, 0); }, {}});
         vs.push_back({"QB16", [=](float *o) { return launch_qb<16>(lp, coords, B, H, W, o); }, {}});
         vs.push_back({"QB32", [=](float *o) { return launch_qb<32>(lp, coords, B, H, W, o); }, {}});
-        // persistent workgroups walking the blocks, next block's coords prefetched (x1 / x2 the
-        // resident workgroup count)
-        for (int pm : {1, 2})
-            vs.push_back({"persist x" + std::to_string(pm), [=](float *o) {
-                              g_lookup_persist = pm;
-                              const hipError_t e = launch_lookup(lp, coords, B, H * W, H, W, 4, 4, o, 0);
-                              g_lookup_persist = 0;
-                              return e;
-                          }, {}});
         vs.push_back({"prod smooth-flow", [=](float *o) { return launch_lookup(lp, coords_s, B, H * W, H, W, 4, 4, o, 0); }, {}});
         vs.push_back({"prod grid (integer)", [=](float *o) { return launch_lookup(lp, coords_g, B, H * W, H, W, 4, 4, o, 0); }, {}});
         vs.push_back({"QB16 smooth-flow", [=](float *o) { return launch_qb<16>(lp, coords_s, B, H, W, o); }, {}});
