@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "corr_build_common.h"
 
@@ -390,7 +391,18 @@ constexpr int gemm_lds_bytes() {
 // chunk's loads have two MFMA phases to land); each chunk is then split LDS -> registers -> the
 // hi/lo staging (the same split and layout as the register path, so the same bits).  Needs 16-B
 // aligned operands, K % 16 == 0 and (BCOL) NJ % 4 == 0.
-template <bool BCOL, bool DMA = false>
+// lo = f16(y - f32(h)) of an element pair in two VOP3P instructions: v_fma_mix{lo,hi}_f16 take
+// h as f16 and y as f32, and y - h is exact in f32 (h is y rounded to 11 bits), so the one
+// rounding to f16 gives the same bits as converting h back, subtracting and converting.
+__device__ __forceinline__ unsigned split_lo_mix(unsigned h2, float y0, float y1) {
+    unsigned lo;
+    asm volatile("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(lo) : "v"(h2), "v"(y0));
+    asm volatile("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(h2), "v"(y1));
+    return lo;
+}
+
+// MIX = false: the lo half by convert back + subtract + convert (measurement A/B only).
+template <bool BCOL, bool DMA = false, bool MIX = true>
 __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
     extern __shared__ __attribute__((aligned(16))) u32x4 gemm_smem[];
     u32x4 *lds = gemm_smem;
@@ -503,7 +515,10 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
                 for (int t = 0; t < 4; ++t) {
                     const f32x2v y = f32x2v{v[2 * t], v[2 * t + 1]} * f32x2v{f, f};
                     h[t] = __builtin_convertvector(y, half2v);
-                    l[t] = __builtin_convertvector(y - __builtin_convertvector(h[t], f32x2v), half2v);
+                    if constexpr (MIX)
+                        l[t] = __builtin_bit_cast(half2v, split_lo_mix(__builtin_bit_cast(unsigned, h[t]), y[0], y[1]));
+                    else
+                        l[t] = __builtin_convertvector(y - __builtin_convertvector(h[t], f32x2v), half2v);
                 }
             } else {
 #pragma unroll
@@ -698,6 +713,7 @@ constexpr long kGemmSlots = 512;
 
 int g_gemm_splits = 0;  // measurement override of the split count (tools/kbench_gemm.hip); 0 = plan
 int g_gemm_dma = 1;     // LDS-DMA operand ring when the shape allows (tools/kbench_gemm.hip A/B)
+int g_gemm_mix = 1;     // lo halves by v_fma_mix (0: convert back + subtract; CORR_GEMM_AB builds only)
 
 int plan_split_k(int NI, int NJ, int nkc, int batch) {
     if (g_gemm_splits > 0) return g_gemm_splits;
@@ -798,14 +814,22 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     const long grid = (long)p.ti * p.tj * p.splits * B;
     const bool dma = g_gemm_dma && p.vec && K % kBK == 0 && (!BCOL || NJ % 4 == 0);
     hipError_t e;
-    if (dma) {
+    auto go = [&](auto dma_tag, auto mix_tag) {
+        constexpr bool D = decltype(dma_tag)::value, M = decltype(mix_tag)::value;
         static std::atomic<unsigned long long> done{0};
-        e = ensure_lds_limit((const void *)split_gemm_f32_kernel<BCOL, true>, gemm_lds_bytes<true>(), done);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, true>), dim3((unsigned)grid), dim3(kNT), gemm_lds_bytes<true>(), s, p);
-    } else {
-        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, false>), dim3((unsigned)grid), dim3(kNT), gemm_lds_bytes<false>(), s, p);
-    }
+        hipError_t e2 = ensure_lds_limit((const void *)split_gemm_f32_kernel<BCOL, D, M>, gemm_lds_bytes<D>(), done);
+        if (e2 != hipSuccess) return e2;
+        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, D, M>), dim3((unsigned)grid), dim3(kNT), gemm_lds_bytes<D>(), s, p);
+        return hipSuccess;
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+#ifdef CORR_GEMM_AB  // tools/kbench_gemm.hip: the convert-back split as well
+    if (!g_gemm_mix) e = dma ? go(T_{}, F_{}) : go(F_{}, F_{});
+    else
+#endif
+    e = dma ? go(T_{}, T_{}) : go(F_{}, T_{});
+    if (e != hipSuccess) return e;
     e = hipGetLastError();
     if (e != hipSuccess || p.direct) return e;
     return launch_splitk_reduce(slab, C, p.splits, (size_t)B * NI * NJ, sD, s);

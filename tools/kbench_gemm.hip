@@ -12,6 +12,7 @@
 #include <string>
 #include <vector>
 
+#define CORR_GEMM_AB
 #include "../e-raft_amd/csrc/corr_bwd_split.hip"
 
 using namespace corr;
@@ -75,10 +76,10 @@ int main(int argc, char **argv) {
     auto g2 = [&](float *out) {
         return gemm_f32<true>(f1, (long)D * NQ, NQ, dc, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, out, w.slab, 0);
     };
-    g_gemm_dma = 0;  // reference: the register-staged kernel
+    g_gemm_dma = 0, g_gemm_mix = 0;  // reference: the register-staged kernel, convert-back split
     CK(g1(r1));
     CK(g2(r2));
-    g_gemm_dma = 1;
+    g_gemm_dma = 1, g_gemm_mix = 1;
     struct V {
         std::string name;
         std::function<hipError_t()> run;
@@ -87,21 +88,23 @@ int main(int argc, char **argv) {
     };
     std::vector<V> vs;
     for (int dma : {0, 1})
-        for (int sp : {0, 2, 3, 4, 6}) {
-            const std::string tag = std::string(dma ? "DMA " : "reg ") + "splits " + (sp ? std::to_string(sp) : "plan");
-            vs.push_back({"dF1 (rows) " + tag, [&, sp, dma] {
-                              g_gemm_splits = sp, g_gemm_dma = dma;
-                              const hipError_t e = g1(o1);
-                              g_gemm_splits = 0, g_gemm_dma = 1;
-                              return e;
-                          }, o1, r1, {}});
-            vs.push_back({"dF2 (cols) " + tag, [&, sp, dma] {
-                              g_gemm_splits = sp, g_gemm_dma = dma;
-                              const hipError_t e = g2(o2);
-                              g_gemm_splits = 0, g_gemm_dma = 1;
-                              return e;
-                          }, o2, r2, {}});
-        }
+        for (int mix : {0, 1})
+            for (int sp : {0}) {
+                const std::string tag = std::string(dma ? "DMA " : "reg ") + (mix ? "mix " : "cvt ") + "splits " +
+                                        (sp ? std::to_string(sp) : "plan");
+                vs.push_back({"dF1 (rows) " + tag, [&, sp, dma, mix] {
+                                  g_gemm_splits = sp, g_gemm_dma = dma, g_gemm_mix = mix;
+                                  const hipError_t e = g1(o1);
+                                  g_gemm_splits = 0, g_gemm_dma = 1, g_gemm_mix = 1;
+                                  return e;
+                              }, o1, r1, {}});
+                vs.push_back({"dF2 (cols) " + tag, [&, sp, dma, mix] {
+                                  g_gemm_splits = sp, g_gemm_dma = dma, g_gemm_mix = mix;
+                                  const hipError_t e = g2(o2);
+                                  g_gemm_splits = 0, g_gemm_dma = 1, g_gemm_mix = 1;
+                                  return e;
+                              }, o2, r2, {}});
+            }
     if (argc > 2) {  // only the variant named exactly argv[2] (PMC passes)
         std::vector<V> keep;
         for (auto &v : vs)
@@ -120,7 +123,7 @@ int main(int argc, char **argv) {
         float dm, rm;
         std::memcpy(&dm, &hv[0], 4);
         std::memcpy(&rm, &hv[1], 4);
-        printf("%-32s max|x - reg plan| / max|reg plan| = %.3e\n", v.name.c_str(), dm / rm);
+        printf("%-32s max|x - reg cvt plan| / max|ref| = %.3e\n", v.name.c_str(), dm / rm);
     }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
