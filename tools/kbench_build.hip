@@ -138,6 +138,9 @@ int main(int argc, char **argv) {
         vs.push_back({"x3 pack only", [&](float *) {
                           return launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0);
                       }, false});
+        vs.push_back({"x3 pack only px64", [&](float *) {
+                          return launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, 64);
+                      }, false});
         auto with_order = [&](int ord, std::function<hipError_t()> f) {
             g_tile_order = ord;
             const hipError_t e = f();
@@ -203,6 +206,21 @@ int main(int argc, char **argv) {
             same("1-tile no half path", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 2); });
             same("1-tile nopipe", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 1); });
 
+        }
+        {  // pack variants: byte-identical workspaces
+            void *ws2;
+            CK(hipMalloc(&ws2, wsb));
+            for (int px : {64}) {
+                CK(hipMemset(ws, 0, wsb));
+                CK(hipMemset(ws2, 0, wsb));
+                CK(launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0));
+                CK(launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws2, 0, px));
+                std::vector<unsigned char> ha(wsb), hb(wsb);
+                CK(hipMemcpy(ha.data(), ws, wsb, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(hb.data(), ws2, wsb, hipMemcpyDeviceToHost));
+                printf("%-10s pack px%d vs default: %s\n", sh.name, px, ha == hb ? "byte-identical" : "DIFFER");
+            }
+            CK(hipFree(ws2));
         }
         {  // pooling of the new kernel: every level bit-identical to avg_pool2d of its own level 0
             CK(launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), ws, 0));
