@@ -120,12 +120,6 @@ int main(int argc, char **argv) {
                           g_build_vec1 = true;
                           return e;
                       }, true});
-        vs.push_back({"f32 BK16 noskip", [&](float *o) {
-                          return launch_build_cfg<BuildCfg<2, 2, 2, 16, 4, true, false>>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
-                      }, true});
-        vs.push_back({"f32 4x1x2 BK16 noskip", [&](float *o) {
-                          return launch_build_cfg<BuildCfg<4, 1, 2, 16, 4, true, false>>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
-                      }, true});
         vs.push_back({"f32 level 0 only", [&](float *o) {
                           return launch_build_cfg<BuildDefault>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 1, lp_of(o), 0);
                       }, false});
