@@ -269,12 +269,8 @@ __global__ __launch_bounds__(256) void pool_fold_max_kernel(FoldArgs a) {
 constexpr int kCmCols = 64, kCmSlices = 16;
 
 __global__ __launch_bounds__(kCmCols *kCmSlices) void colmax_reduce_kernel(const float *__restrict__ part, int G, int N,
-                                                                         unsigned *__restrict__ cmax,
-                                                                         int *__restrict__ tickets, int ntickets) {
+                                                                         unsigned *__restrict__ cmax) {
     __shared__ float red[kCmSlices][kCmCols];
-    // the GEMMs' split-K tickets start at 0 (workgroup (0, 0); the GEMMs run after this kernel)
-    if (blockIdx.x == 0 && blockIdx.y == 0)
-        for (int t = threadIdx.x; t < ntickets; t += blockDim.x) tickets[t] = 0;
     const int b = blockIdx.y, c = threadIdx.x % kCmCols, sl = threadIdx.x / kCmCols;
     const int m = blockIdx.x * kCmCols + c;
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -365,12 +361,6 @@ struct FGemmParams {
     int ti, tj, splits, kc_per;
     float alpha;
     int direct, vec;  // vec: 16-B loads legal (strides / bases / K multiples of 4)
-    // fused split-K reduce: the last split of a tile to finish (ticket) sums the slabs in split
-    // order into out, as splitk_reduce_kernel does (null: the separate reduce kernel)
-    int *tickets;
-    float *out;
-    float sD;
-    int exact;
 };
 
 typedef __attribute__((address_space(3))) void gemm_lds_t;
@@ -713,30 +703,6 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
             }
         }
     }
-    if (p.tickets) {
-        // Release this split's slab at agent scope (every thread: its own stores), then take a
-        // ticket; the split that draws the last one acquires and sums the tile's slabs in split
-        // order — splitk_reduce_kernel's arithmetic, element for element.
-        __threadfence();
-        __syncthreads();
-        const int tile = (b * p.ti + ti) * p.tj + tj;
-        if (tid == 0) lex[0] = atomicAdd(&p.tickets[tile], 1);
-        __syncthreads();
-        if (lex[0] == p.splits - 1) {
-            __threadfence();
-            const size_t base = (size_t)b * p.NI * p.NJ;
-            const int ni = min(kTI, p.NI - i0), nj = min(kTJ, p.NJ - j0);
-            for (int e = tid; e < kTI * kTJ; e += kNT) {
-                const int il = e / kTJ, jl = e - il * kTJ;
-                if (il >= ni || jl >= nj) continue;
-                const size_t off = base + (size_t)(i0 + il) * p.NJ + j0 + jl;
-                float a = p.C[off];
-                for (int k = 1; k < p.splits; ++k) a = a + p.C[(size_t)k * slab + off];
-                p.out[off] = p.exact ? a * p.alpha : a / p.sD;
-            }
-            if (tid == 0) p.tickets[tile] = 0;  // ready for the next GEMM of the call
-        }
-    }
 }
 
 // Split-K so that tiles x splits fills ONE wave of workgroup slots (MI355X: 256 CUs x 2
@@ -748,7 +714,6 @@ constexpr long kGemmSlots = 512;
 int g_gemm_splits = 0;  // measurement override of the split count (tools/kbench_gemm.hip); 0 = plan
 int g_gemm_dma = 1;     // LDS-DMA operand ring when the shape allows (tools/kbench_gemm.hip A/B)
 int g_gemm_mix = 1;     // lo halves by v_fma_mix (0: convert back + subtract; CORR_GEMM_AB builds only)
-int g_gemm_fused_reduce = 1;  // split-K sum by the last split of each tile (0: splitk_reduce_kernel)
 
 int plan_split_k(int NI, int NJ, int nkc, int batch) {
     if (g_gemm_splits > 0) return g_gemm_splits;
@@ -763,8 +728,6 @@ inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 struct BwdWs {
     unsigned *mxA, *mxB, *mxC, *mxA2;  // row max of F2, of dC rows, column max of dC, row max of F1
     unsigned *mx0;                     // start of the four (contiguous, zeroed once per call)
-    int *tickets;                      // split-K tickets, one per GEMM tile (zeroed with the maxima)
-    int ntickets;
     size_t mx_bytes;
     float *slab;                       // split-K partial sums
 };
@@ -782,9 +745,6 @@ BwdWs carve(void *ws, int B, int D, int NQ, int N) {
     w += al256((size_t)B * R * 4);
     r.mxA2 = (unsigned *)w;
     w += al256((size_t)B * D * 4);
-    r.tickets = (int *)w;
-    r.ntickets = (int)(((D + kTI - 1) / kTI) * ((R + kTJ - 1) / kTJ) * (size_t)B);
-    w += al256((size_t)r.ntickets * 4);
     r.mx_bytes = (size_t)(w - (char *)r.mx0);
     r.slab = (float *)w;
     return r;
@@ -824,9 +784,7 @@ namespace {
 size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W) {
     const int N = H * W;
     const size_t R = std::max(NQ, N);
-    const size_t tickets = ((D + kTI - 1) / kTI) * ((R + kTJ - 1) / kTJ) * (size_t)B;
-    return 2 * al256((size_t)B * D * 4) + 2 * al256((size_t)B * R * 4) + al256(tickets * 4) +
-           slab_floats(B, D, NQ, N) * sizeof(float);
+    return 2 * al256((size_t)B * D * 4) + 2 * al256((size_t)B * R * 4) + slab_floats(B, D, NQ, N) * sizeof(float);
 }
 
 // The GEMMs once dC's row maxima (w.mxB) and column maxima (w.mxC) are in the workspace.
@@ -834,7 +792,7 @@ size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W) {
 template <bool BCOL>
 hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long b_sb, long b_sr, long b_sk,
                     const unsigned *mxA, const unsigned *mxB, int B, int NI, int NJ, int K, float sD, float *C,
-                    float *slab, hipStream_t s, int *tickets = nullptr) {
+                    float *slab, hipStream_t s) {
     FGemmParams p{};
     p.A = A, p.a_sb = a_sb, p.a_sr = a_sr;
     p.Bm = Bm, p.b_sb = b_sb, p.b_sr = b_sr, p.b_sk = b_sk;
@@ -850,8 +808,6 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     p.alpha = 1.0f / sD;
     p.direct = p.splits == 1 && exact;
     p.C = p.direct ? C : slab;
-    p.tickets = (!p.direct && g_gemm_fused_reduce) ? tickets : nullptr;
-    p.out = C, p.sD = sD, p.exact = exact ? 1 : 0;
     auto al16 = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
     p.vec = al16(A) && al16(Bm) && a_sb % 4 == 0 && a_sr % 4 == 0 && b_sb % 4 == 0 &&
             (BCOL ? b_sk % 4 == 0 : b_sr % 4 == 0);
@@ -875,7 +831,7 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     e = dma ? go(T_{}, T_{}) : go(F_{}, T_{});
     if (e != hipSuccess) return e;
     e = hipGetLastError();
-    if (e != hipSuccess || p.direct || p.tickets) return e;
+    if (e != hipSuccess || p.direct) return e;
     return launch_splitk_reduce(slab, C, p.splits, (size_t)B * NI * NJ, sD, s);
 }
 
@@ -890,11 +846,10 @@ hipError_t bwd_split_gemms(const float *grad_c, const float *f1, int NQ, const f
     if ((e = (x)) != hipSuccess) return e;
     if (!rowmax_done) CK_(rowmax2(f2, N, w.mxA, f1, NQ, w.mxA2, B, D, s));
     // dF1 = F2 . dC^T : A = F2 rows d (k = m), B = dC rows n (k = m)
-    CK_(gemm_f32<false>(f2, (long)D * N, N, grad_c, (long)NQ * N, N, 1, w.mxA, w.mxB, B, D, NQ, N, sD, df1, w.slab, s,
-                        w.tickets));
+    CK_(gemm_f32<false>(f2, (long)D * N, N, grad_c, (long)NQ * N, N, 1, w.mxA, w.mxB, B, D, NQ, N, sD, df1, w.slab, s));
     // dF2 = F1 . dC : A = F1 rows d (k = n), B = dC columns m (k = n)
     CK_(gemm_f32<true>(f1, (long)D * NQ, NQ, grad_c, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, df2, w.slab,
-                       s, w.tickets));
+                       s));
 #undef CK_
     return hipSuccess;
 }
@@ -974,7 +929,7 @@ hipError_t launch_backward(int algo, const float *const *coords, const float *co
         if (e == hipSuccess) {
             if (algo == CORR_BUILD_F16X3) {
                 hipLaunchKernelGGL(colmax_reduce_kernel, dim3((unsigned)((N + kCmCols - 1) / kCmCols), (unsigned)B),
-                                   dim3(kCmCols * kCmSlices), 0, s, cpart, G, N, cmax, w.tickets, w.ntickets);
+                                   dim3(kCmCols * kCmSlices), 0, s, cpart, G, N, cmax);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 return bwd_split_gemms(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, w, s, true);
             }

@@ -1,8 +1,7 @@
 // kbench_gemm.hip — the backward split GEMMs (corr_bwd_split.hip) at the train shape (B 8,
 // D 256, 36x48): dF1 = F2 dC^T (row operands) and dF2 = F1 dC (dC columns), each with its
-// split-K reduce, for several split counts, with the split-K sum in a separate kernel or fused into
-// the GEMM (last split of each tile); results against the register-staged, convert-back,
-// reduce-kernel plan, which must match bitwise at the plan's split count.
+// split-K reduce, for several split counts, register-staged vs LDS-DMA operand ring (HIP events
+// around back-to-back launches; results against the register-staged plan, which must match bitwise).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++20 -ffp-contract=off -o tools/_build/kbench_gemm tools/kbench_gemm.hip \
 //         e-raft_amd/csrc/corr_bwd.hip e-raft_amd/csrc/corr_build.hip e-raft_amd/csrc/corr_lookup.hip
 #include <algorithm>
@@ -71,19 +70,16 @@ int main(int argc, char **argv) {
     CK(absmax(dc, B, NQ, N, w.mxB, w.mxC, 0));
     CK(rowmax2(f2, N, w.mxA, f1, NQ, w.mxA2, B, D, 0));
     const float sD = 16.0f;
-    CK(hipMemset(w.tickets, 0, (size_t)w.ntickets * 4));
     auto g1 = [&](float *out) {
-        return gemm_f32<false>(f2, (long)D * N, N, dc, (long)NQ * N, N, 1, w.mxA, w.mxB, B, D, NQ, N, sD, out, w.slab, 0,
-                               w.tickets);
+        return gemm_f32<false>(f2, (long)D * N, N, dc, (long)NQ * N, N, 1, w.mxA, w.mxB, B, D, NQ, N, sD, out, w.slab, 0);
     };
     auto g2 = [&](float *out) {
-        return gemm_f32<true>(f1, (long)D * NQ, NQ, dc, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, out, w.slab, 0,
-                              w.tickets);
+        return gemm_f32<true>(f1, (long)D * NQ, NQ, dc, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, out, w.slab, 0);
     };
-    g_gemm_dma = 0, g_gemm_mix = 0, g_gemm_fused_reduce = 0;  // reference: register-staged, convert-back, reduce kernel
+    g_gemm_dma = 0, g_gemm_mix = 0;  // reference: the register-staged kernel, convert-back split
     CK(g1(r1));
     CK(g2(r2));
-    g_gemm_dma = 1, g_gemm_mix = 1, g_gemm_fused_reduce = 1;
+    g_gemm_dma = 1, g_gemm_mix = 1;
     struct V {
         std::string name;
         std::function<hipError_t()> run;
@@ -91,23 +87,24 @@ int main(int argc, char **argv) {
         std::vector<float> us;
     };
     std::vector<V> vs;
-    for (int fr : {0, 1})
-        for (int sp : {0, 2, 3}) {
-            const std::string tag = std::string(fr ? "fused-reduce " : "reduce-kernel ") + "splits " +
-                                    (sp ? std::to_string(sp) : "plan");
-            vs.push_back({"dF1 (rows) " + tag, [&, sp, fr] {
-                              g_gemm_splits = sp, g_gemm_fused_reduce = fr;
-                              const hipError_t e = g1(o1);
-                              g_gemm_splits = 0, g_gemm_fused_reduce = 1;
-                              return e;
-                          }, o1, r1, {}});
-            vs.push_back({"dF2 (cols) " + tag, [&, sp, fr] {
-                              g_gemm_splits = sp, g_gemm_fused_reduce = fr;
-                              const hipError_t e = g2(o2);
-                              g_gemm_splits = 0, g_gemm_fused_reduce = 1;
-                              return e;
-                          }, o2, r2, {}});
-        }
+    for (int dma : {0, 1})
+        for (int mix : {0, 1})
+            for (int sp : {0}) {
+                const std::string tag = std::string(dma ? "DMA " : "reg ") + (mix ? "mix " : "cvt ") + "splits " +
+                                        (sp ? std::to_string(sp) : "plan");
+                vs.push_back({"dF1 (rows) " + tag, [&, sp, dma, mix] {
+                                  g_gemm_splits = sp, g_gemm_dma = dma, g_gemm_mix = mix;
+                                  const hipError_t e = g1(o1);
+                                  g_gemm_splits = 0, g_gemm_dma = 1, g_gemm_mix = 1;
+                                  return e;
+                              }, o1, r1, {}});
+                vs.push_back({"dF2 (cols) " + tag, [&, sp, dma, mix] {
+                                  g_gemm_splits = sp, g_gemm_dma = dma, g_gemm_mix = mix;
+                                  const hipError_t e = g2(o2);
+                                  g_gemm_splits = 0, g_gemm_dma = 1, g_gemm_mix = 1;
+                                  return e;
+                              }, o2, r2, {}});
+            }
     if (argc > 2) {  // only the variant named exactly argv[2] (PMC passes)
         std::vector<V> keep;
         for (auto &v : vs)
@@ -126,7 +123,7 @@ int main(int argc, char **argv) {
         float dm, rm;
         std::memcpy(&dm, &hv[0], 4);
         std::memcpy(&rm, &hv[1], 4);
-        printf("%-32s max|x - ref plan| / max|ref| = %.3e\n", v.name.c_str(), dm / rm);
+        printf("%-32s max|x - reg cvt plan| / max|ref| = %.3e\n", v.name.c_str(), dm / rm);
     }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
