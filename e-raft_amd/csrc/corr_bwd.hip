@@ -175,6 +175,27 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restr
     }
 }
 
+// The same sum, 16 B per lane (per_split % 4 == 0, 16-B aligned slabs and C): the split-K slabs
+// of one float4 are loaded together, each element summed in split order as above.
+__global__ __launch_bounds__(256) void splitk_reduce_vec4_kernel(const float4 *__restrict__ ws,
+                                                                 float4 *__restrict__ C, int splits,
+                                                                 size_t per4, float alpha, int exact_mul,
+                                                                 float s) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < per4;
+         i += (size_t)gridDim.x * blockDim.x) {
+        float4 acc = ws[i];
+        for (int k = 1; k < splits; ++k) {
+            const float4 v = ws[(size_t)k * per4 + i];
+            acc.x = acc.x + v.x, acc.y = acc.y + v.y, acc.z = acc.z + v.z, acc.w = acc.w + v.w;
+        }
+        if (exact_mul)
+            acc.x = acc.x * alpha, acc.y = acc.y * alpha, acc.z = acc.z * alpha, acc.w = acc.w * alpha;
+        else
+            acc.x = acc.x / s, acc.y = acc.y / s, acc.z = acc.z / s, acc.w = acc.w / s;
+        C[i] = acc;
+    }
+}
+
 int plan_splits(int M, int Nn, int K, int batch) {
     const long tiles = (long)((M + kBM - 1) / kBM) * ((Nn + kBN - 1) / kBN) * batch;
     long splits = (kTargetWG + tiles - 1) / tiles;
@@ -230,8 +251,17 @@ hipError_t run_gemm(bool b_kcontig, const float *A, const float *Bm, float *C, i
 
 }  // namespace
 
+int g_reduce_vec4 = 1;  // measurement override (tools/kbench_gemm.hip A/B): 0 = the scalar reduce
+
 // Ordered split-K sum + 1/sqrt(D) for corr_bwd_split.hip's slabs ([split][per] floats).
 hipError_t launch_splitk_reduce(const float *ws, float *C, int splits, size_t per, float sD, hipStream_t s) {
+    if (per % 4 == 0 && ((uintptr_t)ws & 15) == 0 && ((uintptr_t)C & 15) == 0 && g_reduce_vec4) {
+        const size_t per4 = per / 4;
+        const int grid = (int)std::min<size_t>((per4 + 255) / 256, 8192);
+        hipLaunchKernelGGL(splitk_reduce_vec4_kernel, dim3(grid), dim3(256), 0, s, (const float4 *)ws, (float4 *)C,
+                           splits, per4, 1.0f / sD, is_pow2(sD) ? 1 : 0, sD);
+        return hipGetLastError();
+    }
     const int grid = (int)std::min<size_t>((per + 255) / 256, 8192);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, ws, C, splits, per, 1.0f / sD,
                        is_pow2(sD) ? 1 : 0, sD);

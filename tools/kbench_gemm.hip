@@ -15,6 +15,9 @@
 #define CORR_GEMM_AB
 #include "../e-raft_amd/csrc/corr_bwd_split.hip"
 
+namespace corr {
+extern int g_reduce_vec4;  // corr_bwd.hip
+}
 using namespace corr;
 
 #define CK(x)                                                                                 \
@@ -76,10 +79,10 @@ int main(int argc, char **argv) {
     auto g2 = [&](float *out) {
         return gemm_f32<true>(f1, (long)D * NQ, NQ, dc, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, out, w.slab, 0);
     };
-    g_gemm_dma = 0, g_gemm_mix = 0;  // reference: the register-staged kernel, convert-back split
+    g_gemm_dma = 0, g_gemm_mix = 0, g_reduce_vec4 = 0;  // reference: register-staged, convert-back, scalar reduce
     CK(g1(r1));
     CK(g2(r2));
-    g_gemm_dma = 1, g_gemm_mix = 1;
+    g_gemm_dma = 1, g_gemm_mix = 1, g_reduce_vec4 = 1;
     struct V {
         std::string name;
         std::function<hipError_t()> run;
@@ -87,24 +90,21 @@ int main(int argc, char **argv) {
         std::vector<float> us;
     };
     std::vector<V> vs;
-    for (int dma : {0, 1})
-        for (int mix : {0, 1})
-            for (int sp : {0}) {
-                const std::string tag = std::string(dma ? "DMA " : "reg ") + (mix ? "mix " : "cvt ") + "splits " +
-                                        (sp ? std::to_string(sp) : "plan");
-                vs.push_back({"dF1 (rows) " + tag, [&, sp, dma, mix] {
-                                  g_gemm_splits = sp, g_gemm_dma = dma, g_gemm_mix = mix;
-                                  const hipError_t e = g1(o1);
-                                  g_gemm_splits = 0, g_gemm_dma = 1, g_gemm_mix = 1;
-                                  return e;
-                              }, o1, r1, {}});
-                vs.push_back({"dF2 (cols) " + tag, [&, sp, dma, mix] {
-                                  g_gemm_splits = sp, g_gemm_dma = dma, g_gemm_mix = mix;
-                                  const hipError_t e = g2(o2);
-                                  g_gemm_splits = 0, g_gemm_dma = 1, g_gemm_mix = 1;
-                                  return e;
-                              }, o2, r2, {}});
-            }
+    for (int rv : {0, 1}) {
+        const std::string tag = std::string("DMA mix splits plan, reduce ") + (rv ? "vec4" : "scalar");
+        vs.push_back({"dF1 (rows) " + tag, [&, rv] {
+                          g_reduce_vec4 = rv;
+                          const hipError_t e = g1(o1);
+                          g_reduce_vec4 = 1;
+                          return e;
+                      }, o1, r1, {}});
+        vs.push_back({"dF2 (cols) " + tag, [&, rv] {
+                          g_reduce_vec4 = rv;
+                          const hipError_t e = g2(o2);
+                          g_reduce_vec4 = 1;
+                          return e;
+                      }, o2, r2, {}});
+    }
     if (argc > 2) {  // only the variant named exactly argv[2] (PMC passes)
         std::vector<V> keep;
         for (auto &v : vs)
