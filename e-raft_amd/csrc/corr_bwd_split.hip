@@ -406,18 +406,20 @@ __device__ __forceinline__ void gemm_dma16(const void *g, uint32_t lds) {
 
 template <int N>
 __device__ __forceinline__ void gemm_wait_vm_barrier() {
-    static_assert(N == 0 || N == 6, "vmcnt immediates of the DMA ring (6 pieces per wave per chunk)");
+    static_assert(N == 0 || N == 4 || N == 6, "vmcnt immediates of the DMA ring (pieces per wave per chunk)");
     if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // Dynamic LDS of the GEMM: the hi/lo staging (2 stages; DMA: 1), the row exponents, and (DMA)
 // a 2-slot ring of raw fp32 chunks (kRows rows x 16 k; BCOL: B as 16 k-rows x 256 columns).
 constexpr int kRawFloats = kRows * kBK;  // per ring slot
-template <bool DMA>
+template <bool DMA, int WI = kWI>
 constexpr int gemm_lds_bytes() {
-    return (DMA ? 1 : 2) * kRows * 4 * (int)sizeof(u32x4) + kRows * (int)sizeof(int) +
-           (DMA ? 2 * kRawFloats * (int)sizeof(float) : 0);
+    constexpr int rows = 32 * kMI * WI + kTJ;
+    return (DMA ? 1 : 2) * rows * 4 * (int)sizeof(u32x4) + rows * (int)sizeof(int) +
+           (DMA ? 2 * rows * kBK * (int)sizeof(float) : 0);
 }
 
 // DMA = true: the raw fp32 chunks arrive by LDS-DMA two chunks ahead (no register staging, so a
@@ -435,12 +437,20 @@ __device__ __forceinline__ unsigned split_lo_mix(unsigned h2, float y0, float y1
 }
 
 // MIX = false: the lo half by convert back + subtract + convert (measurement A/B only).
-template <bool BCOL, bool DMA = false, bool MIX = true>
-__global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
+template <bool BCOL, bool DMA = false, bool MIX = true, int WI = kWI>
+__global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmParams p) {
+    // WI = 4 (DMA path only): 8 waves, a 256 x 256 tile (each wave still 64 x 128), so every
+    // staged element feeds twice the MFMAs
+    static_assert(WI == kWI || (WI == 4 && DMA), "the wide tile exists on the DMA path only");
+    constexpr int TI = 32 * kMI * WI, NT = 64 * WI * kWJ, ROWS = TI + kTJ;
+    constexpr int UB = 2 * kTJ / NT;      // B row-octets per thread (BCOL = false)
+    constexpr int KO = 2 * kTJ / NT;      // B k-octets per thread (BCOL = true; column tid % kTJ)
+    constexpr int NW = NT / 64, PB = 16 / NW;  // waves; B DMA pieces per wave and chunk
+    static_assert(TI == NT / 2, "one A row-octet per thread");
     extern __shared__ __attribute__((aligned(16))) u32x4 gemm_smem[];
     u32x4 *lds = gemm_smem;
-    int *lex = reinterpret_cast<int *>(gemm_smem + (DMA ? 1 : 2) * kRows * 4);
-    float *raw = reinterpret_cast<float *>(lex + kRows);
+    int *lex = reinterpret_cast<int *>(gemm_smem + (DMA ? 1 : 2) * ROWS * 4);
+    float *raw = reinterpret_cast<float *>(lex + ROWS);
     int id = xcd_swizzle(blockIdx.x, gridDim.x);
     const int tj = id % p.tj;
     id /= p.tj;
@@ -448,15 +458,15 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
     id /= p.ti;
     const int split = id % p.splits;
     const int b = id / p.splits;
-    const int i0 = ti * kTI, j0 = tj * kTJ;
+    const int i0 = ti * TI, j0 = tj * kTJ;
     const int kc0 = split * p.kc_per, kc1 = min(p.nkc, kc0 + p.kc_per);
 
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
     const int wv = tid >> 6, wi = wv / kWJ, wj = wv % kWJ;
 
-    for (int row = tid; row < kRows; row += kNT) {
-        const unsigned m = row < kTI ? p.mxA[(size_t)b * p.NI + min(i0 + row, p.NI - 1)]
-                                     : p.mxB[(size_t)b * p.NJ + min(j0 + row - kTI, p.NJ - 1)];
+    for (int row = tid; row < ROWS; row += NT) {
+        const unsigned m = row < TI ? p.mxA[(size_t)b * p.NI + min(i0 + row, p.NI - 1)]
+                                     : p.mxB[(size_t)b * p.NJ + min(j0 + row - TI, p.NJ - 1)];
         lex[row] = -split_shift(__uint_as_float(m));
     }
     __syncthreads();
@@ -473,18 +483,19 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
     int sb[4];
     bool gb[4];
     int brow[2];
+    const int bcol = tid % kTJ, boct0 = (tid / kTJ) * KO;  // BCOL: column, first k-octet
     if (!BCOL) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            brow[u] = (tid >> 1) + 128 * u;
+        for (int u = 0; u < UB; ++u) {
+            brow[u] = (tid >> 1) + (NT / 2) * u;
             bp[u] = p.Bm + (size_t)b * p.b_sb + (size_t)min(j0 + brow[u], p.NJ - 1) * p.b_sr + aoct * 8;
-            sb[u] = -lex[kTI + brow[u]];
+            sb[u] = -lex[TI + brow[u]];
             gb[u] = row_inf(p.mxB, j0 + brow[u], p.NJ);
         }
     } else {
         bp[0] = p.Bm + (size_t)b * p.b_sb;  // + n * b_sk + j
-        sb[0] = -lex[kTI + tid];
-        gb[0] = row_inf(p.mxB, j0 + tid, p.NJ);
+        sb[0] = -lex[TI + bcol];
+        gb[0] = row_inf(p.mxB, j0 + bcol, p.NJ);
     }
     const bool vec = p.vec;
     // Fast staging (wave-uniform): no staged row has an inf max and every shift has a normal
@@ -493,7 +504,7 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
     bool slow_t = ga || sa > 127;
     if (!BCOL) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) slow_t = slow_t || gb[u] || sb[u] > 127;
+        for (int u = 0; u < UB; ++u) slow_t = slow_t || gb[u] || sb[u] > 127;
     } else {
         slow_t = slow_t || gb[0] || sb[0] > 127;
     }
@@ -502,7 +513,7 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
     const float fa = pow2f(fast ? sa : 0);
     float fb[2];
     fb[0] = pow2f(fast ? sb[0] : 0);
-    fb[1] = BCOL ? 1.0f : pow2f(fast ? sb[1] : 0);
+    fb[1] = (BCOL || UB < 2) ? 1.0f : pow2f(fast ? sb[1] : 0);
     // BCOL: two register sets — chunk c is loaded two iterations before its MFMAs (one iteration
     // before it is staged into LDS), so a load has two MFMA phases to arrive
     float ra0[8], rb0[16], ra1[8], rb1[16];
@@ -540,7 +551,7 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
         }
     };
     auto store_chunk = [&](int st, const float (&ra)[8], const float (&rb)[16]) {
-        u32x4 *S = lds + (size_t)st * kRows * 4;
+        u32x4 *S = lds + (size_t)st * ROWS * 4;
         auto split8 = [&](const float *v, int sh, bool guard, float f, u32x4 &hi, u32x4 &lo) {
             half2v h[4], l[4];
             if (fast) {
@@ -570,19 +581,19 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
         }
         if (!BCOL) {
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < UB; ++u) {
                 u32x4 hi, lo;
                 split8(rb + 8 * u, sb[u], gb[u], fb[u], hi, lo);
-                S[swz(kTI + brow[u], 2 * aoct)] = hi;
-                S[swz(kTI + brow[u], 2 * aoct + 1)] = lo;
+                S[swz(TI + brow[u], 2 * aoct)] = hi;
+                S[swz(TI + brow[u], 2 * aoct + 1)] = lo;
             }
         } else {
 #pragma unroll
-            for (int o = 0; o < 2; ++o) {  // this column's two k-octets
+            for (int o = 0; o < KO; ++o) {  // this thread's k-octets of its column
                 u32x4 hi, lo;
                 split8(rb + 8 * o, sb[0], gb[0], fb[0], hi, lo);
-                S[swz(kTI + tid, 2 * o)] = hi;
-                S[swz(kTI + tid, 2 * o + 1)] = lo;
+                S[swz(TI + bcol, 2 * (boct0 + o))] = hi;
+                S[swz(TI + bcol, 2 * (boct0 + o) + 1)] = lo;
             }
         }
     };
@@ -595,9 +606,9 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
 
-    const int arow0 = wi * (32 * kMI) + l32, brow0 = kTI + wj * (32 * kNJ) + l32;
+    const int arow0 = wi * (32 * kMI) + l32, brow0 = TI + wj * (32 * kNJ) + l32;
     auto mfma_chunk = [&](int st) {
-        const u32x4 *S = lds + (size_t)st * kRows * 4;
+        const u32x4 *S = lds + (size_t)st * ROWS * 4;
         half8 ah[kMI], al[kMI], bh[kNJ], bl[kNJ];
 #pragma unroll
         for (int m = 0; m < kMI; ++m) {
@@ -634,32 +645,32 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
             asrc[q] = p.A + (size_t)b * p.a_sb + (size_t)min(i0 + row, p.NI - 1) * p.a_sr + (lane & 3) * 4;
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < PB; ++q) {
             if (!BCOL) {
-                const int row = 16 * (4 * w + q) + (lane >> 2);
+                const int row = 16 * (PB * w + q) + (lane >> 2);
                 bsrc[q] = p.Bm + (size_t)b * p.b_sb + (size_t)min(j0 + row, p.NJ - 1) * p.b_sr + (lane & 3) * 4;
             } else {
-                bsrc[q] = p.Bm + (size_t)b * p.b_sb + (size_t)(4 * w + q) * p.b_sk + min(j0 + 4 * lane, p.NJ - 4);
+                bsrc[q] = p.Bm + (size_t)b * p.b_sb + (size_t)(PB * w + q) * p.b_sk + min(j0 + 4 * lane, p.NJ - 4);
             }
         }
         auto issue = [&](int kc, int slot) __attribute__((always_inline)) {
-            const uint32_t base = raw_base + slot * kRawFloats * 4;
+            const uint32_t base = raw_base + slot * (ROWS * kBK) * 4;
             const size_t ka = (size_t)kc * kBK, kb = BCOL ? (size_t)kc * kBK * p.b_sk : ka;
 #pragma unroll
             for (int q = 0; q < 2; ++q) gemm_dma16(asrc[q] + ka, base + (2 * w + q) * 1024);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) gemm_dma16(bsrc[q] + kb, base + kTI * kBK * 4 + (4 * w + q) * 1024);
+            for (int q = 0; q < PB; ++q) gemm_dma16(bsrc[q] + kb, base + TI * kBK * 4 + (PB * w + q) * 1024);
         };
         auto read_raw = [&](int slot) __attribute__((always_inline)) {
-            const float *R = raw + slot * kRawFloats;
+            const float *R = raw + slot * (ROWS * kBK);
             const float4 *ar = reinterpret_cast<const float4 *>(R + arow * kBK + aoct * 8);
             const float4 x0 = ar[0], x1 = ar[1];
             ra0[0] = x0.x, ra0[1] = x0.y, ra0[2] = x0.z, ra0[3] = x0.w;
             ra0[4] = x1.x, ra0[5] = x1.y, ra0[6] = x1.z, ra0[7] = x1.w;
-            const float *RB = R + kTI * kBK;
+            const float *RB = R + TI * kBK;
             if (!BCOL) {
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
+                for (int u = 0; u < UB; ++u) {
                     const float4 *br = reinterpret_cast<const float4 *>(RB + brow[u] * kBK + aoct * 8);
                     const float4 y0 = br[0], y1 = br[1];
                     rb0[8 * u + 0] = y0.x, rb0[8 * u + 1] = y0.y, rb0[8 * u + 2] = y0.z, rb0[8 * u + 3] = y0.w;
@@ -667,14 +678,14 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
                 }
             } else {
 #pragma unroll
-                for (int t = 0; t < 16; ++t) rb0[t] = RB[t * kTJ + tid];
+                for (int t = 0; t < 8 * KO; ++t) rb0[t] = RB[(8 * boct0 + t) * kTJ + bcol];
             }
         };
         if (kc0 < kc1) issue(kc0, 0);
         if (kc0 + 1 < kc1) issue(kc0 + 1, 1);
         for (int kc = kc0; kc < kc1; ++kc) {
             const int slot = (kc - kc0) & 1;
-            if (kc + 1 < kc1) gemm_wait_vm_barrier<6>();  // chunk kc landed (every wave's pieces)
+            if (kc + 1 < kc1) gemm_wait_vm_barrier<2 + PB>();  // chunk kc landed (every wave's pieces)
             else gemm_wait_vm_barrier<0>();
             read_raw(slot);
             store_chunk(0, ra0, rb0);
@@ -723,7 +734,7 @@ __global__ __launch_bounds__(kNT, 2) void split_gemm_f32_kernel(FGemmParams p) {
     for (int n = 0; n < kNJ; ++n) {
         const int jl = wj * (32 * kNJ) + 32 * n + l32;
         const int j = j0 + jl;
-        const int ej = lex[kTI + jl];
+        const int ej = lex[TI + jl];
 #pragma unroll
         for (int m = 0; m < kMI; ++m) {
 #pragma unroll
@@ -747,6 +758,7 @@ constexpr long kGemmSlots = 512;
 int g_gemm_splits = 0;  // measurement override of the split count (tools/kbench_gemm.hip); 0 = plan
 int g_gemm_dma = 1;     // LDS-DMA operand ring when the shape allows (tools/kbench_gemm.hip A/B)
 int g_gemm_mix = 1;     // lo halves by v_fma_mix (0: convert back + subtract; CORR_GEMM_AB builds only)
+int g_gemm_wide = 1;    // 256 x 256 tiles of 8 waves on the DMA path when NI > 128 (0: kbench A/B)
 
 int plan_split_k(int NI, int NJ, int nkc, int batch) {
     if (g_gemm_splits > 0) return g_gemm_splits;
@@ -844,24 +856,33 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     auto al16 = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
     p.vec = al16(A) && al16(Bm) && a_sb % 4 == 0 && a_sr % 4 == 0 && b_sb % 4 == 0 &&
             (BCOL ? b_sk % 4 == 0 : b_sr % 4 == 0);
-    const long grid = (long)p.ti * p.tj * p.splits * B;
     const bool dma = g_gemm_dma && p.vec && K % kBK == 0 && (!BCOL || NJ % 4 == 0);
+    // 256-row tiles when there are more than 128 rows (D = 256): every staged element feeds twice
+    // the MFMAs, a third less split work per MFMA (train: dF1 73 -> 67, dF2 75 -> 67 us)
+    const bool wide = dma && g_gemm_wide && NI > 32 * kMI * kWI;
     hipError_t e;
-    auto go = [&](auto dma_tag, auto mix_tag) {
+    auto go = [&](auto dma_tag, auto mix_tag, auto wi_tag) {
         constexpr bool D = decltype(dma_tag)::value, M = decltype(mix_tag)::value;
+        constexpr int WI = decltype(wi_tag)::value;
+        FGemmParams q = p;
+        q.ti = (NI + 32 * kMI * WI - 1) / (32 * kMI * WI);
+        const long grid = (long)q.ti * q.tj * q.splits * B;
         static std::atomic<unsigned long long> done{0};
-        hipError_t e2 = ensure_lds_limit((const void *)split_gemm_f32_kernel<BCOL, D, M>, gemm_lds_bytes<D>(), done);
+        hipError_t e2 = ensure_lds_limit((const void *)split_gemm_f32_kernel<BCOL, D, M, WI>, gemm_lds_bytes<D, WI>(), done);
         if (e2 != hipSuccess) return e2;
-        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, D, M>), dim3((unsigned)grid), dim3(kNT), gemm_lds_bytes<D>(), s, p);
+        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, D, M, WI>), dim3((unsigned)grid), dim3(64 * WI * kWJ),
+                           (gemm_lds_bytes<D, WI>()), s, q);
         return hipSuccess;
     };
     using T_ = std::true_type;
     using F_ = std::false_type;
+    using W2 = std::integral_constant<int, kWI>;
+    using W4 = std::integral_constant<int, 4>;
 #ifdef CORR_GEMM_AB  // tools/kbench_gemm.hip: the convert-back split as well
-    if (!g_gemm_mix) e = dma ? go(T_{}, F_{}) : go(F_{}, F_{});
+    if (!g_gemm_mix) e = dma ? go(T_{}, F_{}, W2{}) : go(F_{}, F_{}, W2{});
     else
 #endif
-    e = dma ? go(T_{}, T_{}) : go(F_{}, T_{});
+    e = wide ? go(T_{}, T_{}, W4{}) : dma ? go(T_{}, T_{}, W2{}) : go(F_{}, T_{}, W2{});
     if (e != hipSuccess) return e;
     e = hipGetLastError();
     if (e != hipSuccess || p.direct) return e;

@@ -79,10 +79,10 @@ int main(int argc, char **argv) {
     auto g2 = [&](float *out) {
         return gemm_f32<true>(f1, (long)D * NQ, NQ, dc, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, out, w.slab, 0);
     };
-    g_gemm_dma = 0, g_gemm_mix = 0, g_reduce_vec4 = 0;  // reference: register-staged, convert-back, scalar reduce
+    g_gemm_dma = 0, g_gemm_mix = 0, g_reduce_vec4 = 0, g_gemm_wide = 0;  // reference: register-staged, convert-back, scalar reduce
     CK(g1(r1));
     CK(g2(r2));
-    g_gemm_dma = 1, g_gemm_mix = 1, g_reduce_vec4 = 1;
+    g_gemm_dma = 1, g_gemm_mix = 1, g_reduce_vec4 = 1, g_gemm_wide = 1;
     struct V {
         std::string name;
         std::function<hipError_t()> run;
@@ -90,18 +90,18 @@ int main(int argc, char **argv) {
         std::vector<float> us;
     };
     std::vector<V> vs;
-    for (int rv : {0, 1}) {
-        const std::string tag = std::string("DMA mix splits plan, reduce ") + (rv ? "vec4" : "scalar");
-        vs.push_back({"dF1 (rows) " + tag, [&, rv] {
-                          g_reduce_vec4 = rv;
+    for (int wide : {0, 1}) {
+        const std::string tag = std::string("DMA mix splits plan, ") + (wide ? "256x256 tiles (8 waves)" : "128x256 tiles");
+        vs.push_back({"dF1 (rows) " + tag, [&, wide] {
+                          g_gemm_wide = wide;
                           const hipError_t e = g1(o1);
-                          g_reduce_vec4 = 1;
+                          g_gemm_wide = 1;
                           return e;
                       }, o1, r1, {}});
-        vs.push_back({"dF2 (cols) " + tag, [&, rv] {
-                          g_reduce_vec4 = rv;
+        vs.push_back({"dF2 (cols) " + tag, [&, wide] {
+                          g_gemm_wide = wide;
                           const hipError_t e = g2(o2);
-                          g_reduce_vec4 = 1;
+                          g_gemm_wide = 1;
                           return e;
                       }, o2, r2, {}});
     }
