@@ -406,7 +406,7 @@ def test_autograd_fused_backward_equals_per_lookup(monkeypatch):
             assert bit_equal(a, b), direct
 
 
-@pytest.mark.parametrize("B,D,H,W", [(1, 256, 60, 80), (2, 32, 18, 24), (1, 20, 17, 23), (8, 16, 12, 16)])
+@pytest.mark.parametrize("B,D,H,W", [(1, 256, 60, 80), (2, 200, 16, 24), (2, 32, 18, 24), (1, 20, 17, 23), (8, 16, 12, 16)])
 @pytest.mark.parametrize("algo", ["f16x3", "fp32"])
 @pytest.mark.parametrize("spread", [False, True])
 def test_build_bwd_vs_oracle(B, D, H, W, algo, spread):
