@@ -357,7 +357,9 @@ __device__ __forceinline__ void split2(float x0, float x1, int s, bool guard, ha
 // ---------------------------------------------------------------------------------------
 // The GEMM: C[b][i][j] (+)= sum_k A[b][i][k] B[b][j][k].  4 waves (2 along i x 2 along j),
 // each 64 i x 128 j (2 x 4 blocks of 32 x 32), workgroup 128 x 256; K chunks staged through
-// LDS double-buffered, the next chunk's global loads in flight during the MFMAs.
+// LDS double-buffered, the next chunk's global loads in flight during the MFMAs.  On the
+// LDS-DMA path with more than 128 rows the workgroup is 8 waves (4 along i), 256 x 256: each
+// staged element then feeds twice the MFMAs (split_gemm_f32_kernel's WI = 4).
 // ---------------------------------------------------------------------------------------
 constexpr int kWI = 2, kWJ = 2, kMI = 2, kNJ = 4;
 constexpr int kTI = 32 * kMI * kWI;   // 128
