@@ -932,7 +932,9 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     unsigned *RM = reinterpret_cast<unsigned *>(fsm + o.aux + kFusedLv * ST::SIZE);  // [BQ]
 
     if (!(PROBE & 4))
-        for (int i = tid; i < o.aux; i += NT) fsm[i] = 0.0f;  // every map of the workgroup
+        // every map of the workgroup, 16 B per store (o.aux is a multiple of 64 floats:
+        // BQ query strides of 64k + 64 / BQ)
+        for (int i = 4 * tid; i < o.aux; i += 4 * NT) *reinterpret_cast<float4 *>(fsm + i) = make_float4(0.f, 0.f, 0.f, 0.f);
     if (tid < BQ) RM[tid] = 0u;
     __syncthreads();
 
