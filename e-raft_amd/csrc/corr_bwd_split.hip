@@ -294,39 +294,6 @@ __global__ __launch_bounds__(kCmCols *kCmSlices) void colmax_reduce_kernel(const
     }
 }
 
-// The same reduction, 4 columns (16 B) per lane: N % 4 == 0 and 16-B aligned partials.
-__global__ __launch_bounds__(kCmCols *kCmSlices) void colmax_reduce_vec4_kernel(const float4 *__restrict__ part, int G,
-                                                                              int N4, uint4 *__restrict__ cmax) {
-    __shared__ float4 red[kCmSlices][kCmCols];
-    const int b = blockIdx.y, c = threadIdx.x % kCmCols, sl = threadIdx.x / kCmCols;
-    const int m = blockIdx.x * kCmCols + c;
-    auto mx4 = [](float4 a, float4 v) {
-        return make_float4(fmaxf(a.x, v.x), fmaxf(a.y, v.y), fmaxf(a.z, v.z), fmaxf(a.w, v.w));
-    };
-    float4 a[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) a[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (m < N4) {
-        const float4 *p = part + (size_t)b * G * N4 + m;
-        int g = sl;
-        for (; g + 3 * kCmSlices < G; g += 4 * kCmSlices)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) a[u] = mx4(a[u], p[(size_t)(g + u * kCmSlices) * N4]);
-        for (; g < G; g += kCmSlices) a[0] = mx4(a[0], p[(size_t)g * N4]);
-    }
-#pragma unroll
-    for (int u = 1; u < 4; ++u) a[0] = mx4(a[0], a[u]);
-    red[sl][c] = a[0];
-    __syncthreads();
-    if (sl == 0 && m < N4) {
-        float4 r = red[0][c];
-#pragma unroll
-        for (int k = 1; k < kCmSlices; ++k) r = mx4(r, red[k][c]);
-        cmax[(size_t)b * N4 + m] = make_uint4(__float_as_uint(r.x), __float_as_uint(r.y), __float_as_uint(r.z),
-                                              __float_as_uint(r.w));
-    }
-}
-
 // Exponent of a row from its max (as split_pack_wide_kernel): max * 2^s < 2^15.
 __device__ __forceinline__ int split_shift(float mm) {
     int s = 0;
@@ -984,13 +951,8 @@ hipError_t launch_backward(int algo, const float *const *coords, const float *co
                                    rm);
         if (e == hipSuccess) {
             if (algo == CORR_BUILD_F16X3) {
-                if (N % 4 == 0 && ((uintptr_t)cpart & 15) == 0 && ((uintptr_t)cmax & 15) == 0)
-                    hipLaunchKernelGGL(colmax_reduce_vec4_kernel,
-                                       dim3((unsigned)((N / 4 + kCmCols - 1) / kCmCols), (unsigned)B),
-                                       dim3(kCmCols * kCmSlices), 0, s, (const float4 *)cpart, G, N / 4, (uint4 *)cmax);
-                else
-                    hipLaunchKernelGGL(colmax_reduce_kernel, dim3((unsigned)((N + kCmCols - 1) / kCmCols), (unsigned)B),
-                                       dim3(kCmCols * kCmSlices), 0, s, cpart, G, N, cmax);
+                hipLaunchKernelGGL(colmax_reduce_kernel, dim3((unsigned)((N + kCmCols - 1) / kCmCols), (unsigned)B),
+                                   dim3(kCmCols * kCmSlices), 0, s, cpart, G, N, cmax);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
                 return bwd_split_gemms(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, w, s, true);
             }
