@@ -38,12 +38,21 @@ METRIC = "CorrBlock build+lookup frame-pairs/sec & HBM GB/s at DSEC 480Ã—640, 1â
 PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
 PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E spec
 PEAK_F16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense BF16/F16 MFMA
-BUILD_ALGO = {0: "fp32", 1: "f16x3"}
-BUILD_KERNELS = {0: "corr_build_kernel", 1: "split_pack_wide_kernel+corr_build_split_kernel"}
+BUILD_ALGO = {0: "fp32", 1: "f16x3", 2: "bf16x6"}
+BUILD_KERNELS = {0: "corr_build_kernel", 1: "split_pack_wide_kernel+corr_build_split_kernel",
+                 2: "bf16_pack_kernel+corr_build_bf16_kernel"}
+PACK_KERNEL = {1: "split_pack_wide_kernel", 2: "bf16_pack_kernel"}
+MFMA_KERNEL = {1: "corr_build_split_kernel", 2: "corr_build_bf16_kernel"}
+EXEC_FACTOR = {0: 1, 1: 3, 2: 6}  # MFMA products executed per fp32 product
 # what "dtype": "f32" means for the build: the arithmetic that forms each fp32 product
 BUILD_ARITH = {0: "fp32 MFMA (exact fp32 products, fp32 accumulate; the reference's arithmetic)",
                1: "f16x3 emulated fp32: per-pixel 2^e (hi + lo) f16 split, 3 f16 MFMAs per product "
-                  "(hi.hi + hi.lo + lo.hi, ~2^-22 relative), fp32 accumulate"}
+                  "(hi.hi + hi.lo + lo.hi, ~2^-22 relative: NARROWER than fp32), fp32 accumulate",
+               2: "bf16x6, no narrower than fp32: every fp32 feature split EXACTLY into three bf16 pieces "
+                  "(hi + mid + lo, fp32's exponent range, no scale or flush), the 6 piece products of "
+                  "weight >= 2^-16 on the bf16 MFMA (dropped terms <= 2^-23 |ab|), fp32 accumulate "
+                  "(6D/32 roundings per dot product vs D for an fp32 fmaf chain); per-row error vs fp64 "
+                  "<= the fp32 MFMA build's (tests/test_gpu_parity.py::test_build_bf16x6_not_narrower_than_fp32)"}
 BUILD_NOTE = {
     0: "fp32 operands on v_mfma_f32_32x32x2_f32: achieved = 2*B*N^2*D flops / build kernel time, "
        "against the fp32 MFMA peak",
@@ -51,6 +60,10 @@ BUILD_NOTE = {
        "fp32 product, fp32 accumulate): achieved = EXECUTED f16 flops (3 * 2*B*N^2*D) / (pack + "
        "MFMA kernel time, each kernel timed alone: kernel_us), against the dense f16 MFMA peak; "
        "the fp32-equivalent rate is fp32_equivalent_tflops",
+    2: "fp32 product on the bf16 MFMA pipe (exact three-piece bf16 split, 6 bf16 MFMAs per fp32 "
+       "product, fp32 accumulate): achieved = EXECUTED bf16 flops (6 * 2*B*N^2*D) / (pack + MFMA "
+       "kernel time, each kernel timed alone: kernel_us), against the dense bf16 MFMA peak; the "
+       "fp32-equivalent rate (2*B*N^2*D / time) is fp32_equivalent_tflops",
 }
 
 WORKLOADS = {
@@ -331,8 +344,8 @@ def graph_time_ms(fn, stream, rep=10, trials=5):
 
 def build_roofline(algo, fl, bb, t_ms, traffic_b):
     """The build kernel against the roofline of the pipe it runs on (see BUILD_NOTE)."""
-    executed = 3 * fl if algo == 1 else fl
-    peak = PEAK_F16_MFMA_TFLOPS if algo == 1 else PEAK_FP32_MFMA_TFLOPS
+    executed = EXEC_FACTOR[algo] * fl
+    peak = PEAK_F16_MFMA_TFLOPS if algo != 0 else PEAK_FP32_MFMA_TFLOPS
     ach = executed / (t_ms * 1e-3) / 1e12
     # The build is bounded by BOTH its pipe and its HBM bytes (the pyramid write); report which
     # floor binds and the fraction of that floor achieved, beside the pipe fraction above.
@@ -406,7 +419,8 @@ def main():
         outs = [torch.empty(B, L * K, H, W, device=dev) for _ in range(iters)]
 
     algo = _lib.default_algo()
-    ws = _lib.build_workspace(f1, f2, algo)  # packed f16 operands (F16X3), reused every step
+    ws = _lib.build_workspace(f1, f2, algo)  # the split operands (BF16X6 / F16X3), reused every step
+    ws_x3 = _lib.build_workspace(f1, f2, _lib.BUILD_F16X3)
 
     def build_only():
         _lib.build(f1, f2, pyr, algo, ws)
@@ -414,7 +428,10 @@ def main():
     def build_fp32():
         _lib.build(f1, f2, pyr, _lib.BUILD_FP32, None)
 
-    def build_pack():  # the f16x3 build's two kernels timed apart (corr_build_ex measurement flags)
+    def build_f16x3():
+        _lib.build(f1, f2, pyr, _lib.BUILD_F16X3, ws_x3)
+
+    def build_pack():  # the split build's two kernels timed apart (corr_build_ex measurement flags)
         _lib.build(f1, f2, pyr, algo | _lib.BUILD_ONLY_PACK, ws)
 
     def build_mfma():
@@ -519,16 +536,51 @@ def main():
         if world > 1:
             dist.barrier()
 
+        # the same step with the other build algorithms, and through the public drop-in API
+        # (CorrBlock ctor: pyramid + workspace allocation, then 12 __call__s), reported beside
+        # `value` â€” same K steps after W warmups, HIP graphs unless --eager
+        alt_values = {}
+        if not train and not sharded:
+            def timed(fn):
+                st = fn
+                if launch == "hipgraph":
+                    gg = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gg, stream=stream):
+                        fn()
+                    st = gg.replay
+                for _ in range(args.warmup):
+                    st()
+                torch.cuda.synchronize()
+                a0 = time.perf_counter()
+                for _ in range(args.steps):
+                    st()
+                torch.cuda.synchronize()
+                return round(B * args.steps / (time.perf_counter() - a0), 2)
+
+            def api_pair():
+                cb = CorrBlock(f1, f2, num_levels=L, radius=r)
+                for c in coords:
+                    cb(c)
+
+            for nm, bfn in (("fp32", build_fp32), ("f16x3", build_f16x3)):
+                if BUILD_ALGO[algo] != nm:
+                    alt_values[f"build_{nm}"] = timed(lambda bfn=bfn: (bfn(), run_lookups()))
+            try:
+                alt_values[f"corrblock_api_{BUILD_ALGO[algo]}"] = timed(api_pair)
+            except Exception as exc:  # noqa: BLE001 â€” report, keep the headline
+                alt_values["corrblock_api_error"] = str(exc)[:200]
+
         # per-kernel durations on the launch stream (graph_time_ms)
         build_call_ms = graph_time_ms(build_only, stream)
-        if algo == _lib.BUILD_F16X3:  # per-kernel: pack + MFMA, each timed alone (kernel-trace comparable)
+        if algo != _lib.BUILD_FP32:  # per-kernel: pack + MFMA, each timed alone (kernel-trace comparable)
             pack_ms, mfma_ms = graph_time_ms(build_pack, stream), graph_time_ms(build_mfma, stream)
             build_ms = pack_ms + mfma_ms
         else:
             pack_ms = mfma_ms = None
             build_ms = build_call_ms
         look_ms = graph_time_ms(run_lookups, stream) / iters
-        fp32_ms = graph_time_ms(build_fp32, stream, rep=4) if algo == _lib.BUILD_F16X3 else None
+        fp32_ms = graph_time_ms(build_fp32, stream, rep=4) if algo != _lib.BUILD_FP32 else None
+        x3_ms = graph_time_ms(build_f16x3, stream, rep=4) if algo == _lib.BUILD_BF16X6 else None
         bwd_ms = graph_time_ms(run_bwd_kernels, stream, rep=4) if train else None
         bwd_staged_ms = graph_time_ms(run_bwd_staged, stream, rep=4) if train else None
         if sharded and world > 1:  # per-rank broadcast time (eager, events on the stream)
@@ -603,11 +655,20 @@ def main():
             "hbm_gbs_algorithmic": round(hbm_gbs, 1),
         }
         if pack_ms is not None:
-            res["roofline"]["kernel_us"] = {"split_pack_wide_kernel": round(pack_ms * 1e3, 2),
-                                            "corr_build_split_kernel": round(mfma_ms * 1e3, 2),
+            res["roofline"]["kernel_us"] = {PACK_KERNEL[algo]: round(pack_ms * 1e3, 2),
+                                            MFMA_KERNEL[algo]: round(mfma_ms * 1e3, 2),
                                             "build_call_in_graph": round(build_call_ms * 1e3, 2)}
-        if fp32_ms is not None:  # the reference's own precision, beside the f16x3 default
+        if fp32_ms is not None:  # the fp32-operand MFMA build, beside the default
             res["build_fp32"] = build_roofline(0, fl, bb, fp32_ms, build_traffic(wl_name, 0))
+        if x3_ms is not None:  # the narrower f16x3 split (round-3 default), labelled
+            res["build_f16x3"] = build_roofline(1, fl, bb, x3_ms, build_traffic(wl_name, 1))
+            res["build_f16x3"]["arith"] = BUILD_ARITH[1]
+        if alt_values:
+            res["alt_values"] = alt_values
+            res["alt_values_note"] = ("frame-pairs/s of the same step (K steps after W warmups): with the "
+                                      "fp32-operand MFMA build, with the f16x3 split build (narrower than "
+                                      "fp32), and through the public CorrBlock API (its per-pair pyramid and "
+                                      "workspace allocations included)")
         if train:
             res["backward_kernels"] = {
                 "phase": f"corr_backward: {iters} lookup backwards in one launch + pool fold with dC "

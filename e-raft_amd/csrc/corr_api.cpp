@@ -98,7 +98,9 @@ size_t corr_build_workspace(int algo, int B, int D, int NQ, int H, int W) {
     if (B < 1 || D < 1 || NQ < 1 || H < 1 || W < 1) return 0;
     if (algo == CORR_BUILD_F16X3)
         return build_split_supported(D) ? build_split_workspace(B, D, NQ, H, W) : (size_t)-1;
-    return 0;
+    if (algo == CORR_BUILD_BF16X6) return build_bf16_workspace(B, D, NQ, H, W);
+    if (algo == CORR_BUILD_FP32) return 0;
+    return (size_t)-1;
 }
 
 int corr_build_ex(int algo, const float *fmap1_rows, int NQ, const float *fmap2, int B, int D,
@@ -109,21 +111,26 @@ int corr_build_ex(int algo, const float *fmap1_rows, int NQ, const float *fmap2,
     g_err[0] = 0;
     const int phase = algo & (CORR_BUILD_ONLY_PACK | CORR_BUILD_ONLY_MFMA);
     algo &= ~(CORR_BUILD_ONLY_PACK | CORR_BUILD_ONLY_MFMA);
-    if (algo != CORR_BUILD_F16X3 || phase == (CORR_BUILD_ONLY_PACK | CORR_BUILD_ONLY_MFMA))
+    if ((algo != CORR_BUILD_F16X3 && algo != CORR_BUILD_BF16X6) ||
+        phase == (CORR_BUILD_ONLY_PACK | CORR_BUILD_ONLY_MFMA))
         return fail(CORR_EINVAL, "%s: unknown algorithm %d", fn, algo | phase);
+    const bool bf = algo == CORR_BUILD_BF16X6;
     int rc = check_dims(fn, B, NQ, H, W, levels);
     if (rc) return rc;
     if (D < 1) return fail(CORR_EINVAL, "%s: D must be >= 1 (got %d)", fn, D);
-    if (!build_split_supported(D))
+    if (!bf && !build_split_supported(D))
         return fail(CORR_EUNSUPPORTED, "%s: D = %d is too large for CORR_BUILD_F16X3", fn, D);
     if ((rc = check_ptr(fn, fmap1_rows, "fmap1")) || (rc = check_ptr(fn, fmap2, "fmap2"))) return rc;
     if ((uintptr_t)workspace % 256) return fail(CORR_EINVAL, "%s: workspace is not 256-byte aligned", fn);
-    const size_t need = build_split_workspace(B, D, NQ, H, W);
+    const size_t need = bf ? build_bf16_workspace(B, D, NQ, H, W) : build_split_workspace(B, D, NQ, H, W);
     if (workspace_bytes < need || !workspace)
         return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
     LevelPtrs lp{};
     if ((rc = check_levels(fn, pyr, levels, "pyr", lp.p))) return rc;
     const int part = phase == CORR_BUILD_ONLY_PACK ? 1 : phase == CORR_BUILD_ONLY_MFMA ? 2 : 0;
+    if (bf)
+        return hip_status(
+            launch_build_bf16(fmap1_rows, NQ, fmap2, B, D, H, W, levels, lp, workspace, (hipStream_t)stream, part), fn);
     return hip_status(launch_build_split(fmap1_rows, NQ, fmap2, B, D, H, W, levels, lp, workspace, (hipStream_t)stream, part),
                       fn);
 }

@@ -373,13 +373,12 @@ hipError_t launch_pool_levels(const LevelPtrs &pyr, int l_from, int levels, long
     return hipSuccess;
 }
 
-// 16-B level-1 stores when the shape allows (tools/kbench_build.hip turns them off for its A/B).
-bool g_build_vec1 = true;
-
 // Launch one build with tile geometry Cfg (exposed for tools/kbench_build.hip).
+// vec1_ok: 16-B level-1 stores when the shape allows (tools/kbench_build.hip turns them off for
+// its A/B).
 template <class Cfg>
 hipError_t launch_build_cfg(const float *f1, int NQ, const float *f2, int B, int D, int H, int W,
-                            int levels, const LevelPtrs &pyr, hipStream_t s) {
+                            int levels, const LevelPtrs &pyr, hipStream_t s, bool vec1_ok = true) {
     BuildParams p{};
     p.f1 = f1;
     p.f2 = f2;
@@ -404,7 +403,7 @@ hipError_t launch_build_cfg(const float *f1, int NQ, const float *f2, int B, int
     const long tiles = (long)p.nq * p.npx * p.npy * B;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
     // 16-B level-1 / 8-B level-2 stores: whole 8-column sub-patches and aligned level bases
-    const bool vec1 = g_build_vec1 && vec && W % 8 == 0 && (p.nlev < 2 || (uintptr_t)pyr.p[1] % 16 == 0) &&
+    const bool vec1 = vec1_ok && vec && W % 8 == 0 && (p.nlev < 2 || (uintptr_t)pyr.p[1] % 16 == 0) &&
                       (p.nlev < 3 || (uintptr_t)pyr.p[2] % 8 == 0);
     static std::atomic<unsigned long long> lds_done[3];
     auto go = [&](auto vm_tag) {

@@ -1,0 +1,565 @@
+// corr_build_bf16.hip — the all-pairs build and its pyramid on gfx950's bf16 MFMA, at no less
+// than fp32 accuracy.  Replaces CorrBlock.corr (model/corr.py:52-60: matmul(F1^T, F2) / sqrt(D))
+// and the pyramid loop of CorrBlock.__init__ (model/corr.py:21-27).
+//
+// Operands.  bf16 has fp32's exponent range and 8 significant bits, so every fp32 feature is
+// EXACTLY the sum of three bf16 pieces,
+//     x = hi + mid + lo,   hi = bf16_rn(x),  mid = bf16_rn(x - hi),  lo = x - hi - mid,
+// (x - hi and x - hi - mid are exact in fp32; lo has at most 8 significant bits, so it is a bf16
+// value as it stands) with |mid| <= 2^-8 |x| and |lo| <= 2^-16 |x|.  No per-pixel scale and no
+// flush: the only exception is the bf16 subnormal floor for lo (|x| below ~2^-110).  A dot
+// product takes, per 32-deep K step, the six bf16 MFMAs of largest weight chained from zero,
+//     t = lo_t hi_q + hi_t lo_q + mid_t mid_q + mid_t hi_q + hi_t mid_q + hi_t hi_q
+// (smallest first; bf16 x bf16 products are exact in fp32), and adds t to its fp32
+// accumulator: the accumulator rounds ONCE per K step (D / 32 times per dot product, where an
+// fp32 fmaf chain rounds D times), t's own roundings happen at one K step's magnitude.  What is
+// dropped (mid lo + lo mid + lo lo) is <= 2^-23 |x_t x_q| per term.  The fp64-oracle test holds this build's per-row error to at most the
+// exact-fp32 MFMA build's (tests/test_gpu_parity.py::test_build_bf16x6_not_narrower_than_fp32).
+//
+// MFMA orientation (as corr_build_split.hip): v_mfma_f32_16x16x32_bf16 with A = TARGETS (rows)
+// and B = QUERIES (columns); lane l = 16 grp + ci owns query ci of a 16-query block and targets
+// 4 grp .. 4 grp + 3 of a 16-target block (one map row x 16 columns), so a lane holds runs of
+// 4 consecutive pixels of one query's map: level 0 leaves as 16-B row stores, the 2x2 / 4x4
+// windows of levels 1-2 sit inside one lane, level 3 pairs lanes 16 apart.
+//
+// Workgroup = 4 waves x 32 queries against one 8 x 16 target patch.  The patch's records
+// (24 KiB per 32-deep K step) stream into a 3-slot LDS ring by LDS-DMA two steps ahead; each
+// wave loads its own queries' records into registers, also two steps ahead.  One barrier per K
+// step.  Two workgroups per CU (72 KiB LDS each).
+//
+// Packed operand images (bf16_pack_kernel), one 3 KiB record per (K step s, 16-pixel block):
+//   bytes [0, 1024)      hi:  lane l = 16 grp + ci at 16 l: 8 bf16 of k = 32 s + 8 grp + j, pixel ci
+//   bytes [1024, 2048)   mid: the same positions
+//   bytes [2048, 3072)   lo:  the same positions
+// i.e. exactly the MFMA fragment images of that block: the LDS fill and every fragment read are
+// contiguous 1 KiB (conflict-free ds_read_b128, coalesced loads).
+//   pq [B][S][NQB][3 KiB]     queries: block = 16 consecutive query pixels, NQp = NQB*16
+//   pt [B][S][Hp][CB][3 KiB]  targets: block = (row y, columns 16 cb .. 16 cb + 15)
+// Padding pixels and k >= D are zero.
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+
+#include "corr_build_common.h"
+
+namespace corr {
+
+typedef __bf16 bfx8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bfx2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+namespace bf16b {
+
+constexpr int kStepK = 32;                              // k per MFMA step
+constexpr int kPieces = 3;                              // hi, mid, lo
+constexpr int kRecU = kPieces * 64;                     // u32x4 per record (3 KiB)
+constexpr int kPatchRows = 8;                           // target patch: 8 rows x 16 columns
+constexpr int kWaves = 4, kQPerWave = 32;               // 2 query blocks per wave
+constexpr int kQPerWG = kWaves * kQPerWave;             // 128
+constexpr int kRing = 3;                                // LDS ring slots (prefetch distance 2)
+constexpr int kSlotBytes = kPatchRows * kPieces * 1024; // 24 KiB per K step
+constexpr int kLds = kRing * kSlotBytes;                // 72 KiB
+constexpr int kDmaPerWave = kPatchRows * kPieces / kWaves;  // 6 LDS-DMA pieces per wave and step
+constexpr int kQLoads = 2 * kPieces;                    // query loads per wave and step
+constexpr int kPixBytes = kStepK * kPieces * 2;         // workspace bytes per pixel and K step
+
+struct Geom {
+    int S, NQp, NQB, NQG, Hp, CB, Wp;
+};
+
+inline Geom geom(int D, int NQ, int H, int W) {
+    Geom g;
+    g.S = (D + kStepK - 1) / kStepK;
+    g.NQp = (NQ + kQPerWG - 1) / kQPerWG * kQPerWG;
+    g.NQB = g.NQp / 16;
+    g.NQG = g.NQp / kQPerWG;
+    g.Hp = (H + kPatchRows - 1) / kPatchRows * kPatchRows;
+    g.CB = (W + 15) / 16;
+    g.Wp = g.CB * 16;
+    return g;
+}
+
+// bf16 round-to-nearest-even of a pair, as fp32 values and as the packed pair.
+__device__ __forceinline__ unsigned rn_pair(float a, float b, float &ha, float &hb) {
+    const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2_t{a, b}, bfx2_t));
+    ha = __builtin_bit_cast(float, u << 16);
+    hb = __builtin_bit_cast(float, u & 0xffff0000u);
+    return u;
+}
+
+// Split a pair of fp32 features into packed bf16 (hi, mid, lo) pairs, x = hi + mid + lo exactly.
+// Guards: an infinite feature keeps hi = x and mid = lo = 0 (its products are x * the other
+// operand, as in fp32); a finite feature whose hi rounds up past the bf16 range (|x| within
+// 2^-9 of FLT_MAX) takes the truncated hi instead.  NaN propagates through hi.
+__device__ __forceinline__ void split3(float a, float b, unsigned &hi, unsigned &mid, unsigned &lo) {
+    float ha, hb;
+    hi = rn_pair(a, b, ha, hb);
+    if (__builtin_expect(__builtin_isinf(ha) | __builtin_isinf(hb), 0)) {
+        const unsigned ua = __builtin_bit_cast(unsigned, a), ub = __builtin_bit_cast(unsigned, b);
+        if (__builtin_isinf(ha) && !__builtin_isinf(a)) ha = __builtin_bit_cast(float, ua & 0xffff0000u);
+        if (__builtin_isinf(hb) && !__builtin_isinf(b)) hb = __builtin_bit_cast(float, ub & 0xffff0000u);
+        hi = (__builtin_bit_cast(unsigned, ha) >> 16) | (__builtin_bit_cast(unsigned, hb) & 0xffff0000u);
+    }
+    float ra = __builtin_isinf(a) ? 0.f : a - ha, rb = __builtin_isinf(b) ? 0.f : b - hb;
+    float ma, mb;
+    mid = rn_pair(ra, rb, ma, mb);
+    float da, db;
+    lo = rn_pair(ra - ma, rb - mb, da, db);  // exact: the residuals have <= 8 significant bits
+}
+
+// ---------------------------------------------------------------------------------------
+// Operand pack: one wave per record (K step, 16-pixel block) of one batch item and tensor;
+// lane = 16 grp + ci holds the 8 k of its fragment position, splits them and writes 16 B of
+// each piece (each store instruction writes one contiguous 1 KiB piece).
+// ---------------------------------------------------------------------------------------
+struct PackArgs {
+    const float *f[2];
+    u32x4_t *pk[2];
+    int np[2];    // source pixels per batch item: NQ, H*W
+    int nblk[2];  // blocks per batch item in the image: NQB, Hp*CB
+    int D, S, H, W, CB;
+};
+
+__global__ __launch_bounds__(256) void bf16_pack_kernel(PackArgs a) {
+    const int z = blockIdx.z, b = blockIdx.y;
+    const int nblk = a.nblk[z];
+    const int rec = blockIdx.x * 4 + (threadIdx.x >> 6);  // record = s * nblk + blk
+    if (rec >= a.S * nblk) return;
+    const int s = rec / nblk, blk = rec - s * nblk;
+    const int lane = threadIdx.x & 63, ci = lane & 15, grp = lane >> 4;
+    int n;
+    bool valid;
+    if (z == 0) {
+        n = blk * 16 + ci;
+        valid = n < a.np[0];
+    } else {
+        const int y = blk / a.CB, x = (blk - y * a.CB) * 16 + ci;
+        valid = y < a.H && x < a.W;
+        n = y * a.W + x;
+    }
+    const int NP = a.np[z], k0 = s * kStepK + 8 * grp;
+    const float *src = a.f[z] + (size_t)b * a.D * NP + (valid ? n : 0);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (valid && k0 + j < a.D) ? src[(size_t)(k0 + j) * NP] : 0.f;
+    unsigned hh[4], mm[4], ll[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split3(v[2 * j], v[2 * j + 1], hh[j], mm[j], ll[j]);
+    const u32x4_t h{hh[0], hh[1], hh[2], hh[3]}, m{mm[0], mm[1], mm[2], mm[3]}, l{ll[0], ll[1], ll[2], ll[3]};
+    u32x4_t *out = a.pk[z] + (((size_t)b * a.S + s) * nblk + blk) * kRecU + lane;
+    out[0] = h;
+    out[64] = m;
+    out[128] = l;
+}
+
+// ---------------------------------------------------------------------------------------
+// The MFMA build.
+// ---------------------------------------------------------------------------------------
+struct Args {
+    const u32x4_t *pq, *pt;
+    float *lvl[kFusedLevels];
+    int B, H, W, N, NQ, S, nlev;
+    int NQp, NQB, NQG, Hp, CB, npatch;
+    int exact;         // 1/sqrt(D) is a power of two (multiply); else divide by s
+    int mode0, mode1;  // store width of levels 0 / 1: 2 = 16 B, 1 = 8 B, 0 = elements
+    int cons;          // levels 1 and 2 as 16-B stores (W/2, W/4 multiples of 4, 16-B aligned bases)
+    float inv_s, s;
+    int order;  // tile order (patch_tile)
+};
+
+// SS > 0: S = SS K steps, fully unrolled (straight-line code: the compiler's own waits on the
+// query registers are exact and never drain the prefetch).  SS = 0: any S, runtime loop.
+// NR: map rows of the patch whose MFMAs run (8; 4 for a patch with at most 4 rows inside the
+// map — its rows 4-7 are padding whose accumulators stay zero and whose stores are dropped).
+// ACC2 (default): the five small piece products of every K step accumulate in a second fp32
+// accumulator and hi*hi alone in the first; they meet once, in the epilogue.  The first
+// accumulator rounds D / 32 times per dot product, the second's roundings are 2^-8 smaller.  Its
+// 64 extra registers leave room for three query register slots (prefetch distance 2; the
+// compiler's own wait on them then also covers the next step's query loads, which have landed
+// by then).  ACC2 = false: the six products of a K step chained from zero into a transient and
+// added to one accumulator by VALU (four query slots) — the same rounding count, measured slower.
+template <int SS, int NR, bool ACC2>
+__device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
+    constexpr int QS = ACC2 ? 3 : 4, QD = QS - 1;
+    extern __shared__ __attribute__((aligned(16))) char smem_bf16[];
+    char *smem = smem_bf16;
+
+    const int b = tl.b, y0 = tl.py * kPatchRows, x0 = tl.cb * 16;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ci = lane & 15, grp = lane >> 4;
+    const int qb0 = tl.qg * (kQPerWG / 16) + 2 * w;  // this wave's first 16-query block
+    const int S = SS > 0 ? SS : p.S;
+    const bool qact = qb0 * 16 < p.NQ;  // wave-uniform
+
+    // LDS-DMA pieces of this wave: pc = w + 4 m (m < 6) -> patch row pc / 3, piece pc % 3, landing
+    // at slot offset pc KiB (row r's pieces at 3 r .. 3 r + 2).
+    const size_t tstep = (size_t)p.Hp * p.CB * kRecU;  // u32x4 per K step of the target image
+    const u32x4_t *tbase = p.pt + (((size_t)b * S * p.Hp + y0) * p.CB + tl.cb) * kRecU + lane;
+    unsigned toff[kDmaPerWave];
+#pragma unroll
+    for (int m = 0; m < kDmaPerWave; ++m) {
+        const int pc = w + 4 * m;
+        toff[m] = (unsigned)((pc / kPieces) * p.CB * kRecU + (pc % kPieces) * 64);
+    }
+    const size_t qstep = (size_t)p.NQB * kRecU;
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_void_t *)smem;
+    const u32x4_t *qsrc = p.pq + ((size_t)b * S * p.NQB + qb0) * kRecU + lane;
+
+    // Issue schedule (SS > 0): step k issues the wave's 6 query loads of step k + 3 (register
+    // slot (k + 3) % 4), then its 6 LDS-DMA pieces of step k + 2 (ring slot (k + 2) % 3); the
+    // prologue plays Q0 Q1 T0 Q2 T1.  At step k's barrier the operations younger than T(k) are
+    // exactly step k - 1's group (Q(k + 2), T(k + 1): vmcnt(12) while both exist), and Q(k) is
+    // older than T(k); the query registers then pass through an empty asm, before which the
+    // compiler's own wait (it counts only the query loads: Q(k + 1), Q(k + 2) younger) is
+    // already satisfied: no drain.
+    u32x4_t qv[QS][2][kPieces];
+    auto issue_q = [&](int s, int slot) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int c = 0; c < kPieces; ++c) qv[slot][i][c] = qsrc[s * qstep + i * kRecU + c * 64];
+    };
+    auto issue_t = [&](int s, int slot) __attribute__((always_inline)) {
+        const uint32_t base = lds_base + slot * kSlotBytes;
+        const u32x4_t *src = tbase + s * tstep;
+#pragma unroll
+        for (int m = 0; m < kDmaPerWave; ++m) dma16(src + toff[m], base + (w + 4 * m) * 1024);
+    };
+
+    f32x4_t acc[2][kPatchRows], acs[2][kPatchRows];  // hi*hi; the small products (ACC2)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < kPatchRows; ++r) acc[i][r] = acs[i][r] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    // One K step: per map row, its three target fragments (read one row ahead) and 12 MFMAs.
+    auto compute = [&](int tslot, int qslot) __attribute__((always_inline)) {
+        const u32x4_t *A = reinterpret_cast<const u32x4_t *>(smem + tslot * kSlotBytes);
+        bfx8_t qh[2], qm[2], ql[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            qh[i] = __builtin_bit_cast(bfx8_t, qv[qslot][i][0]);
+            qm[i] = __builtin_bit_cast(bfx8_t, qv[qslot][i][1]);
+            ql[i] = __builtin_bit_cast(bfx8_t, qv[qslot][i][2]);
+        }
+        bfx8_t th[2], tm[2], tl8[2];
+        th[0] = __builtin_bit_cast(bfx8_t, A[lane]);
+        tm[0] = __builtin_bit_cast(bfx8_t, A[64 + lane]);
+        tl8[0] = __builtin_bit_cast(bfx8_t, A[128 + lane]);
+        if constexpr (ACC2) {
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int c = r & 1;
+                if (r + 1 < NR) {
+                    th[c ^ 1] = __builtin_bit_cast(bfx8_t, A[(3 * r + 3) * 64 + lane]);
+                    tm[c ^ 1] = __builtin_bit_cast(bfx8_t, A[(3 * r + 4) * 64 + lane]);
+                    tl8[c ^ 1] = __builtin_bit_cast(bfx8_t, A[(3 * r + 5) * 64 + lane]);
+                }
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acs[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tl8[c], qh[i], acs[i][r], 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acs[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th[c], ql[i], acs[i][r], 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acs[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tm[c], qm[i], acs[i][r], 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acs[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tm[c], qh[i], acs[i][r], 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acs[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th[c], qm[i], acs[i][r], 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acc[i][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th[c], qh[i], acc[i][r], 0, 0, 0);
+            }
+            // schedule: row 0's reads, then per row the next row's 3 reads ahead of its 12 MFMAs
+            __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                if (r + 1 < NR) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+            }
+        } else {
+            f32x4_t t[2][2];  // per row: the six products of one K step, summed from zero (row parity)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int c = r & 1;
+                if (r + 1 < NR) {
+                    th[c ^ 1] = __builtin_bit_cast(bfx8_t, A[(3 * r + 3) * 64 + lane]);
+                    tm[c ^ 1] = __builtin_bit_cast(bfx8_t, A[(3 * r + 4) * 64 + lane]);
+                    tl8[c ^ 1] = __builtin_bit_cast(bfx8_t, A[(3 * r + 5) * 64 + lane]);
+                }
+                const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < 2; ++i) t[c][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tl8[c], qh[i], z, 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) t[c][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th[c], ql[i], t[c][i], 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) t[c][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tm[c], qm[i], t[c][i], 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) t[c][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tm[c], qh[i], t[c][i], 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) t[c][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th[c], qm[i], t[c][i], 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) t[c][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(th[c], qh[i], t[c][i], 0, 0, 0);
+                // the previous row's step sum joins its accumulator (one rounding per K step) while
+                // this row's MFMAs run
+                if (r > 0) {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) acc[i][r - 1] += t[c ^ 1][i];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) acc[i][NR - 1] += t[(NR - 1) & 1][i];
+            // schedule: row 0's reads, then per row the next row's 3 reads ahead of its 12 MFMAs and
+            // the previous row's 8 accumulator adds behind them
+            __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                if (r + 1 < NR) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+                if (r > 0) __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        }
+    };
+
+    if constexpr (SS > 0) {
+        issue_q(0, 0);
+        if (SS > 1) issue_q(1, 1);
+        issue_t(0, 0);
+        if (QD > 2 && SS > 2) issue_q(2, 2);
+        if (SS > 1) issue_t(1, 1);
+#pragma unroll
+        for (int s = 0; s < SS; ++s) {
+            // operations younger than T(s): at step 0 the prologue's [Q2,] T1; else step s - 1's
+            // group Q(s - 1 + QD), T(s + 1) — where they exist
+            const int younger = s == 0 ? (QD > 2 && SS > 2 ? kQLoads : 0) + (SS > 1 ? kDmaPerWave : 0)
+                                       : (s - 1 + QD < SS ? kQLoads : 0) + (s + 1 < SS ? kDmaPerWave : 0);
+            if (younger == kQLoads + kDmaPerWave) wait_vmcnt_barrier<kQLoads + kDmaPerWave>();
+            else if (younger == kDmaPerWave) wait_vmcnt_barrier<kDmaPerWave>();
+            else if (younger == kQLoads) wait_vmcnt_barrier<kQLoads>();
+            else wait_vmcnt_barrier<0>();
+            const int qs = s % QS;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                asm volatile("" : "+v"(qv[qs][i][0]), "+v"(qv[qs][i][1]), "+v"(qv[qs][i][2]));
+            if (s + QD < SS) issue_q(s + QD, (s + QD) % QS);
+            if (s + 2 < SS) issue_t(s + 2, (s + 2) % kRing);
+            if (qact) compute(s % kRing, qs);  // a wave whose queries all lie past NQ skips its MFMAs
+        }
+    } else {
+        // any S: no prefetch (one group in flight, drained every step)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int s = 0; s < S; ++s) {
+            issue_q(s, 0);
+            issue_t(s, 0);
+            wait_vmcnt_barrier<0>();
+            if (qact) compute(0, 0);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // slot 0 is refilled next
+        }
+    }
+
+    // ---- epilogue: 1/sqrt(D), level 0 from registers, levels 1-3 in registers ----
+    const int H = p.H, W = p.W, N = p.N, NQ = p.NQ, nlev = p.nlev;
+    const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
+    const int N1 = H1 * W1, N2 = H2 * W2, N3 = H3 * W3;
+    const int X0 = x0 + 4 * grp;
+    float l2s[2][2];  // both blocks' level-2 values: their stores are merged below
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int q = (qb0 + i) * 16 + ci;
+        const bool qok = q < NQ;
+        const size_t qrow = (size_t)b * NQ + q;
+        float v[kPatchRows][4];
+#pragma unroll
+        for (int r = 0; r < kPatchRows; ++r)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float x = ACC2 ? acc[i][r][g] + acs[i][r][g] : acc[i][r][g];
+                v[r][g] = p.exact ? x * p.inv_s : x / p.s;
+            }
+        if (qok && nlev > 0) {
+            float *row0 = p.lvl[0] + qrow * N;
+#pragma unroll
+            for (int r = 0; r < kPatchRows; ++r)
+                if (y0 + r < H) store4(row0 + (size_t)(y0 + r) * W, X0, W, v[r], p.mode0);
+        }
+        float l1[4][2];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            l1[r][0] = pool4(v[2 * r][0], v[2 * r][1], v[2 * r + 1][0], v[2 * r + 1][1]);
+            l1[r][1] = pool4(v[2 * r][2], v[2 * r][3], v[2 * r + 1][2], v[2 * r + 1][3]);
+        }
+        float l2[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) l2[r] = pool4(l1[2 * r][0], l1[2 * r][1], l1[2 * r + 1][0], l1[2 * r + 1][1]);
+        l2s[i][0] = l2[0], l2s[i][1] = l2[1];
+        if (p.cons) {
+            // Level 1 as 16-B stores: lanes grp 2m and 2m + 1 hold level-1 columns x0/2 + 4m + {0,1}
+            // and {2,3} of the patch's 4 rows; they swap one row's pair (lanes 16 apart) so that the
+            // even lane stores rows 0, 2 and the odd lane rows 1, 3, 4 columns each.
+            const bool odd = grp & 1;
+            const int X1 = (x0 >> 1) + 4 * (grp >> 1);
+#pragma unroll
+            for (int rp = 0; rp < 2; ++rp) {
+                const int ra = 2 * rp, rb = ra + 1, r = odd ? rb : ra;
+                const float g0 = __shfl_xor(odd ? l1[ra][0] : l1[rb][0], 16);
+                const float g1 = __shfl_xor(odd ? l1[ra][1] : l1[rb][1], 16);
+                const float4 o = odd ? make_float4(g0, g1, l1[rb][0], l1[rb][1]) : make_float4(l1[ra][0], l1[ra][1], g0, g1);
+                if (qok && nlev > 1 && (y0 >> 1) + r < H1 && X1 < W1)
+                    *reinterpret_cast<float4 *>(p.lvl[1] + qrow * N1 + (size_t)((y0 >> 1) + r) * W1 + X1) = o;
+            }
+        } else {
+            if (qok && nlev > 1) {
+                float *row1 = p.lvl[1] + qrow * N1;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if ((y0 >> 1) + r < H1) store2(row1 + (size_t)((y0 >> 1) + r) * W1, X0 >> 1, W1, l1[r][0], l1[r][1], p.mode1);
+            }
+            if (qok && nlev > 2) {
+                float *row2 = p.lvl[2] + qrow * N2;
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+                    if ((y0 >> 2) + r < H2 && (X0 >> 2) < W2) row2[((y0 >> 2) + r) * W2 + (X0 >> 2)] = l2[r];
+            }
+        }
+    }
+    // Levels 2 and 3 of BOTH query blocks in one store instruction each (an xor exchange has one
+    // receiver per sender, so every sender sends what its receiver's block needs).
+    if (p.cons) {
+        // Level 2: lanes grp 0..3 hold columns x0/4 + grp of 2 rows per block; lane g gathers row
+        // g & 1 of block g >> 1 (exchanges with lanes 16, 32, 48 apart), 16 B per lane.
+        const int bl = grp >> 1, rw = grp & 1;
+        auto sel = [&](int k) { return k == 0 ? l2s[0][0] : k == 1 ? l2s[0][1] : k == 2 ? l2s[1][0] : l2s[1][1]; };
+        const float t0 = sel(grp);
+        const float t1 = __shfl_xor(sel(grp ^ 1), 16), t2 = __shfl_xor(sel(grp ^ 2), 32), t3 = __shfl_xor(sel(grp ^ 3), 48);
+        // t_d is column grp ^ d of the wanted row, so component c (column c) is t_(c ^ grp)
+        auto pick = [&](int k) { return k == 0 ? t0 : k == 1 ? t1 : k == 2 ? t2 : t3; };
+        const float4 o = make_float4(pick(grp), pick(grp ^ 1), pick(grp ^ 2), pick(grp ^ 3));
+        const int q = (qb0 + bl) * 16 + ci;
+        if (q < NQ && nlev > 2 && (y0 >> 2) + rw < H2 && (x0 >> 2) < W2)
+            *reinterpret_cast<float4 *>(p.lvl[2] + ((size_t)b * NQ + q) * N2 + (size_t)((y0 >> 2) + rw) * W2 + (x0 >> 2)) = o;
+    }
+    {
+        // Level 3: the 2x2 window of level-2 values (a row pair in one lane, the column pair in the
+        // lanes 16 apart); even lanes pool block 0, odd lanes block 1, in ((a + b) + c) + d order.
+        const int bl = grp & 1;
+        const float y0v = __shfl_xor(bl ? l2s[0][0] : l2s[1][0], 16), y1v = __shfl_xor(bl ? l2s[0][1] : l2s[1][1], 16);
+        const float l3 = bl == 0 ? pool4(l2s[0][0], y0v, l2s[0][1], y1v) : pool4(y0v, l2s[1][0], y1v, l2s[1][1]);
+        const int q = (qb0 + bl) * 16 + ci;
+        const int Y3 = y0 >> 3, X3 = X0 >> 3;
+        if (q < NQ && nlev > 3 && Y3 < H3 && X3 < W3) p.lvl[3][((size_t)b * NQ + q) * N3 + Y3 * W3 + X3] = l3;
+    }
+}
+
+template <int SS, bool ACC2 = true>
+__global__ __launch_bounds__(256, 2) void corr_build_bf16_kernel(Args p) {
+    const Tile tl = patch_tile(xcd_swizzle(blockIdx.x, gridDim.x), p.npatch, p.NQG, p.CB, p.order);
+    // two whole code paths (no value flows out of either): a half patch runs half the MFMAs
+    if (SS > 0 && tl.py * kPatchRows + kPatchRows / 2 >= p.H) build_tile<SS, kPatchRows / 2, ACC2>(p, tl);
+    else build_tile<SS, kPatchRows, ACC2>(p, tl);
+}
+
+struct Ws {
+    u32x4_t *pq, *pt;
+};
+
+inline Ws workspace_of(void *ws, int B, const Geom &g) {
+    char *w = (char *)ws;
+    Ws r;
+    r.pq = (u32x4_t *)w;
+    w += align256((size_t)B * g.S * g.NQp * kPixBytes);
+    r.pt = (u32x4_t *)w;
+    return r;
+}
+
+template <int SS, bool ACC2 = true>
+hipError_t launch_kernel(dim3 grid, const Args &p, hipStream_t s) {
+    static std::atomic<unsigned long long> lds_done{0};
+    const hipError_t e = ensure_lds_limit((const void *)corr_build_bf16_kernel<SS, ACC2>, kLds, lds_done);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((corr_build_bf16_kernel<SS, ACC2>), grid, dim3(256), kLds, s, p);
+    return hipGetLastError();
+}
+
+
+// Workspace: the packed query and target images (3 KiB per K step and 16-pixel block).
+size_t workspace_bytes(int B, int D, int NQ, int H, int W) {
+    const Geom g = geom(D, NQ, H, W);
+    return align256((size_t)B * g.S * g.NQp * kPixBytes) + align256((size_t)B * g.S * g.Hp * g.Wp * kPixBytes);
+}
+
+hipError_t launch_pack(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, void *ws,
+                            hipStream_t s) {
+    const Geom g = geom(D, NQ, H, W);
+    const Ws w = workspace_of(ws, B, g);
+    PackArgs a{};
+    a.f[0] = f1, a.f[1] = f2;
+    a.pk[0] = w.pq, a.pk[1] = w.pt;
+    a.np[0] = NQ, a.np[1] = H * W;
+    a.nblk[0] = g.NQB, a.nblk[1] = g.Hp * g.CB;
+    a.D = D, a.S = g.S, a.H = H, a.W = W, a.CB = g.CB;
+    const int recs = g.S * std::max(a.nblk[0], a.nblk[1]);
+    hipLaunchKernelGGL(bf16_pack_kernel, dim3((unsigned)((recs + 3) / 4), B, 2), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// The MFMA part (operands already packed in ws).  levels == 0: the MFMAs and epilogue
+// arithmetic without stores (measurement).  variant 1: the single-accumulator form (ACC2 =
+// false; tools/kbench_build.hip A/B).
+hipError_t launch_mfma(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
+                       hipStream_t s, int variant = 0) {
+    const Geom g = geom(D, NQ, H, W);
+    const Ws w = workspace_of(ws, B, g);
+    Args p{};
+    p.pq = w.pq, p.pt = w.pt;
+    p.B = B, p.H = H, p.W = W, p.N = H * W, p.NQ = NQ, p.S = g.S;
+    p.nlev = std::min(levels, kFusedLevels);
+    for (int l = 0; l < kFusedLevels; ++l) p.lvl[l] = l < p.nlev ? pyr.p[l] : nullptr;
+    p.NQp = g.NQp, p.NQB = g.NQB, p.NQG = g.NQG, p.Hp = g.Hp, p.CB = g.CB;
+    p.npatch = (g.Hp / kPatchRows) * g.CB;
+    p.s = std::sqrt((float)D);
+    p.inv_s = 1.0f / p.s;
+    p.exact = is_pow2(p.s);
+    p.mode0 = p.nlev > 0 ? level_store_mode(W, pyr.p[0]) : 0;
+    p.mode1 = p.nlev > 1 ? level_store_mode(W >> 1, pyr.p[1]) : 0;
+    p.cons = p.mode1 == 2 && (p.nlev <= 2 || level_store_mode(W >> 2, pyr.p[2]) == 2);
+    p.order = 1;
+    const long tiles = (long)B * p.npatch * g.NQG;
+    if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)tiles);
+    hipError_t e;
+    if (variant == 1) {
+        if (g.S != 8) return hipErrorInvalidValue;
+        e = launch_kernel<8, false>(grid, p, s);
+    } else switch (g.S <= 8 ? g.S : 0) {
+#define CORR_BF16_CASE(c) \
+    case c: e = launch_kernel<c>(grid, p, s); break;
+        CORR_BF16_CASE(0) CORR_BF16_CASE(1) CORR_BF16_CASE(2) CORR_BF16_CASE(3) CORR_BF16_CASE(4)
+        CORR_BF16_CASE(5) CORR_BF16_CASE(6) CORR_BF16_CASE(7) CORR_BF16_CASE(8)
+#undef CORR_BF16_CASE
+        default: return hipErrorInvalidValue;
+    }
+    if (e != hipSuccess) return e;
+    if (levels > kFusedLevels) return launch_pool_levels(pyr, kFusedLevels, levels, (long)B * NQ, H, W, s);
+    return hipSuccess;
+}
+
+}  // namespace bf16b
+
+size_t build_bf16_workspace(int B, int D, int NQ, int H, int W) {
+    return bf16b::workspace_bytes(B, D, NQ, H, W);
+}
+
+// part: 0 = pack + MFMA; 1 = the pack alone; 2 = the MFMA kernel alone (measurement: the
+// workspace must already hold this pair's pack).
+hipError_t launch_build_bf16(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, int levels,
+                             const LevelPtrs &pyr, void *ws, hipStream_t s, int part) {
+    if (part != 2) {
+        const hipError_t e = bf16b::launch_pack(f1, NQ, f2, B, D, H, W, ws, s);
+        if (e != hipSuccess || part == 1) return e;
+    }
+    return bf16b::launch_mfma(NQ, B, D, H, W, levels, pyr, ws, s);
+}
+
+}  // namespace corr

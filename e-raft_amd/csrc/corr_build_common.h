@@ -10,6 +10,7 @@
 namespace corr {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void_t;
 
 // Blocks are dealt round-robin to the 8 XCDs; give each XCD a contiguous range of tiles
 // (which share operands in its L2) — bijective for any nwg (speed only).
@@ -45,5 +46,96 @@ inline bool is_pow2(float s) {
     int e;
     return std::frexp(s, &e) == 0.5f;
 }
+
+// ---------------------------------------------------------------------------------------
+// Shared by the two split builds (corr_build_split.hip, corr_build_bf16.hip): tile order,
+// LDS-DMA pieces and the pyramid's run stores.
+// ---------------------------------------------------------------------------------------
+constexpr int kGroupQ = 8;  // query groups per L2 tile group
+
+struct Tile {
+    int b, qg, py, cb;
+};
+
+// Tile t of (batch item, query group, target patch).  order 0: per batch item, query groups in
+// groups of kGroupQ; inside a group the query group runs fastest, then the patch (the ~64 tiles
+// one XCD has in flight cover ~8 patches x 8 query groups).  order 1: a patch row's patches
+// consecutive for one query group (the 64-B row segments of horizontally adjacent patches share
+// 128-B lines and are written close in time on one XCD).
+__device__ __forceinline__ Tile patch_tile(int t, int npatch, int NQG, int CB, int order) {
+    Tile o;
+    const int per_b = npatch * NQG;
+    o.b = t / per_b;
+    const int r = t - o.b * per_b;
+    const int g = r / (kGroupQ * npatch);
+    const int gm = min(kGroupQ, NQG - g * kGroupQ);
+    const int r2 = r - g * kGroupQ * npatch;
+    if (order == 1) {
+        o.py = r2 / (gm * CB);
+        const int r3 = r2 - o.py * gm * CB;
+        o.qg = g * kGroupQ + r3 / CB;
+        o.cb = r3 - (r3 / CB) * CB;
+        return o;
+    }
+    const int patch = r2 / gm;
+    o.qg = g * kGroupQ + (r2 - patch * gm);
+    o.py = patch / CB;
+    o.cb = patch - o.py * CB;
+    return o;
+}
+
+// s_waitcnt vmcnt(N) lgkmcnt(0) + s_barrier with N an immediate (the rings' hand-counted waits).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_barrier() {
+    static_assert(N >= 0 && N < 64, "vmcnt immediate");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// One LDS-DMA piece: 16 B per lane from g into LDS at lds + 16 * lane (global_load_lds_dwordx4;
+// M0 = the wave-uniform LDS base).  Counted in vmcnt like any vector load.  Inline asm, so the
+// compiler does not make every ds_read wait for all outstanding DMAs (it cannot tell ring slots
+// apart); the callers count vmcnt themselves.
+__device__ __forceinline__ void dma16(const void *g, uint32_t lds) {
+    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(lds) : "memory");
+}
+
+// One LDS-DMA dword per lane: g -> LDS at lds + 4 * lane.
+__device__ __forceinline__ void dma4(const void *g, uint32_t lds) {
+    asm volatile("global_load_lds_dword %0, off" ::"v"(g), "{m0}"(lds) : "memory");
+}
+
+// A run of 4 at column X (a multiple of 4) of a row of width Wl; mode per level (uniform):
+// 2 = one 16-B store, 1 = two 8-B stores, 0 = elements.
+__device__ __forceinline__ void store4(float *row, int X, int Wl, const float (&v)[4], int mode) {
+    if (mode == 2) {
+        if (X < Wl) *reinterpret_cast<float4 *>(row + X) = make_float4(v[0], v[1], v[2], v[3]);
+    } else if (mode == 1) {
+        if (X < Wl) *reinterpret_cast<float2 *>(row + X) = make_float2(v[0], v[1]);
+        if (X + 2 < Wl) *reinterpret_cast<float2 *>(row + X + 2) = make_float2(v[2], v[3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (X + k < Wl) row[X + k] = v[k];
+    }
+}
+
+// A run of 2 at an even column X.
+__device__ __forceinline__ void store2(float *row, int X, int Wl, float a, float b, int mode) {
+    if (mode >= 1) {
+        if (X < Wl) *reinterpret_cast<float2 *>(row + X) = make_float2(a, b);
+    } else {
+        if (X < Wl) row[X] = a;
+        if (X + 1 < Wl) row[X + 1] = b;
+    }
+}
+
+// Store width of one level's runs (columns X = 4k or 2k; row offsets are multiples of Wl).
+inline int level_store_mode(int Wl, const float *base) {
+    if (Wl % 4 == 0 && (uintptr_t)base % 16 == 0) return 2;
+    if (Wl % 2 == 0 && (uintptr_t)base % 8 == 0) return 1;
+    return 0;
+}
+
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace corr

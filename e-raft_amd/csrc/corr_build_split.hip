@@ -47,7 +47,6 @@ namespace corr {
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int kStepK = 32;                          // k per MFMA step
 constexpr int kRecU = 128;                          // u32x4 per record (2 KiB)
@@ -57,7 +56,6 @@ constexpr int kQPerWG = kWaves * kQPerWave;         // 128
 constexpr int kRing = 3;                            // LDS ring slots (prefetch distance 2)
 constexpr int kSlotBytes = kPatchRows * 2 * 1024;   // 16 KiB per K step
 constexpr int kBuildLds = kRing * kSlotBytes + kPatchRows * 16 * 4;
-constexpr int kGroupQ = 8;                          // query groups per L2 tile group
 constexpr int kMaxPackCpt = 8;                      // D <= 1024
 
 struct SplitGeom {
@@ -184,83 +182,8 @@ struct BuildArgs {
     int order;       // tile order: 0 = query group fastest (groups of kGroupQ), 1 = patch column fastest
 };
 
-// Tile order (L2 reuse): per batch item, query groups in groups of kGroupQ; inside a group the
-// query group runs fastest, then the target patch.  The ~64 tiles one XCD has in flight
-// (consecutive, xcd_swizzle) cover ~8 patches x 8 query groups (2 MiB of operands at D = 256).
-struct Tile {
-    int b, qg, py, cb;
-};
-
 __device__ __forceinline__ Tile tile_of(const BuildArgs &p, int t) {
-    Tile o;
-    const int per_b = p.npatch * p.NQG;
-    o.b = t / per_b;
-    const int r = t - o.b * per_b;
-    if (p.order == 1) {
-        // a patch row's patches consecutive for one query group: the 64-B row segments of
-        // horizontally adjacent patches share 128-B lines, written close in time (one XCD)
-        const int CB = p.CB, npr = p.npatch / CB;
-        const int g = r / (kGroupQ * p.npatch);
-        const int gm = min(kGroupQ, p.NQG - g * kGroupQ);
-        const int r2 = r - g * kGroupQ * p.npatch;
-        o.py = r2 / (gm * CB);
-        const int r3 = r2 - o.py * gm * CB;
-        o.qg = g * kGroupQ + r3 / CB;
-        o.cb = r3 - (r3 / CB) * CB;
-        (void)npr;
-        return o;
-    }
-    const int g = r / (kGroupQ * p.npatch);
-    const int gm = min(kGroupQ, p.NQG - g * kGroupQ);
-    const int r2 = r - g * kGroupQ * p.npatch;
-    const int patch = r2 / gm;
-    o.qg = g * kGroupQ + (r2 - patch * gm);
-    o.py = patch / p.CB;
-    o.cb = patch - o.py * p.CB;
-    return o;
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt_barrier() {
-    static_assert(N == 0 || N == 4 || N == 8, "vmcnt immediates used by the ring");
-    if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-// One LDS-DMA piece: 16 B per lane from g into LDS at lds + 16 * lane (global_load_lds_dwordx4;
-// M0 = the wave-uniform LDS base).  Counted in vmcnt like any vector load.
-__device__ __forceinline__ void dma16(const void *g, uint32_t lds) {
-    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(lds) : "memory");
-}
-
-// One LDS-DMA dword per lane: g -> LDS at lds + 4 * lane.
-__device__ __forceinline__ void dma4(const void *g, uint32_t lds) {
-    asm volatile("global_load_lds_dword %0, off" ::"v"(g), "{m0}"(lds) : "memory");
-}
-
-// A run of 4 at column X (a multiple of 4) of a row of width Wl; mode per level (uniform).
-__device__ __forceinline__ void store4(float *row, int X, int Wl, const float (&v)[4], int mode) {
-    if (mode == 2) {
-        if (X < Wl) *reinterpret_cast<float4 *>(row + X) = make_float4(v[0], v[1], v[2], v[3]);
-    } else if (mode == 1) {
-        if (X < Wl) *reinterpret_cast<float2 *>(row + X) = make_float2(v[0], v[1]);
-        if (X + 2 < Wl) *reinterpret_cast<float2 *>(row + X + 2) = make_float2(v[2], v[3]);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (X + k < Wl) row[X + k] = v[k];
-    }
-}
-
-// A run of 2 at an even column X.
-__device__ __forceinline__ void store2(float *row, int X, int Wl, float a, float b, int mode) {
-    if (mode >= 1) {
-        if (X < Wl) *reinterpret_cast<float2 *>(row + X) = make_float2(a, b);
-    } else {
-        if (X < Wl) row[X] = a;
-        if (X + 1 < Wl) row[X + 1] = b;
-    }
+    return patch_tile(t, p.npatch, p.NQG, p.CB, p.order);
 }
 
 // SS > 0: S = SS K steps, fully unrolled (straight-line code: the compiler's own waits on the
@@ -540,8 +463,6 @@ __global__ __launch_bounds__(256, 2) void corr_build_split_kernel(BuildArgs p) {
 // Host side.
 // ---------------------------------------------------------------------------------------
 namespace {
-size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
-
 struct SplitWs {
     u32x4 *pq, *pt;
     int *eq, *et;
@@ -558,13 +479,6 @@ SplitWs split_ws(void *ws, int B, const SplitGeom &g) {
     w += align256((size_t)B * g.NQp * 4);
     r.et = (int *)w;
     return r;
-}
-
-// Store width of one level's runs (columns X = 4k or 2k; row offsets are multiples of Wl).
-int store_mode(int Wl, const float *base) {
-    if (Wl % 4 == 0 && (uintptr_t)base % 16 == 0) return 2;
-    if (Wl % 2 == 0 && (uintptr_t)base % 8 == 0) return 1;
-    return 0;
 }
 
 }  // namespace
@@ -620,13 +534,11 @@ hipError_t launch_build_kernel(dim3 grid, const BuildArgs &p, hipStream_t s) {
 // The MFMA part (operands already packed in ws).  levels == 0: the MFMAs and epilogue
 // arithmetic without stores (measurement).  cons = false: levels 1-2 as element stores (the
 // previous epilogue, kept for the A/B; same bits).
-// Tile order of the build (BuildArgs::order): 1 = a patch row's patches consecutive for one
-// query group (the default: 1280x960 1006 -> 948 us, DSEC / train / MVSEC 1-4 % faster,
-// profiles/r03b_kbench_build_order.txt); tools/kbench_build.hip overrides it for the A/B.
-int g_tile_order = 1;
-
+// order: the build's tile order (BuildArgs::order): 1 = a patch row's patches consecutive for
+// one query group (the default: 1280x960 1006 -> 948 us, DSEC / train / MVSEC 1-4 % faster,
+// profiles/r03b_kbench_build_order.txt); tools/kbench_build.hip passes 0 for the A/B.
 hipError_t launch_split_mfma(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
-                             hipStream_t s, bool cons = true, int variant = 0) {
+                             hipStream_t s, bool cons = true, int variant = 0, int order = 1) {
     const SplitGeom g = split_geom(D, NQ, H, W);
     const SplitWs w = split_ws(ws, B, g);
     BuildArgs p{};
@@ -645,10 +557,10 @@ hipError_t launch_split_mfma(int NQ, int B, int D, int H, int W, int levels, con
         std::frexp(p.inv_s, &e);
         p.eshift = e - 1;  // 1/s = 2^(e-1)
     }
-    p.mode0 = p.nlev > 0 ? store_mode(W, pyr.p[0]) : 0;
-    p.mode1 = p.nlev > 1 ? store_mode(W >> 1, pyr.p[1]) : 0;
-    p.cons = cons && p.mode1 == 2 && (p.nlev <= 2 || store_mode(W >> 2, pyr.p[2]) == 2);
-    p.order = g_tile_order;
+    p.mode0 = p.nlev > 0 ? level_store_mode(W, pyr.p[0]) : 0;
+    p.mode1 = p.nlev > 1 ? level_store_mode(W >> 1, pyr.p[1]) : 0;
+    p.cons = cons && p.mode1 == 2 && (p.nlev <= 2 || level_store_mode(W >> 2, pyr.p[2]) == 2);
+    p.order = order;
     const long tiles = (long)B * p.npatch * g.NQG;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
     const dim3 grid((unsigned)tiles);

@@ -251,11 +251,10 @@ hipError_t run_gemm(bool b_kcontig, const float *A, const float *Bm, float *C, i
 
 }  // namespace
 
-int g_reduce_vec4 = 1;  // measurement override (tools/kbench_gemm.hip A/B): 0 = the scalar reduce
-
 // Ordered split-K sum + 1/sqrt(D) for corr_bwd_split.hip's slabs ([split][per] floats).
-hipError_t launch_splitk_reduce(const float *ws, float *C, int splits, size_t per, float sD, hipStream_t s) {
-    if (per % 4 == 0 && ((uintptr_t)ws & 15) == 0 && ((uintptr_t)C & 15) == 0 && g_reduce_vec4) {
+// vec4 = false: the scalar reduce (tools/kbench_gemm.hip A/B).
+hipError_t launch_splitk_reduce(const float *ws, float *C, int splits, size_t per, float sD, hipStream_t s, bool vec4) {
+    if (per % 4 == 0 && ((uintptr_t)ws & 15) == 0 && ((uintptr_t)C & 15) == 0 && vec4) {
         const size_t per4 = per / 4;
         const int grid = (int)std::min<size_t>((per4 + 255) / 256, 8192);
         hipLaunchKernelGGL(splitk_reduce_vec4_kernel, dim3(grid), dim3(256), 0, s, (const float4 *)ws, (float4 *)C,

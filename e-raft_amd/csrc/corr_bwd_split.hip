@@ -331,7 +331,6 @@ __device__ __forceinline__ void split2(float x0, float x1, int s, bool guard, ha
 constexpr int kWI = 2, kWJ = 2, kMI = 2, kNJ = 4;
 constexpr int kTI = 32 * kMI * kWI;   // 128
 constexpr int kTJ = 32 * kNJ * kWJ;   // 256
-constexpr int kRows = kTI + kTJ;      // LDS rows per stage (64 B each)
 constexpr int kNT = 256;
 static_assert(kTI == kNT / 2 && kTJ == kNT, "staging: one A row-octet and two B row-octets per thread");
 
@@ -382,8 +381,7 @@ __device__ __forceinline__ void gemm_wait_vm_barrier() {
 }
 
 // Dynamic LDS of the GEMM: the hi/lo staging (2 stages; DMA: 1), the row exponents, and (DMA)
-// a 2-slot ring of raw fp32 chunks (kRows rows x 16 k; BCOL: B as 16 k-rows x 256 columns).
-constexpr int kRawFloats = kRows * kBK;  // per ring slot
+// a 2-slot ring of raw fp32 chunks (kTI + kTJ rows x 16 k; BCOL: B as 16 k-rows x 256 columns).
 template <bool DMA, int WI = kWI>
 constexpr int gemm_lds_bytes() {
     constexpr int rows = 32 * kMI * WI + kTJ;
@@ -405,8 +403,7 @@ __device__ __forceinline__ unsigned split_lo_mix(unsigned h2, float y0, float y1
     return lo;
 }
 
-// MIX = false: the lo half by convert back + subtract + convert (measurement A/B only).
-template <bool BCOL, bool DMA = false, bool MIX = true, int WI = kWI>
+template <bool BCOL, bool DMA = false, int WI = kWI>
 __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmParams p) {
     // WI = 4 (DMA path only): 8 waves, a 256 x 256 tile (each wave still 64 x 128), so every
     // staged element feeds twice the MFMAs
@@ -528,10 +525,7 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
                 for (int t = 0; t < 4; ++t) {
                     const f32x2v y = f32x2v{v[2 * t], v[2 * t + 1]} * f32x2v{f, f};
                     h[t] = __builtin_convertvector(y, half2v);
-                    if constexpr (MIX)
-                        l[t] = __builtin_bit_cast(half2v, split_lo_mix(__builtin_bit_cast(unsigned, h[t]), y[0], y[1]));
-                    else
-                        l[t] = __builtin_convertvector(y - __builtin_convertvector(h[t], f32x2v), half2v);
+                    l[t] = __builtin_bit_cast(half2v, split_lo_mix(__builtin_bit_cast(unsigned, h[t]), y[0], y[1]));
                 }
             } else {
 #pragma unroll
@@ -724,13 +718,17 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
 // 436 us with 5 splits = 560 workgroups, 401 us with 3).
 constexpr long kGemmSlots = 512;
 
-int g_gemm_splits = 0;  // measurement override of the split count (tools/kbench_gemm.hip); 0 = plan
-int g_gemm_dma = 1;     // LDS-DMA operand ring when the shape allows (tools/kbench_gemm.hip A/B)
-int g_gemm_mix = 1;     // lo halves by v_fma_mix (0: convert back + subtract; CORR_GEMM_AB builds only)
-int g_gemm_wide = 1;    // 256 x 256 tiles of 8 waves on the DMA path when NI > 128 (0: kbench A/B)
+// Plan knobs of the backward GEMMs.  The library always runs the defaults; tools/kbench_gemm.hip
+// passes others for its A/B runs (no global state).
+struct GemmTune {
+    int splits = 0;          // split-K count override (0 = plan_split_k's plan)
+    bool dma = true;         // LDS-DMA operand ring when the shape allows
+    bool wide = true;        // 256 x 256 tiles of 8 waves on the DMA path when NI > 128
+    bool reduce_vec4 = true; // the 16-B split-K reduce when aligned
+};
 
-int plan_split_k(int NI, int NJ, int nkc, int batch) {
-    if (g_gemm_splits > 0) return g_gemm_splits;
+int plan_split_k(int NI, int NJ, int nkc, int batch, const GemmTune &t = GemmTune{}) {
+    if (t.splits > 0) return t.splits;
     const long tiles = (long)((NI + kTI - 1) / kTI) * ((NJ + kTJ - 1) / kTJ) * batch;
     long splits = std::max(1L, kGemmSlots / tiles);
     splits = std::min<long>(splits, std::max(1, nkc / 8));  // >= 128 k per split
@@ -764,10 +762,10 @@ BwdWs carve(void *ws, int B, int D, int NQ, int N) {
     return r;
 }
 
-size_t slab_floats(int B, int D, int NQ, int N) {
+size_t slab_floats(int B, int D, int NQ, int N, const GemmTune &t = GemmTune{}) {
     const int K1 = (N + kBK - 1) / kBK, K2 = (NQ + kBK - 1) / kBK;
-    const size_t s1 = (size_t)plan_split_k(D, NQ, K1, B) * B * D * NQ;
-    const size_t s2 = (size_t)plan_split_k(D, N, K2, B) * B * D * N;
+    const size_t s1 = (size_t)plan_split_k(D, NQ, K1, B, t) * B * D * NQ;
+    const size_t s2 = (size_t)plan_split_k(D, N, K2, B, t) * B * D * N;
     return std::max(s1, s2);
 }
 
@@ -790,15 +788,14 @@ hipError_t rowmax2(const float *X0, int cols0, unsigned *rmax0, const float *X1,
 
 }  // namespace
 
-hipError_t launch_splitk_reduce(const float *ws, float *C, int splits, size_t per, float sD, hipStream_t s);
-
-namespace {
-}  // namespace
-
-size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W) {
+size_t bwd_split_workspace_tuned(int B, int D, int NQ, int H, int W, const GemmTune &t) {
     const int N = H * W;
     const size_t R = std::max(NQ, N);
-    return 2 * al256((size_t)B * D * 4) + 2 * al256((size_t)B * R * 4) + slab_floats(B, D, NQ, N) * sizeof(float);
+    return 2 * al256((size_t)B * D * 4) + 2 * al256((size_t)B * R * 4) + slab_floats(B, D, NQ, N, t) * sizeof(float);
+}
+
+size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W) {
+    return bwd_split_workspace_tuned(B, D, NQ, H, W, GemmTune{});
 }
 
 // The GEMMs once dC's row maxima (w.mxB) and column maxima (w.mxC) are in the workspace.
@@ -806,7 +803,7 @@ size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W) {
 template <bool BCOL>
 hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long b_sb, long b_sr, long b_sk,
                     const unsigned *mxA, const unsigned *mxB, int B, int NI, int NJ, int K, float sD, float *C,
-                    float *slab, hipStream_t s) {
+                    float *slab, hipStream_t s, const GemmTune &t = GemmTune{}) {
     FGemmParams p{};
     p.A = A, p.a_sb = a_sb, p.a_sr = a_sr;
     p.Bm = Bm, p.b_sb = b_sb, p.b_sr = b_sr, p.b_sk = b_sk;
@@ -815,7 +812,7 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     p.nkc = (K + kBK - 1) / kBK;
     p.ti = (NI + kTI - 1) / kTI;
     p.tj = (NJ + kTJ - 1) / kTJ;
-    p.splits = plan_split_k(NI, NJ, p.nkc, B);
+    p.splits = plan_split_k(NI, NJ, p.nkc, B, t);
     p.kc_per = (p.nkc + p.splits - 1) / p.splits;
     p.splits = (p.nkc + p.kc_per - 1) / p.kc_per;
     const bool exact = is_pow2(sD);
@@ -825,21 +822,21 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     auto al16 = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
     p.vec = al16(A) && al16(Bm) && a_sb % 4 == 0 && a_sr % 4 == 0 && b_sb % 4 == 0 &&
             (BCOL ? b_sk % 4 == 0 : b_sr % 4 == 0);
-    const bool dma = g_gemm_dma && p.vec && K % kBK == 0 && (!BCOL || NJ % 4 == 0);
+    const bool dma = t.dma && p.vec && K % kBK == 0 && (!BCOL || NJ % 4 == 0);
     // 256-row tiles when there are more than 128 rows (D = 256): every staged element feeds twice
     // the MFMAs, a third less split work per MFMA (train: dF1 73 -> 67, dF2 75 -> 67 us)
-    const bool wide = dma && g_gemm_wide && NI > 32 * kMI * kWI;
+    const bool wide = dma && t.wide && NI > 32 * kMI * kWI;
     hipError_t e;
-    auto go = [&](auto dma_tag, auto mix_tag, auto wi_tag) {
-        constexpr bool D = decltype(dma_tag)::value, M = decltype(mix_tag)::value;
+    auto go = [&](auto dma_tag, auto wi_tag) {
+        constexpr bool D = decltype(dma_tag)::value;
         constexpr int WI = decltype(wi_tag)::value;
         FGemmParams q = p;
         q.ti = (NI + 32 * kMI * WI - 1) / (32 * kMI * WI);
         const long grid = (long)q.ti * q.tj * q.splits * B;
         static std::atomic<unsigned long long> done{0};
-        hipError_t e2 = ensure_lds_limit((const void *)split_gemm_f32_kernel<BCOL, D, M, WI>, gemm_lds_bytes<D, WI>(), done);
+        hipError_t e2 = ensure_lds_limit((const void *)split_gemm_f32_kernel<BCOL, D, WI>, gemm_lds_bytes<D, WI>(), done);
         if (e2 != hipSuccess) return e2;
-        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, D, M, WI>), dim3((unsigned)grid), dim3(64 * WI * kWJ),
+        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, D, WI>), dim3((unsigned)grid), dim3(64 * WI * kWJ),
                            (gemm_lds_bytes<D, WI>()), s, q);
         return hipSuccess;
     };
@@ -847,15 +844,11 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     using F_ = std::false_type;
     using W2 = std::integral_constant<int, kWI>;
     using W4 = std::integral_constant<int, 4>;
-#ifdef CORR_GEMM_AB  // tools/kbench_gemm.hip: the convert-back split as well
-    if (!g_gemm_mix) e = dma ? go(T_{}, F_{}, W2{}) : go(F_{}, F_{}, W2{});
-    else
-#endif
-    e = wide ? go(T_{}, T_{}, W4{}) : dma ? go(T_{}, T_{}, W2{}) : go(F_{}, T_{}, W2{});
+    e = wide ? go(T_{}, W4{}) : dma ? go(T_{}, W2{}) : go(F_{}, W2{});
     if (e != hipSuccess) return e;
     e = hipGetLastError();
     if (e != hipSuccess || p.direct) return e;
-    return launch_splitk_reduce(slab, C, p.splits, (size_t)B * NI * NJ, sD, s);
+    return launch_splitk_reduce(slab, C, p.splits, (size_t)B * NI * NJ, sD, s, t.reduce_vec4);
 }
 
 // rowmax_done: F2's and F1's row maxima are already in w.mxA / w.mxA2 (computed by the fold

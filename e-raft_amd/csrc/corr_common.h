@@ -62,6 +62,13 @@ size_t build_split_workspace(int B, int D, int NQ, int H, int W);
 bool build_split_supported(int D);
 hipError_t launch_build_split(const float *f1, int NQ, const float *f2, int B, int D, int H, int W,
                               int levels, const LevelPtrs &pyr, void *ws, hipStream_t s, int part = 0);
+// The bf16 three-piece build (corr_build_bf16.hip): pack kernel + bf16 MFMA kernel.
+size_t build_bf16_workspace(int B, int D, int NQ, int H, int W);
+hipError_t launch_build_bf16(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, int levels,
+                             const LevelPtrs &pyr, void *ws, hipStream_t s, int part = 0);
+// Ordered split-K sum + 1/sqrt(D) of [splits][per] partial slabs into C (corr_bwd.hip).
+hipError_t launch_splitk_reduce(const float *ws, float *C, int splits, size_t per, float sD, hipStream_t s,
+                                bool vec4 = true);
 size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W);
 hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, const float *f2, int B, int D, int H,
                                   int W, float *df1, float *df2, void *ws, hipStream_t s);

@@ -1399,11 +1399,17 @@ size_t fused_lds_bytes(int H, int W, int levels, FusedOut *o) {
 template <int S>
 hipError_t launch_fused_s(const BwdLookups &lk, FusedOut o, hipStream_t s) {
     const size_t bytes = fused_lds_bytes<S>(o.H, o.W, o.L, &o);
-    if (bytes > 160 * 1024) return hipErrorNotSupported;
     // the dynamic-LDS limit is raised once per device to the largest image this path accepts
-    // (not to this call's size: a later, larger shape must not run against a smaller limit)
+    // (not to this call's size: a later, larger shape must not run against a smaller limit),
+    // capped at what the device offers per workgroup
+    int dev = 0, dev_max = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&dev_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
+    if (e != hipSuccess) return e;
+    const int limit = std::min(160 * 1024, dev_max);
+    if (bytes > (size_t)limit) return hipErrorNotSupported;
     static std::atomic<unsigned long long> done{0};
-    hipError_t e = ensure_lds_limit((const void *)lookup_bwd_fold_kernel<S>, 160 * 1024, done);
+    e = ensure_lds_limit((const void *)lookup_bwd_fold_kernel<S>, limit, done);
     if (e != hipSuccess) return e;
     const int nqb = (o.NQ + FusedStage<S>::BQ - 1) / FusedStage<S>::BQ;
     o.nfold = nqb * o.B;

@@ -31,22 +31,31 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
            "corr_voxel_grid_tbilinear", "corr_lookup_bwd_multi", "corr_pool_fold", "corr_backward_workspace",
            "corr_backward", "corr_convex_upsample_bwd_workspace", "corr_convex_upsample_bwd")
 
-# Build algorithms (include/corr_mi355x.h).  F16X3 is the default: fp32 features split into
-# f16 hi/lo pairs, three f16 MFMAs per product, fp32 accumulate (~1e-6 of max|C| from the
-# exact-fp32 MFMA build; both are inside the north_star's 1e-4).  ERAFT_AMD_BUILD=fp32
-# selects the fp32-operand MFMA build instead.
+# Build algorithms (include/corr_mi355x.h).  BF16X6 is the default: every fp32 feature split
+# exactly into three bf16 pieces, the six largest piece products on the bf16 MFMA, fp32
+# accumulate — no narrower than the exact-fp32 MFMA build (test_build_bf16x6_not_narrower_than_fp32).
+# ERAFT_AMD_BUILD=fp32 selects the fp32-operand MFMA build, =f16x3 the two-piece f16 split
+# (~2^-22 per feature, narrower than fp32).
 BUILD_FP32 = 0
 BUILD_F16X3 = 1
-BUILD_ONLY_PACK = 0x100  # measurement: OR into BUILD_F16X3 to run only the operand pack
+BUILD_BF16X6 = 2
+BUILD_ONLY_PACK = 0x100  # measurement: OR into BUILD_F16X3 / _BF16X6 to run only the operand pack
 BUILD_ONLY_MFMA = 0x200  # ... or only the MFMA kernel (the workspace holds this pair's pack)
-_ALGOS = {"fp32": BUILD_FP32, "f16x3": BUILD_F16X3}
+_ALGOS = {"fp32": BUILD_FP32, "f16x3": BUILD_F16X3, "bf16x6": BUILD_BF16X6}
 
 
 def default_algo() -> int:
-    name = os.environ.get("ERAFT_AMD_BUILD", "f16x3").lower()
+    name = os.environ.get("ERAFT_AMD_BUILD", "bf16x6").lower()
     if name not in _ALGOS:
         raise ValueError(f"ERAFT_AMD_BUILD must be one of {sorted(_ALGOS)} (got {name!r})")
     return _ALGOS[name]
+
+
+def backward_algo(algo=None) -> int:
+    """The backward GEMMs' algorithm for a build algorithm: the f16x3 split GEMMs serve the
+    f16x3 and bf16x6 builds, the fp32 GEMMs the fp32 build."""
+    algo = default_algo() if algo is None else algo
+    return BUILD_FP32 if algo == BUILD_FP32 else BUILD_F16X3
 
 _lib = None
 
@@ -177,7 +186,7 @@ def build_workspace(fmap1, fmap2, algo=None):
 def build(fmap1, fmap2, levels, algo=None, workspace=None):
     """corr_build_ex into caller-allocated levels [B*NQ, 1, H>>l, W>>l].  fmap1 may be a row
     slab [B, D, rows, W] of the query map; fmap2 is the full target map [B, D, H, W].
-    algo: BUILD_F16X3 (default, see default_algo) or BUILD_FP32."""
+    algo: BUILD_BF16X6 (default, see default_algo), BUILD_F16X3 or BUILD_FP32."""
     algo = default_algo() if algo is None else algo
     B, D, H, W = fmap2.shape
     a, b, pp = _dev(fmap1, "fmap1"), _dev(fmap2, "fmap2"), _ptrs(levels, "pyr")
@@ -222,8 +231,8 @@ def pool_bwd(grad_levels, H, W):
 def build_bwd(grad_c, fmap1, fmap2, algo=None):
     """Returns (dfmap1, dfmap2) for grad_c = dLoss/dcorr ([B*NQ, H*W] or any view of it).
     With a row slab fmap1, dfmap1 is the slab's and dfmap2 is this slab's partial sum.
-    algo: BUILD_F16X3 (default, as the forward) or BUILD_FP32 (corr_build_bwd_ex)."""
-    algo = default_algo() if algo is None else algo
+    algo: BUILD_F16X3 (default, see backward_algo) or BUILD_FP32 (corr_build_bwd_ex)."""
+    algo = backward_algo() if algo is None else algo
     B, D, H, W = fmap2.shape
     for t, nm in ((grad_c, "grad_c"), (fmap1, "fmap1"), (fmap2, "fmap2")):
         _dev(t, nm)
@@ -265,8 +274,9 @@ def pool_fold(grad_levels, B, H, W):
 
 def backward(coords_list, grad_list, radius, grad_levels, fmap1, fmap2, algo=None):
     """corr_backward: (dfmap1, dfmap2) of one build and its lookups (all at once, in order).
-    grad_levels: scratch gradient pyramid (overwritten; level 0 ends as dLoss/dcorr)."""
-    algo = default_algo() if algo is None else algo
+    grad_levels: scratch gradient pyramid (overwritten; level 0 ends as dLoss/dcorr).
+    algo: the GEMMs' algorithm (default: backward_algo())."""
+    algo = backward_algo() if algo is None else algo
     B, D, H, W = fmap2.shape
     lib = load()
     NQ = _nq(fmap1)

@@ -14,7 +14,7 @@ SRC = os.path.join(os.path.dirname(PKG), "csrc")
 OUT_DIR = os.path.join(PKG, "_build")
 SO_NAME = "libcorr_mi355x.so"
 SO_PATH = os.path.join(OUT_DIR, SO_NAME)
-SOURCES = ["corr_build.hip", "corr_build_split.hip", "corr_lookup.hip", "corr_bwd.hip", "corr_bwd_split.hip", "corr_splat.hip",
+SOURCES = ["corr_build.hip", "corr_build_split.hip", "corr_build_bf16.hip", "corr_lookup.hip", "corr_bwd.hip", "corr_bwd_split.hip", "corr_splat.hip",
            "corr_upsample.hip", "corr_voxel.hip",
            "corr_api.cpp"]
 HEADERS = ["corr_common.h", "corr_build_common.h", os.path.join("..", "..", "include", "corr_mi355x.h")]

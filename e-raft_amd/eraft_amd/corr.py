@@ -21,6 +21,8 @@ avg-pool backward folded into level 0 in one pass, and the two MFMA GEMMs.
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 
 from . import _lib
@@ -62,16 +64,20 @@ def _validate_fmaps(fmap1, fmap2, num_levels):
         raise RuntimeError(f"{H}x{W} feature maps are too small for {num_levels} pyramid levels")
 
 
+_WEIGHT_PACKS = weakref.WeakKeyDictionary()
+
+
 def _weight_pack(weight):
-    """convc1.weight's packed split for lookup_conv, cached ON the weight tensor itself with the
-    (data_ptr, _version) it was made from: a new tensor (another model, a reloaded checkpoint)
-    never sees another tensor's pack, and an in-place update (optimizer step, load_state_dict's
-    copy_) bumps _version and re-packs."""
+    """convc1.weight's packed split for lookup_conv, cached per weight tensor (a weak-keyed map,
+    so nothing is attached to the Parameter: pickling or torch.save of the model is unaffected,
+    and the pack dies with its tensor) together with the (data_ptr, _version) it was made from:
+    a new tensor (another model, a reloaded checkpoint) never sees another tensor's pack, and an
+    in-place update (optimizer step, load_state_dict's copy_) bumps _version and re-packs."""
     key = (weight.data_ptr(), weight._version)
-    cached = getattr(weight, "_eraft_amd_pack", None)
+    cached = _WEIGHT_PACKS.get(weight)
     if cached is None or cached[0] != key:
         cached = (key, _lib.lookup_conv_weights(weight))
-        weight._eraft_amd_pack = cached
+        _WEIGHT_PACKS[weight] = cached
     return cached[1]
 
 
@@ -174,7 +180,7 @@ class _LookupFn(torch.autograd.Function):
 class _LookupConvFn(torch.autograd.Function):
     """relu(convc1(lookup(coords))) (update.py:68,75) as one fused kernel in the forward; the
     324-channel lookup output is never written.  Backward (training, config 4): g = dL/dout
-    masked by out > 0 (ReLU's threshold backward); d bias = sum of g; the lookup is recomputed
+    zeroed where out <= 0 (ReLU's threshold backward); d bias = sum of g; the lookup is recomputed
     by the lookup kernel (bit-identical to the forward's values) for dW = g lk^T; the lookup's
     own gradient W^T g goes into the build's stash, exactly as a plain lookup's backward does,
     so corr_backward folds it with every other lookup."""
@@ -194,8 +200,8 @@ class _LookupConvFn(torch.autograd.Function):
         coords, weight, out = ctx.saved_tensors
         st = ctx.state
         g = grad_out.contiguous()
-        if ctx.relu:
-            g = torch.where(out > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
+        if ctx.relu:  # threshold_backward: zero where out <= 0 (a NaN output passes its gradient, as torch.relu's)
+            g = torch.where(out <= 0, torch.zeros((), dtype=g.dtype, device=g.device), g)
         B, O, H, W = g.shape
         C = weight.shape[1]
         gf = g.view(B, O, H * W)

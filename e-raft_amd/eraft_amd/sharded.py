@@ -194,7 +194,15 @@ class Fmap2DoubleBuffer:
     argument is that rank's fmap2 (it is copied into the buffer on the compute stream, so the
     caller may reuse its own tensor); the other ranks pass None.  Stream order makes the
     reuse safe: the collective waits for the compute stream's earlier work (pair k-1's build,
-    the last reader of the buffer it overwrites) before it starts."""
+    the last reader of the buffer it overwrites) before it starts.
+
+    Inference only: the buffers are detached copies that the prefetch two pairs later
+    overwrites, so no gradient could reach the caller's fmap2 through them, and a delayed
+    backward would read a later pair's features.  prefetch() raises on the source rank when
+    handed an fmap2 that requires grad with autograd enabled (after its broadcast completed, so
+    the other ranks are not left inside it), and RowShardedCorrBlock raises on every rank when
+    handed a PendingFmap2 while its fmap1 requires grad; train with the blocking broadcast
+    (RowShardedCorrBlock(fmap1, fmap2))."""
 
     def __init__(self, shape, device, group=None, src=0, dtype=torch.float32):
         self.group, self.src = group, src
@@ -209,7 +217,14 @@ class Fmap2DoubleBuffer:
             if fmap2 is None:
                 raise ValueError(f"rank {self.src} is the broadcast source: pass its fmap2")
             buf.copy_(fmap2.detach())
-        return RowShardedCorrBlock.prefetch(buf, src=self.src, group=self.group)
+        pending = RowShardedCorrBlock.prefetch(buf, src=self.src, group=self.group)
+        if self.rank == self.src and torch.is_grad_enabled() and fmap2.requires_grad:
+            # refuse only after the broadcast is issued and done, so the other ranks' matching
+            # broadcast completes and no rank is left inside a collective
+            pending.wait()
+            raise RuntimeError("Fmap2DoubleBuffer is inference-only (its buffers carry no gradient "
+                               "back to fmap2); train with RowShardedCorrBlock(fmap1, fmap2)")
+        return pending
 
 
 class RowShardedCorrBlock:
@@ -241,6 +256,12 @@ class RowShardedCorrBlock:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         if isinstance(fmap2, PendingFmap2):  # broadcast already issued (prefetch): wait for it
+            if torch.is_grad_enabled() and fmap1.requires_grad:
+                # every rank sees the same fmap1 flag (SPMD), so all ranks refuse together and
+                # none is left waiting in a gradient all-reduce
+                raise RuntimeError("a prefetched (double-buffered) fmap2 is inference-only: its buffer "
+                                   "carries no gradient and is overwritten two pairs later; train with "
+                                   "RowShardedCorrBlock(fmap1, fmap2)")
             fmap2 = fmap2.wait()
             broadcast = False
         B, D, H, W = fmap2.shape

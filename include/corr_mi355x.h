@@ -54,15 +54,24 @@ const char *corr_last_error(void);
  *   pyr[l][q][y][x]       = avg_pool2d(pyr[l-1], 2, stride 2)[q][y][x]   (floor)
  * `pyr` is a HOST array of `levels` device pointers.  levels == 1 gives CorrBlock.corr's
  * [B,H,W,1,H,W] volume.  fp32 in / fp32 MFMA accumulate / fp32 out (CORR_BUILD_FP32;
- * corr_build_ex selects the faster CORR_BUILD_F16X3).
+ * corr_build_ex selects the faster CORR_BUILD_BF16X6, no less accurate, or CORR_BUILD_F16X3).
  */
 int corr_build(const float *fmap1, const float *fmap2, int B, int D, int H, int W, int levels,
                float *const *pyr, void *stream);
 
 /*
  * Build algorithms for corr_build_ex (same outputs, same pyramid arithmetic; they differ only
- * in how the fp32 dot products are formed — both accumulate in fp32):
+ * in how the fp32 dot products are formed — all accumulate in fp32):
  *   CORR_BUILD_FP32   fp32 operands on v_mfma_f32_32x32x2_f32 (the corr_build path).
+ *   CORR_BUILD_BF16X6 each fp32 feature is split EXACTLY into three bf16 pieces, x = hi + mid +
+ *                     lo (bf16 keeps fp32's exponent range: no scale, no flush — the one floor
+ *                     is lo's bf16 subnormal range, |x| < ~2^-110); six bf16 MFMAs per product
+ *                     (every piece pair of weight >= 2^-16: lo*hi + hi*lo + mid*mid + mid*hi +
+ *                     hi*mid + hi*hi) into one fp32 accumulator.  The dropped terms are <= 2^-23
+ *                     of |x_t x_q| and the accumulator rounds 6D/32 times per dot product (an fp32
+ *                     fmaf chain: D times): no narrower than CORR_BUILD_FP32 (checked per query
+ *                     row against an fp64 oracle).  Needs a workspace for the split operands.
+ *                     ~2x faster than CORR_BUILD_FP32 on gfx950.
  *   CORR_BUILD_F16X3  each fp32 feature x of pixel n is split as 2^e_n * (hi + lo), f16 hi/lo,
  *                     e_n putting the pixel's largest |x| in [2^14, 2^15); three f16 MFMAs
  *                     (hi*hi + hi*lo + lo*hi) per product into one fp32 accumulator.  Each
@@ -72,7 +81,8 @@ int corr_build(const float *fmap1, const float *fmap2, int B, int D, int H, int 
  */
 #define CORR_BUILD_FP32 0
 #define CORR_BUILD_F16X3 1
-/* Measurement only (OR-ed into CORR_BUILD_F16X3): run just one of its two kernels — the
+#define CORR_BUILD_BF16X6 2
+/* Measurement only (OR-ed into CORR_BUILD_F16X3 / _BF16X6): run just one of its two kernels — the
  * operand pack, or the MFMA build from a workspace that already holds this pair's pack — so a
  * benchmark can time each kernel on its own.  The pyramid is complete only after both. */
 #define CORR_BUILD_ONLY_PACK 0x100
@@ -217,8 +227,10 @@ size_t corr_forward_splat_workspace(int B, int H, int W);
  * (per-query and per-output-channel power-of-two scales; |error| ~ 2^-22 of the larger operands,
  * the build's f16x3 contract).  The weight (convc1.weight viewed [256][L*K], fp32) is split once
  * per weight version by corr_lookup_conv_weights into a corr_lookup_conv_weights_bytes() buffer;
- * out [B][256][H][W].  radius 4, levels <= 4 (E-RAFT); CORR_EUNSUPPORTED otherwise.  Inference
- * (no gradient).
+ * out [B][256][H][W].  radius 4, levels <= 4 (E-RAFT); CORR_EUNSUPPORTED otherwise.  This call
+ * is the forward only; its training backward is composed from the other entry points (the
+ * Python side's _LookupConvFn: corr_lookup_conv_bwd for dW / bias and the lookup's gradient
+ * W^T g into corr_backward's lookup list).
  */
 size_t corr_lookup_conv_weights_bytes(void);
 int corr_lookup_conv_weights(const float *weight, int out_channels, int in_channels, void *packed, void *stream);

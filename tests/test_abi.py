@@ -82,6 +82,14 @@ def test_build_ex_workspace_and_validation(lib):
     assert n >= 2 * 4800 * 256 * 4 + 2 * 4800 * 4
     assert lib.corr_build_workspace(0, 1, 256, 4800, 60, 80) == 0  # fp32 needs none
     assert lib.corr_build_workspace(1, 1, 10 ** 6, 4800, 60, 80) == ctypes.c_size_t(-1).value
+    # BF16X6 workspace: hi/mid/lo bf16 operands (6 B per padded channel per pixel), any D
+    n = lib.corr_build_workspace(2, 1, 256, 4800, 60, 80)
+    assert n >= 2 * 4800 * 256 * 6
+    assert lib.corr_build_workspace(2, 1, 1000, 4800, 60, 80) >= 2 * 4800 * 1000 * 6
+    assert lib.corr_build_workspace(9, 1, 256, 4800, 60, 80) == ctypes.c_size_t(-1).value
+    rc = lib.corr_build_ex(2, 256, 4800, 256, 1, 256, 60, 80, 4, pyr := (ctypes.c_void_p * 4)(256, 256, 256, 256),
+                           256, 16, None)
+    assert rc == -1 and "workspace" in lib.corr_last_error().decode()
     pyr = (ctypes.c_void_p * 4)(256, 256, 256, 256)
     rc = lib.corr_build_ex(1, 256, 4800, 256, 1, 256, 60, 80, 4, pyr, 256, 16, None)
     assert rc == -1 and "workspace" in lib.corr_last_error().decode()
@@ -91,8 +99,8 @@ def test_build_ex_workspace_and_validation(lib):
     assert rc == -1 and "unknown algorithm" in lib.corr_last_error().decode()
     rc = lib.corr_build_ex(1, 256, 4800, 256, 1, 256, 60, 80, 4, pyr, 260, 1 << 40, None)
     assert rc == -1 and "256-byte aligned" in lib.corr_last_error().decode()
-    # measurement phase flags: one at a time, and only on the f16x3 build
-    for algo in (0x100 | 0x200 | 1, 0x100 | 0, 0x200 | 0):
+    # measurement phase flags: one at a time, and only on the split builds
+    for algo in (0x100 | 0x200 | 1, 0x100 | 0x200 | 2, 0x100 | 0, 0x200 | 0):
         rc = lib.corr_build_ex(algo, 256, 4800, 256, 1, 256, 60, 80, 4, pyr, 256, 1 << 40, None)
         assert rc == -1 and "unknown algorithm" in lib.corr_last_error().decode(), hex(algo)
 
@@ -100,9 +108,13 @@ def test_build_ex_workspace_and_validation(lib):
 def test_build_algo_env(monkeypatch):
     from eraft_amd import _lib
     monkeypatch.delenv("ERAFT_AMD_BUILD", raising=False)
-    assert _lib.default_algo() == _lib.BUILD_F16X3
+    assert _lib.default_algo() == _lib.BUILD_BF16X6
+    assert _lib.backward_algo() == _lib.BUILD_F16X3
     monkeypatch.setenv("ERAFT_AMD_BUILD", "fp32")
     assert _lib.default_algo() == _lib.BUILD_FP32
+    assert _lib.backward_algo() == _lib.BUILD_FP32
+    monkeypatch.setenv("ERAFT_AMD_BUILD", "f16x3")
+    assert _lib.default_algo() == _lib.BUILD_F16X3
     monkeypatch.setenv("ERAFT_AMD_BUILD", "bf16")
     with pytest.raises(ValueError):
         _lib.default_algo()

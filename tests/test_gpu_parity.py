@@ -37,7 +37,7 @@ def _fmaps(meta, dev=DEV):
     return f1, f2, torch.from_numpy(f1).to(dev), torch.from_numpy(f2).to(dev)
 
 
-ALGOS = ["f16x3", "fp32"]
+ALGOS = ["bf16x6", "f16x3", "fp32"]
 
 
 @pytest.mark.parametrize("algo", ALGOS)
@@ -59,15 +59,20 @@ def test_build_matches_reference(name, algo, monkeypatch):
         assert bit_equal(oracle.avg_pool2x2(gpu[l - 1]), gpu[l]), l
 
 
+@pytest.mark.parametrize("algo", ["bf16x6", "f16x3"])
 @pytest.mark.parametrize("shape", [(1, 256, 60, 80), (8, 256, 36, 48), (3, 256, 36, 44), (2, 200, 17, 23),
-                                   (1, 64, 9, 130), (2, 96, 20, 46), (1, 128, 16, 32), (2, 40, 7, 5)])
-def test_split_build_shapes_deterministic(shape, monkeypatch):
-    """The f16x3 build at shapes that exercise its padding (query count not a multiple of 128,
-    H not a multiple of 8, W not a multiple of 16 / 4 / 2, K not a multiple of 32): level 0
-    within tolerance of the oracle on sampled queries, levels 1-3 bit-identical to avg_pool2d of
-    the kernel's own level 0 (16-B, 8-B and element stores), and two runs bit-identical."""
+                                   (1, 64, 9, 130), (2, 96, 20, 46), (1, 128, 16, 32), (2, 40, 7, 5),
+                                   (1, 300, 12, 16)])
+def test_split_build_shapes_deterministic(shape, algo, monkeypatch):
+    """The split builds at shapes that exercise their padding (query count not a multiple of 128,
+    H not a multiple of 8, W not a multiple of 16 / 4 / 2, K not a multiple of 32, D > 256: the
+    runtime K loop): level 0 within tolerance of the oracle on sampled queries, levels 1-3
+    bit-identical to avg_pool2d of the kernel's own level 0 (16-B, 8-B and element stores), and
+    two runs bit-identical."""
     B, D, H, W = shape
-    monkeypatch.setenv("ERAFT_AMD_BUILD", "f16x3")
+    if algo == "f16x3" and D > 256:
+        pytest.skip("f16x3 supports D <= 1024 through the same loop; covered at D <= 256")
+    monkeypatch.setenv("ERAFT_AMD_BUILD", algo)
     f1, f2 = prng.gauss(11, (B, D, H, W)), prng.gauss(12, (B, D, H, W))
     t1, t2 = torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV)
     L = min(4, int(np.log2(min(H, W))) + 1)
@@ -87,11 +92,13 @@ def test_split_build_shapes_deterministic(shape, monkeypatch):
         assert bit_equal(oracle.avg_pool2x2(pyrs[0][l - 1]), pyrs[0][l]), l
 
 
+@pytest.mark.parametrize("algo", ["bf16x6", "f16x3"])
 @pytest.mark.parametrize("shape", [(1, 256, 60, 80), (2, 200, 17, 23)])
-def test_split_build_phases_compose(shape):
+def test_split_build_phases_compose(shape, algo):
     """The measurement flags CORR_BUILD_ONLY_PACK then CORR_BUILD_ONLY_MFMA (bench.py times the
     two kernels separately with them) write the same pyramid, bit for bit, as one full build."""
     from eraft_amd import _lib
+    A = _lib._ALGOS[algo]
     B, D, H, W = shape
     t1 = torch.from_numpy(prng.gauss(21, (B, D, H, W))).to(DEV)
     t2 = torch.from_numpy(prng.gauss(22, (B, D, H, W))).to(DEV)
@@ -99,11 +106,11 @@ def test_split_build_phases_compose(shape):
     shapes = [(B * H * W, 1, H >> l, W >> l) for l in range(L)]
     full = [torch.empty(s, device=DEV) for s in shapes]
     split = [torch.full(s, float("nan"), device=DEV) for s in shapes]
-    ws = _lib.build_workspace(t1, t2, _lib.BUILD_F16X3)
-    _lib.build(t1, t2, full, _lib.BUILD_F16X3, ws)
+    ws = _lib.build_workspace(t1, t2, A)
+    _lib.build(t1, t2, full, A, ws)
     ws.zero_()
-    _lib.build(t1, t2, split, _lib.BUILD_F16X3 | _lib.BUILD_ONLY_PACK, ws)
-    _lib.build(t1, t2, split, _lib.BUILD_F16X3 | _lib.BUILD_ONLY_MFMA, ws)
+    _lib.build(t1, t2, split, A | _lib.BUILD_ONLY_PACK, ws)
+    _lib.build(t1, t2, split, A | _lib.BUILD_ONLY_MFMA, ws)
     torch.cuda.synchronize()
     for l in range(L):
         assert bit_equal(full[l].cpu().numpy(), split[l].cpu().numpy()), l
@@ -242,6 +249,159 @@ def test_build_f16x3_dynamic_range(case):
         ok = scale > 0
         assert (err[ok] / scale[ok]).max() < REL_TOL, (algo, (err[ok] / scale[ok]).max())
         assert (err[~ok] == 0).all()
+
+
+def _fp64_rows(f1, f2, rows):
+    """fp64 restatement of corr.py:58-60 for query pixels `rows` of batch item 0: [len, N]."""
+    B, D, H, W = f1.shape
+    a = f1[0].reshape(D, H * W).astype(np.float64)[:, rows]
+    b = f2[0].reshape(D, H * W).astype(np.float64)
+    return (a.T @ b) / np.sqrt(np.float64(D))
+
+
+def _dyn_range_inputs(case, B=1, D=96, H=12, W=16):
+    f1 = prng.gauss(11, (B, D, H, W)).astype(np.float64)
+    f2 = prng.gauss(12, (B, D, H, W)).astype(np.float64)
+    if case == "channel_scales":  # the small features of one map meet the large of the other
+        s = 10.0 ** np.linspace(-3, 3, D)[None, :, None, None]
+        f1, f2 = f1 * s, f2 * s[:, ::-1]
+    elif case == "pixel_scales":
+        s = 10.0 ** np.linspace(-10, 10, H * W).reshape(1, 1, H, W)
+        f1, f2 = f1 * s, f2 * s[..., ::-1, ::-1]
+    elif case == "zeros":
+        f1[:, :, ::3] = 0.0
+        f2[:, :, :, ::5] = 0.0
+    elif case == "tiny":
+        f1, f2 = f1 * 1e-15, f2 * 1e-16
+    elif case == "huge":
+        f1, f2 = f1 * 1e17, f2 * 1e17
+    elif case == "cancel":  # dot products that cancel to ~1e-4 of their terms
+        f2[:, 1::2] = -f2[:, 0::2] * (1 + 1e-4 * prng.gauss(13, f2[:, 1::2].shape))
+        f1[:, 1::2] = f1[:, 0::2]
+    return f1.astype(np.float32), f2.astype(np.float32)
+
+
+BF16_CASES = ["gauss", "channel_scales", "pixel_scales", "zeros", "tiny", "huge", "dsec"]
+
+
+@pytest.mark.parametrize("case", BF16_CASES + ["cancel"])
+def test_build_bf16x6_error_bound(case):
+    """Element-wise a-priori bound of the bf16x6 build: |C - C64| <= (3 + 6 S) u sum_k |a_k b_k| / sqrt(D)
+    (u = 2^-24, S = ceil(D / 32)): 2u for the dropped piece products, one rounding per MFMA into
+    the accumulator (6 S of them), one for the output.  An fp32 fmaf chain's bound is D u sum|ab|
+    (Higham's gamma_D) — 256 u at D = 256 against 51 u here — so the split is provably no
+    narrower.  Includes a cancelling case (results ~1e-4 of their terms), where only such a bound
+    is meaningful."""
+    from eraft_amd import _lib
+    if case == "dsec":
+        f1, f2 = prng.gauss(31, (1, 256, 60, 80)), prng.gauss(32, (1, 256, 60, 80))
+        rows = np.unique(np.linspace(0, 4799, 48).astype(int))
+    else:
+        f1, f2 = _dyn_range_inputs(case)
+        rows = np.arange(f1.shape[2] * f1.shape[3])
+    B, D, H, W = f1.shape
+    S = (D + 31) // 32
+    t1, t2 = torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV)
+    lvl = torch.empty(B * H * W, 1, H, W, device=DEV)
+    _lib.build(t1, t2, [lvl], _lib.BUILD_BF16X6)
+    o = lvl.cpu().numpy().reshape(B * H * W, H * W)[rows].astype(np.float64)
+    ref = _fp64_rows(f1, f2, rows)
+    a = np.abs(f1[0].reshape(D, H * W).astype(np.float64)[:, rows])
+    b = np.abs(f2[0].reshape(D, H * W).astype(np.float64))
+    mag = (a.T @ b) / np.sqrt(np.float64(D))
+    bound = (3 + 6 * S) * 2.0 ** -24 * mag
+    ratio = np.abs(o - ref) / np.maximum(bound, 1e-300)
+    print(f"{case}: max |err| / bound = {ratio.max():.3f}")
+    assert (np.abs(o - ref) <= bound).all()
+
+
+@pytest.mark.parametrize("case", BF16_CASES)
+def test_build_bf16x6_not_narrower_than_fp32(case):
+    """The bf16x6 build (three exact bf16 pieces per feature, six piece products) is no narrower
+    than the exact-fp32 MFMA build (the arithmetic of the reference's fp32 matmul, corr.py:58):
+    on every query row its max error against an fp64 restatement is at most the fp32 build's
+    plus one fp32 ulp of the row's largest value (both round their results to fp32), and over
+    all rows its worst and its mean row error are at most the fp32 build's."""
+    from eraft_amd import _lib
+    if case == "dsec":
+        f1, f2 = prng.gauss(31, (1, 256, 60, 80)), prng.gauss(32, (1, 256, 60, 80))
+        rows = np.unique(np.linspace(0, 4799, 96).astype(int))
+    else:
+        f1, f2 = _dyn_range_inputs(case)
+        rows = np.arange(f1.shape[2] * f1.shape[3])
+    B, D, H, W = f1.shape
+    t1, t2 = torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV)
+    ref = _fp64_rows(f1, f2, rows)
+    err = {}
+    for algo in (_lib.BUILD_BF16X6, _lib.BUILD_FP32):
+        lvl = torch.empty(B * H * W, 1, H, W, device=DEV)
+        _lib.build(t1, t2, [lvl], algo)
+        o = lvl.cpu().numpy().reshape(B * H * W, H * W)[rows].astype(np.float64)
+        assert np.isfinite(o).all()
+        err[algo] = np.abs(o - ref).max(axis=1)
+    scale = np.abs(ref).max(axis=1)
+    ulp = scale * 2.0 ** -23
+    bf, f32 = err[_lib.BUILD_BF16X6], err[_lib.BUILD_FP32]
+    ok = scale > 0
+    rel_bf, rel_f32 = bf[ok] / scale[ok], f32[ok] / scale[ok]
+    print(f"{case}: bf16x6 row error max {rel_bf.max():.3e} mean {rel_bf.mean():.3e}; "
+          f"fp32 max {rel_f32.max():.3e} mean {rel_f32.mean():.3e}")
+    assert (bf[~ok] == 0).all()
+    assert (bf <= f32 + ulp).all(), np.max((bf - f32) / np.maximum(scale, 1e-300))
+    assert rel_bf.max() <= rel_f32.max()
+    assert rel_bf.mean() <= rel_f32.mean()
+
+
+def _bf16_to_f32(u16):
+    return (u16.astype(np.uint32) << 16).view(np.float32)
+
+
+def test_bf16x6_pack_is_exact_split():
+    """The bf16x6 operand pack (CORR_BUILD_ONLY_PACK) writes every fp32 feature as three bf16
+    pieces whose sum is the feature EXACTLY (checked in fp64, bit for bit), hi = bf16_rn(x), and
+    the special values as documented: +-inf -> (inf, 0, 0), NaN -> NaN hi, |x| near FLT_MAX ->
+    a finite truncated hi, fp32 subnormals -> within the bf16 subnormal floor.  Padding is zero."""
+    from eraft_amd import _lib
+    B, D, H, W = 2, 40, 9, 21
+    f1 = prng.gauss(41, (B, D, H, W)) * np.float32(3.0)
+    f2 = prng.gauss(42, (B, D, H, W)) * np.float32(1e-20)
+    sp = np.array([np.inf, -np.inf, np.nan, 3.4028235e38, -3.3961e38, 3.3895e38, 1e-40, -3e-39, 1.2e-38,
+                   0.0, -0.0, 1.0 + 2.0 ** -23, 2.0 ** -100, 65504.0, 1e30], np.float32)
+    f1.reshape(-1)[7:7 + sp.size] = sp
+    f2.reshape(-1)[100:100 + sp.size] = sp
+    t1, t2 = torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV)
+    ws = _lib.build_workspace(t1, t2, _lib.BUILD_BF16X6)
+    ws.fill_(0xAB)
+    lvl = torch.empty(B * H * W, 1, H, W, device=DEV)
+    _lib.build(t1, t2, [lvl], _lib.BUILD_BF16X6 | _lib.BUILD_ONLY_PACK, ws)
+    w = ws.cpu().numpy()
+    N, S = H * W, (D + 31) // 32
+    NQp = (N + 127) // 128 * 128
+    Hp, CB = (H + 7) // 8 * 8, (W + 15) // 16
+    nq = B * S * NQp * 192
+    toff = (nq + 255) // 256 * 256
+    # record layout: [piece 3][grp 4][ci 16][j 8] bf16; k = 32 s + 8 grp + j
+    q = w[:nq].view(np.uint16).reshape(B, S, NQp // 16, 3, 4, 16, 8)
+    q = _bf16_to_f32(q).transpose(0, 3, 1, 4, 6, 2, 5).reshape(B, 3, S * 32, NQp)
+    t = w[toff:toff + B * S * Hp * CB * 16 * 192].view(np.uint16).reshape(B, S, Hp, CB, 3, 4, 16, 8)
+    t = _bf16_to_f32(t).transpose(0, 4, 1, 5, 7, 2, 3, 6).reshape(B, 3, S * 32, Hp, CB * 16)
+    for img, x in ((q[..., :N].reshape(B, 3, S * 32, H, W), f1), (t[..., :H, :W], f2)):
+        hi, mid, lo = (img[:, c, :D] for c in range(3))
+        fin = np.isfinite(x)
+        big = fin & (np.abs(x) >= 2.0 ** -100)
+        tot = hi.astype(np.float64) + mid + lo
+        assert np.array_equal(tot[big], x[big].astype(np.float64))
+        assert np.all(np.abs(tot[fin] - x[fin]) <= 2.0 ** -133)
+        rn = torch.from_numpy(x).to(torch.bfloat16).float().numpy()
+        okrn = big & np.isfinite(rn)
+        assert np.array_equal(hi[okrn].view(np.uint32), rn[okrn].view(np.uint32))
+        inf = np.isinf(x)
+        assert np.array_equal(hi[inf], x[inf]) and (mid[inf] == 0).all() and (lo[inf] == 0).all()
+        assert np.isnan(hi[np.isnan(x)]).all()
+        assert np.isfinite(hi[fin]).all()
+        # padding (k >= D, pixels past the map) is zero
+        assert (img[:, :, D:] == 0).all()
+    assert (q[..., N:] == 0).all() and (t[..., H:, :] == 0).all() and (t[..., W:] == 0).all()
 
 
 def test_lookup_nan_and_inf_coords():
@@ -687,7 +847,7 @@ def test_lookup_conv_autograd_matches_unfused():
 
 
 def test_lookup_conv_weight_pack_not_aliased():
-    """The packed convc1 split is cached on the weight tensor: a second weight that reuses the
+    """The packed convc1 split is cached per weight tensor: a second weight that reuses the
     first one's allocation (same data_ptr, same _version) must not see the first one's pack.
     (16 x 16: every level at least 2 x 2, so the reference composition is finite.)"""
     B, D, H, W, L, r = 1, 16, 16, 16, 4, 4
@@ -720,6 +880,19 @@ def test_lookup_conv_nan_level_propagates():
     ref = torch.relu(torch.nn.functional.conv2d(cb(c), w, bias)).cpu().numpy()
     out = cb.lookup_conv(c, w, bias).cpu().numpy()
     assert np.array_equal(np.isnan(out), np.isnan(ref)) and np.isnan(ref).any()
+    # backward: ReLU's threshold_backward passes the gradient where the output is NaN, so the
+    # fused path's bias gradient (sum of g) matches the unfused autograd's NaN pattern and values
+    g = torch.from_numpy(prng.gauss(120, (B, 256, H, W))).to(DEV)
+    grads = []
+    for fused in (True, False):
+        wv = w.clone().requires_grad_(True)
+        bv = bias.clone().requires_grad_(True)
+        o = cb.lookup_conv(c, wv, bv) if fused else torch.relu(torch.nn.functional.conv2d(cb(c), wv, bv))
+        (o * g).sum().backward()
+        grads.append(bv.grad.cpu().numpy())
+    assert np.array_equal(np.isnan(grads[0]), np.isnan(grads[1]))
+    fin = np.isfinite(grads[1])
+    assert np.abs(grads[0][fin] - grads[1][fin]).max(initial=0.0) <= 1e-5 * max(1.0, np.abs(grads[1][fin]).max(initial=0.0))
 
 
 @pytest.mark.parametrize("N,h,w", [(1, 60, 80), (2, 9, 70)])

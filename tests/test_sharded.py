@@ -181,6 +181,61 @@ def test_row_sharded_prefetch_pipeline():
             assert bit_equal(outs[k], ref)
 
 
+def _pipe_train_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from eraft_amd.sharded import Fmap2DoubleBuffer, RowShardedCorrBlock, row_partition
+
+        B, D, H, W, L, r = 1, 4, 8, 8, 2, 1
+        OracleRows.h0 = row_partition(H, world, rank)[0]
+        dbuf = Fmap2DoubleBuffer((B, D, H, W), "cpu")
+        f2 = torch.from_numpy(prng.gauss(5, (B, D, H, W))).requires_grad_(True)
+        errs = []
+        try:  # the source rank refuses an fmap2 that requires grad (after the broadcast completed)
+            dbuf.prefetch(f2 if rank == 0 else None).wait()
+            errs.append("prefetch accepted")
+        except RuntimeError:
+            errs.append("prefetch refused")
+        pending = dbuf.prefetch(f2.detach() if rank == 0 else None)
+        f1 = torch.from_numpy(prng.gauss(6, (B, D, H, W))).requires_grad_(True)
+        try:  # every rank refuses a prefetched fmap2 for a block that trains
+            RowShardedCorrBlock(f1, pending, L, r, backend=OracleRows)
+            errs.append("block accepted")
+        except RuntimeError:
+            errs.append("block refused")
+        with torch.no_grad():  # inference through the same pending buffer still works
+            blk = RowShardedCorrBlock(f1, pending, L, r, backend=OracleRows)
+            out = blk.gather(blk(torch.from_numpy(prng.lookup_coords(7, B, H, W, 1.0))))
+        q.put((rank, errs, out.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_row_sharded_prefetch_rejects_training():
+    """Fmap2DoubleBuffer / PendingFmap2 are inference-only: the source rank's prefetch refuses an
+    fmap2 that requires grad, every rank refuses to build a training block from a prefetched
+    fmap2 (no rank is left waiting in a gradient all-reduce), and no-grad use is unaffected."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_train_worker, args=(g, world, port, q)) for g in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] == ["prefetch refused", "block refused"]
+    assert res[1][1] == ["prefetch accepted", "block refused"]  # non-source ranks pass None
+    ref = oracle.lookup(oracle.build_pyramid(prng.gauss(6, (1, 4, 8, 8)), prng.gauss(5, (1, 4, 8, 8)), 2),
+                        prng.lookup_coords(7, 1, 8, 8, 1.0), 1)
+    for _, _, out in res:
+        assert bit_equal(out, ref)
+
+
 def _train_worker(rank, world, port, shape, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)

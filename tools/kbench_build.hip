@@ -17,6 +17,7 @@
 
 #include "../e-raft_amd/csrc/corr_build.hip"
 #include "../e-raft_amd/csrc/corr_build_split.hip"
+#include "../e-raft_amd/csrc/corr_build_bf16.hip"
 
 using namespace corr;
 
@@ -91,8 +92,10 @@ int main(int argc, char **argv) {
         }
         const size_t fe = (size_t)sh.B * sh.D * N;
         float *f1, *f2, *ref, *out;
-        void *ws;
+        void *ws, *wsbf;
         const size_t wsb = build_split_workspace(sh.B, sh.D, (int)N, sh.H, sh.W);
+        const size_t wsbfb = build_bf16_workspace(sh.B, sh.D, (int)N, sh.H, sh.W);
+        CK(hipMalloc(&wsbf, wsbfb));
         CK(hipMalloc(&f1, fe * 4));
         CK(hipMalloc(&f2, fe * 4));
         CK(hipMalloc(&ref, tot * 4));
@@ -115,16 +118,31 @@ int main(int argc, char **argv) {
                           return launch_build_cfg<BuildCfg<2, 2, 2, 8, 4, true, true>>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
                       }, true});
         vs.push_back({"f32 element level-1/2 stores", [&](float *o) {
-                          g_build_vec1 = false;
-                          const hipError_t e = launch_build_cfg<BuildDefault>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
-                          g_build_vec1 = true;
-                          return e;
+                          return launch_build_cfg<BuildDefault>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0, false);
                       }, true});
         vs.push_back({"f32 level 0 only", [&](float *o) {
                           return launch_build_cfg<BuildDefault>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 1, lp_of(o), 0);
                       }, false});
         vs.push_back({"f32 default NOSTORE", [&](float *o) {
                           return launch_build_cfg<BuildCfg<2, 2, 2, 8, 4, true, false, true>>(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), 0);
+                      }, false});
+        vs.push_back({"bf16x6 pack+mfma", [&](float *o) {
+                          return launch_build_bf16(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), wsbf, 0, 0);
+                      }, true});
+        vs.push_back({"bf16x6 pack only", [&](float *o) {
+                          return launch_build_bf16(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), wsbf, 0, 1);
+                      }, false});
+        vs.push_back({"bf16x6 mfma only", [&](float *o) {
+                          return launch_build_bf16(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), wsbf, 0, 2);
+                      }, false});
+        vs.push_back({"bf16x6 mfma tchain", [&](float *o) {
+                          return bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), wsbf, 0, 1);
+                      }, false});
+        vs.push_back({"bf16x6 mfma tchain NOSTORE", [&](float *o) {
+                          return bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), wsbf, 0, 1);
+                      }, false});
+        vs.push_back({"bf16x6 mfma NOSTORE", [&](float *o) {
+                          return launch_build_bf16(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), wsbf, 0, 2);
                       }, false});
         vs.push_back({"x3 pack+mfma", [&](float *o) {
                           return launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0);
@@ -135,20 +153,14 @@ int main(int argc, char **argv) {
         vs.push_back({"x3 pack only px64", [&](float *) {
                           return launch_split_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, ws, 0, 64);
                       }, false});
-        auto with_order = [&](int ord, std::function<hipError_t()> f) {
-            g_tile_order = ord;
-            const hipError_t e = f();
-            g_tile_order = 1;
-            return e;
-        };
         vs.push_back({"x3 mfma 1-tile order0", [&](float *o) {
-                          return with_order(0, [&] { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
+                          return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 0, 0);
                       }, false});
         vs.push_back({"x3 mfma 1-tile NOSTORE", [&](float *o) {
                           return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), ws, 0);
                       }, false});
         vs.push_back({"x3 mfma 1-tile order1", [&](float *o) {
-                          return with_order(1, [&] { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
+                          return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 0, 1);
                       }, false});
         vs.push_back({"x3 mfma 1-tile no half path", [&](float *o) {
                           return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 2);
@@ -194,9 +206,7 @@ int main(int argc, char **argv) {
                        bad ? "DIFFER" : "bit-identical", bad);
             };
             same("16-B level 1/2 stores", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
-            same("1-tile order0", [&](float *o) {
-                return with_order(0, [&] { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0); });
-            });
+            same("1-tile order0", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 0, 0); });
             same("1-tile no half path", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 2); });
             same("1-tile nopipe", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 1); });
 
@@ -216,8 +226,9 @@ int main(int argc, char **argv) {
             }
             CK(hipFree(ws2));
         }
-        {  // pooling of the new kernel: every level bit-identical to avg_pool2d of its own level 0
-            CK(launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), ws, 0));
+        for (int which = 0; which < 2; ++which) {  // pooling: every level bit-identical to avg_pool2d of its own level 0
+            if (which == 0) CK(launch_build_split(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), ws, 0));
+            else CK(launch_build_bf16(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), wsbf, 0, 0));
             std::vector<float> h(tot);
             CK(hipMemcpy(h.data(), out, tot * 4, hipMemcpyDeviceToHost));
             size_t bad = 0;
@@ -233,7 +244,7 @@ int main(int argc, char **argv) {
                             if (std::memcmp(&e, &g, 4)) ++bad;
                         }
             }
-            printf("%-10s pooling levels 1-3 vs own level 0: %s (%zu mismatches)\n", sh.name,
+            printf("%-10s %s pooling levels 1-3 vs own level 0: %s (%zu mismatches)\n", sh.name, which ? "bf16x6" : "x3",
                    bad ? "DIFFER" : "bit-identical", bad);
         }
         if (vfilter) {
@@ -256,9 +267,9 @@ int main(int argc, char **argv) {
         for (auto &v : vs) {
             std::sort(v.us.begin(), v.us.end());
             const float med = v.us[v.us.size() / 2];
-            printf("%-10s %-28s median %8.2f us  min %8.2f us  %7.1f TF/s fp32-equiv  %6.3f of 2.5 PF f16 pipe (x3)\n",
+            printf("%-10s %-28s median %8.2f us  min %8.2f us  %7.1f TF/s fp32-equiv  %6.3f of 2.5 PF (x3)  %6.3f (x6)\n",
                    sh.name, v.name.c_str(), med, v.us[0], flops / (med * 1e-6) / 1e12,
-                   3.0 * flops / (med * 1e-6) / 2.5e15);
+                   3.0 * flops / (med * 1e-6) / 2.5e15, 6.0 * flops / (med * 1e-6) / 2.5e15);
         }
         fflush(stdout);
         CK(hipFree(f1));
@@ -266,6 +277,7 @@ int main(int argc, char **argv) {
         CK(hipFree(ref));
         CK(hipFree(out));
         CK(hipFree(ws));
+        CK(hipFree(wsbf));
     }
     return 0;
 }

@@ -12,12 +12,8 @@
 #include <string>
 #include <vector>
 
-#define CORR_GEMM_AB
 #include "../e-raft_amd/csrc/corr_bwd_split.hip"
 
-namespace corr {
-extern int g_reduce_vec4;  // corr_bwd.hip
-}
 using namespace corr;
 
 #define CK(x)                                                                                 \
@@ -63,9 +59,9 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f1, (size_t)B * D * N, 1u);
     hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f2, (size_t)B * D * N, 2u);
     hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, dc, (size_t)B * NQ * N, 3u);
-    g_gemm_splits = 16;  // the largest slab the variants need
-    const size_t wsb = build_bwd_split_workspace(B, D, NQ, H, W);
-    g_gemm_splits = 0;
+    GemmTune big;
+    big.splits = 16;  // the largest slab the variants need
+    const size_t wsb = bwd_split_workspace_tuned(B, D, NQ, H, W, big);
     void *ws;
     CK(hipMalloc(&ws, wsb));
     const BwdWs w = carve(ws, B, D, NQ, N);
@@ -73,16 +69,16 @@ int main(int argc, char **argv) {
     CK(absmax(dc, B, NQ, N, w.mxB, w.mxC, 0));
     CK(rowmax2(f2, N, w.mxA, f1, NQ, w.mxA2, B, D, 0));
     const float sD = 16.0f;
-    auto g1 = [&](float *out) {
-        return gemm_f32<false>(f2, (long)D * N, N, dc, (long)NQ * N, N, 1, w.mxA, w.mxB, B, D, NQ, N, sD, out, w.slab, 0);
+    auto g1 = [&](float *out, const GemmTune &t) {
+        return gemm_f32<false>(f2, (long)D * N, N, dc, (long)NQ * N, N, 1, w.mxA, w.mxB, B, D, NQ, N, sD, out, w.slab, 0, t);
     };
-    auto g2 = [&](float *out) {
-        return gemm_f32<true>(f1, (long)D * NQ, NQ, dc, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, out, w.slab, 0);
+    auto g2 = [&](float *out, const GemmTune &t) {
+        return gemm_f32<true>(f1, (long)D * NQ, NQ, dc, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, out, w.slab, 0, t);
     };
-    g_gemm_dma = 0, g_gemm_mix = 0, g_reduce_vec4 = 0, g_gemm_wide = 0;  // reference: register-staged, convert-back, scalar reduce
-    CK(g1(r1));
-    CK(g2(r2));
-    g_gemm_dma = 1, g_gemm_mix = 1, g_reduce_vec4 = 1, g_gemm_wide = 1;
+    GemmTune ref;  // reference: register-staged, 128-row tiles, scalar reduce
+    ref.dma = false, ref.wide = false, ref.reduce_vec4 = false;
+    CK(g1(r1, ref));
+    CK(g2(r2, ref));
     struct V {
         std::string name;
         std::function<hipError_t()> run;
@@ -92,18 +88,10 @@ int main(int argc, char **argv) {
     std::vector<V> vs;
     for (int wide : {0, 1}) {
         const std::string tag = std::string("DMA mix splits plan, ") + (wide ? "256x256 tiles (8 waves)" : "128x256 tiles");
-        vs.push_back({"dF1 (rows) " + tag, [&, wide] {
-                          g_gemm_wide = wide;
-                          const hipError_t e = g1(o1);
-                          g_gemm_wide = 1;
-                          return e;
-                      }, o1, r1, {}});
-        vs.push_back({"dF2 (cols) " + tag, [&, wide] {
-                          g_gemm_wide = wide;
-                          const hipError_t e = g2(o2);
-                          g_gemm_wide = 1;
-                          return e;
-                      }, o2, r2, {}});
+        GemmTune t;
+        t.wide = wide;
+        vs.push_back({"dF1 (rows) " + tag, [&, t] { return g1(o1, t); }, o1, r1, {}});
+        vs.push_back({"dF2 (cols) " + tag, [&, t] { return g2(o2, t); }, o2, r2, {}});
     }
     if (argc > 2) {  // only the variant named exactly argv[2] (PMC passes)
         std::vector<V> keep;
