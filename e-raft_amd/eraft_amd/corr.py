@@ -64,21 +64,25 @@ def _validate_fmaps(fmap1, fmap2, num_levels):
         raise RuntimeError(f"{H}x{W} feature maps are too small for {num_levels} pyramid levels")
 
 
-_WEIGHT_PACKS = weakref.WeakKeyDictionary()
+_WEIGHT_PACKS = {}  # id(weight) -> (weakref to the weight, (data_ptr, _version), pack)
 
 
 def _weight_pack(weight):
-    """convc1.weight's packed split for lookup_conv, cached per weight tensor (a weak-keyed map,
-    so nothing is attached to the Parameter: pickling or torch.save of the model is unaffected,
-    and the pack dies with its tensor) together with the (data_ptr, _version) it was made from:
-    a new tensor (another model, a reloaded checkpoint) never sees another tensor's pack, and an
-    in-place update (optimizer step, load_state_dict's copy_) bumps _version and re-packs."""
+    """convc1.weight's packed split for lookup_conv, cached per weight tensor in a module-level
+    map keyed by the tensor's id and held by a weak reference (nothing is attached to the
+    Parameter, so pickling or torch.save of the model is unaffected, and the entry goes when the
+    tensor does), together with the (data_ptr, _version) it was made from: a new tensor
+    (another model, a reloaded checkpoint) never sees another tensor's pack, and an in-place
+    update (optimizer step, load_state_dict's copy_) bumps _version and re-packs.  (A
+    WeakKeyDictionary cannot hold tensors: its key comparison calls Tensor.__eq__.)"""
     key = (weight.data_ptr(), weight._version)
-    cached = _WEIGHT_PACKS.get(weight)
-    if cached is None or cached[0] != key:
-        cached = (key, _lib.lookup_conv_weights(weight))
-        _WEIGHT_PACKS[weight] = cached
-    return cached[1]
+    wid = id(weight)
+    ent = _WEIGHT_PACKS.get(wid)
+    if ent is None or ent[0]() is not weight or ent[1] != key:
+        ref = weakref.ref(weight, lambda _r, wid=wid: _WEIGHT_PACKS.pop(wid, None))
+        ent = (ref, key, _lib.lookup_conv_weights(weight))
+        _WEIGHT_PACKS[wid] = ent
+    return ent[2]
 
 
 class _State:
