@@ -162,7 +162,7 @@ struct Args {
     float *lvl[kFusedLevels];
     int B, H, W, N, NQ, S, nlev;
     int NQp, NQB, NQG, Hp, CB, npatch;
-    int exact;         // 1/sqrt(D) is a power of two (multiply); else divide by s
+    int exact;         // 1/sqrt(D) is a power of two (x * 1/s == x / s); else x * RN(1/s), within ~1 ulp
     int mode0, mode1;  // store width of levels 0 / 1: 2 = 16 B, 1 = 8 B, 0 = elements
     int cons;          // levels 1 and 2 as 16-B stores (W/2, W/4 multiples of 4, 16-B aligned bases)
     float inv_s, s;
@@ -180,7 +180,13 @@ struct Args {
 // compiler's own wait on them then also covers the next step's query loads, which have landed
 // by then).  ACC2 = false: the six products of a K step chained from zero into a transient and
 // added to one accumulator by VALU (four query slots) — the same rounding count, measured slower.
-template <int SS, int NR, bool ACC2>
+// VF (measurement variants, tools/kbench_build.hip; 0 in the library): bit 0 = query loads by
+// inline asm (the compiler then adds no wait of its own on them), bit 1 = s_setprio 1 over the
+// K loop (the epilogue of a neighbouring workgroup yields issue slots to MFMA-phase waves), bit 2 =
+// no half-patch body (padding rows computed and discarded: one kernel body).
+// FAST: every level stored as 16-B runs (levels == 4, W % 4 == 0 with 16-B aligned levels and
+// W/2, W/4 multiples of 4: mode0 == 2 and cons), no store-mode branches in the epilogue.
+template <int SS, int NR, bool ACC2, int VF = 0, bool FAST = false>
 __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
     constexpr int QS = ACC2 ? 3 : 4, QD = QS - 1;
     extern __shared__ __attribute__((aligned(16))) char smem_bf16[];
@@ -220,7 +226,12 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int c = 0; c < kPieces; ++c) qv[slot][i][c] = qsrc[s * qstep + i * kRecU + c * 64];
+            for (int c = 0; c < kPieces; ++c) {
+                if constexpr (VF & 1)
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qv[slot][i][c]) : "v"(qsrc + s * qstep + i * kRecU + c * 64) : "memory");
+                else
+                    qv[slot][i][c] = qsrc[s * qstep + i * kRecU + c * 64];
+            }
     };
     auto issue_t = [&](int s, int slot) __attribute__((always_inline)) {
         const uint32_t base = lds_base + slot * kSlotBytes;
@@ -324,6 +335,7 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
     };
 
     if constexpr (SS > 0) {
+        if constexpr ((VF & 2) != 0) __builtin_amdgcn_s_setprio(1);
         issue_q(0, 0);
         if (SS > 1) issue_q(1, 1);
         issue_t(0, 0);
@@ -347,6 +359,7 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
             if (s + 2 < SS) issue_t(s + 2, (s + 2) % kRing);
             if (qact) compute(s % kRing, qs);  // a wave whose queries all lie past NQ skips its MFMAs
         }
+        if constexpr ((VF & 2) != 0) __builtin_amdgcn_s_setprio(0);
     } else {
         // any S: no prefetch (one group in flight, drained every step)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -360,7 +373,7 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
     }
 
     // ---- epilogue: 1/sqrt(D), level 0 from registers, levels 1-3 in registers ----
-    const int H = p.H, W = p.W, N = p.N, NQ = p.NQ, nlev = p.nlev;
+    const int H = p.H, W = p.W, N = p.N, NQ = p.NQ, nlev = FAST ? 4 : p.nlev;
     const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
     const int N1 = H1 * W1, N2 = H2 * W2, N3 = H3 * W3;
     const int X0 = x0 + 4 * grp;
@@ -374,15 +387,19 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
 #pragma unroll
         for (int r = 0; r < kPatchRows; ++r)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float x = ACC2 ? acc[i][r][g] + acs[i][r][g] : acc[i][r][g];
-                v[r][g] = p.exact ? x * p.inv_s : x / p.s;
-            }
+            for (int g = 0; g < 4; ++g) v[r][g] = (ACC2 ? acc[i][r][g] + acs[i][r][g] : acc[i][r][g]) * p.inv_s;
         if (qok && nlev > 0) {
             float *row0 = p.lvl[0] + qrow * N;
+            if constexpr (FAST) {
+                float *rp = row0 + (size_t)y0 * W + X0;
 #pragma unroll
-            for (int r = 0; r < kPatchRows; ++r)
-                if (y0 + r < H) store4(row0 + (size_t)(y0 + r) * W, X0, W, v[r], p.mode0);
+                for (int r = 0; r < kPatchRows; ++r)
+                    if (y0 + r < H && X0 < W) *reinterpret_cast<float4 *>(rp + r * W) = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
+            } else {
+#pragma unroll
+                for (int r = 0; r < kPatchRows; ++r)
+                    if (y0 + r < H) store4(row0 + (size_t)(y0 + r) * W, X0, W, v[r], p.mode0);
+            }
         }
         float l1[4][2];
 #pragma unroll
@@ -394,7 +411,7 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
 #pragma unroll
         for (int r = 0; r < 2; ++r) l2[r] = pool4(l1[2 * r][0], l1[2 * r][1], l1[2 * r + 1][0], l1[2 * r + 1][1]);
         l2s[i][0] = l2[0], l2s[i][1] = l2[1];
-        if (p.cons) {
+        if (FAST || p.cons) {
             // Level 1 as 16-B stores: lanes grp 2m and 2m + 1 hold level-1 columns x0/2 + 4m + {0,1}
             // and {2,3} of the patch's 4 rows; they swap one row's pair (lanes 16 apart) so that the
             // even lane stores rows 0, 2 and the odd lane rows 1, 3, 4 columns each.
@@ -426,7 +443,7 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
     }
     // Levels 2 and 3 of BOTH query blocks in one store instruction each (an xor exchange has one
     // receiver per sender, so every sender sends what its receiver's block needs).
-    if (p.cons) {
+    if (FAST || p.cons) {
         // Level 2: lanes grp 0..3 hold columns x0/4 + grp of 2 rows per block; lane g gathers row
         // g & 1 of block g >> 1 (exchanges with lanes 16, 32, 48 apart), 16 B per lane.
         const int bl = grp >> 1, rw = grp & 1;
@@ -452,12 +469,14 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
     }
 }
 
-template <int SS, bool ACC2 = true>
+template <int SS, bool ACC2 = true, int VF = 0, bool FAST = false>
 __global__ __launch_bounds__(256, 2) void corr_build_bf16_kernel(Args p) {
     const Tile tl = patch_tile(xcd_swizzle(blockIdx.x, gridDim.x), p.npatch, p.NQG, p.CB, p.order);
     // two whole code paths (no value flows out of either): a half patch runs half the MFMAs
-    if (SS > 0 && tl.py * kPatchRows + kPatchRows / 2 >= p.H) build_tile<SS, kPatchRows / 2, ACC2>(p, tl);
-    else build_tile<SS, kPatchRows, ACC2>(p, tl);
+    if (!(VF & 4) && SS > 0 && tl.py * kPatchRows + kPatchRows / 2 >= p.H)
+        build_tile<SS, kPatchRows / 2, ACC2, VF, FAST>(p, tl);
+    else
+        build_tile<SS, kPatchRows, ACC2, VF, FAST>(p, tl);
 }
 
 struct Ws {
@@ -473,12 +492,18 @@ inline Ws workspace_of(void *ws, int B, const Geom &g) {
     return r;
 }
 
-template <int SS, bool ACC2 = true>
+template <int SS, bool ACC2 = true, int VF = 0>
 hipError_t launch_kernel(dim3 grid, const Args &p, hipStream_t s) {
-    static std::atomic<unsigned long long> lds_done{0};
-    const hipError_t e = ensure_lds_limit((const void *)corr_build_bf16_kernel<SS, ACC2>, kLds, lds_done);
+    const bool fast = p.nlev == 4 && p.mode0 == 2 && p.cons;
+    static std::atomic<unsigned long long> lds_done[2];
+    const void *fn = fast ? (const void *)corr_build_bf16_kernel<SS, ACC2, VF, true>
+                          : (const void *)corr_build_bf16_kernel<SS, ACC2, VF, false>;
+    const hipError_t e = ensure_lds_limit(fn, kLds, lds_done[fast]);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((corr_build_bf16_kernel<SS, ACC2>), grid, dim3(256), kLds, s, p);
+    if (fast)
+        hipLaunchKernelGGL((corr_build_bf16_kernel<SS, ACC2, VF, true>), grid, dim3(256), kLds, s, p);
+    else
+        hipLaunchKernelGGL((corr_build_bf16_kernel<SS, ACC2, VF, false>), grid, dim3(256), kLds, s, p);
     return hipGetLastError();
 }
 
@@ -505,8 +530,8 @@ hipError_t launch_pack(const float *f1, int NQ, const float *f2, int B, int D, i
 }
 
 // The MFMA part (operands already packed in ws).  levels == 0: the MFMAs and epilogue
-// arithmetic without stores (measurement).  variant 1: the single-accumulator form (ACC2 =
-// false; tools/kbench_build.hip A/B).
+// arithmetic without stores (measurement).  variant (tools/kbench_build.hip A/B, D = 256 only):
+// 1 = the single-accumulator form (ACC2 = false), 2..4 = VF 1..3, 5 = VF 4.
 hipError_t launch_mfma(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
                        hipStream_t s, int variant = 0) {
     const Geom g = geom(D, NQ, H, W);
@@ -529,9 +554,16 @@ hipError_t launch_mfma(int NQ, int B, int D, int H, int W, int levels, const Lev
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
     const dim3 grid((unsigned)tiles);
     hipError_t e;
-    if (variant == 1) {
+    if (variant != 0) {
         if (g.S != 8) return hipErrorInvalidValue;
-        e = launch_kernel<8, false>(grid, p, s);
+        switch (variant) {
+            case 1: e = launch_kernel<8, false>(grid, p, s); break;
+            case 2: e = launch_kernel<8, true, 1>(grid, p, s); break;
+            case 3: e = launch_kernel<8, true, 2>(grid, p, s); break;
+            case 4: e = launch_kernel<8, true, 3>(grid, p, s); break;
+            case 5: e = launch_kernel<8, true, 4>(grid, p, s); break;
+            default: return hipErrorInvalidValue;
+        }
     } else switch (g.S <= 8 ? g.S : 0) {
 #define CORR_BF16_CASE(c) \
     case c: e = launch_kernel<c>(grid, p, s); break;

@@ -141,6 +141,12 @@ int main(int argc, char **argv) {
         vs.push_back({"bf16x6 mfma tchain NOSTORE", [&](float *o) {
                           return bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), wsbf, 0, 1);
                       }, false});
+        for (int vv : {2, 3, 5}) {
+            const char *nm[] = {"", "", "bf16x6 mfma hiddenQ", "bf16x6 mfma prio", "bf16x6 mfma hiddenQ+prio", "bf16x6 mfma no half path"};
+            vs.push_back({nm[vv], [&, vv](float *o) {
+                              return bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), wsbf, 0, vv);
+                          }, false});
+        }
         vs.push_back({"bf16x6 mfma NOSTORE", [&](float *o) {
                           return launch_build_bf16(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), wsbf, 0, 2);
                       }, false});
@@ -209,6 +215,21 @@ int main(int argc, char **argv) {
             same("1-tile order0", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 0, 0); });
             same("1-tile no half path", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 2); });
             same("1-tile nopipe", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 1); });
+            if (sh.D == 256) {
+                for (int vv : {2, 3, 5}) {  // bf16x6 variants vs the default bf16x6 kernel
+                    CK(launch_build_bf16(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(ref), wsbf, 0, 0));
+                    CK(hipMemset(out, 0xff, tot * 4));
+                    CK(bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), wsbf, 0, vv));
+                    std::vector<unsigned> ha(tot), hb(tot);
+                    CK(hipMemcpy(ha.data(), out, tot * 4, hipMemcpyDeviceToHost));
+                    CK(hipMemcpy(hb.data(), ref, tot * 4, hipMemcpyDeviceToHost));
+                    size_t bad = 0;
+                    for (int l = 0; l < 4; ++l)
+                        for (size_t i = off[l]; i < off[l] + cnt[l]; ++i) bad += ha[i] != hb[i];
+                    printf("%-10s bf16x6 variant %d vs default, all levels: %s (%zu mismatches)\n", sh.name, vv,
+                           bad ? "DIFFER" : "bit-identical", bad);
+                }
+            }
 
         }
         {  // pack variants: byte-identical workspaces
