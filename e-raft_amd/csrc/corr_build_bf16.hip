@@ -166,8 +166,51 @@ struct Args {
     int mode0, mode1;  // store width of levels 0 / 1: 2 = 16 B, 1 = 8 B, 0 = elements
     int cons;          // levels 1 and 2 as 16-B stores (W/2, W/4 multiples of 4, 16-B aligned bases)
     float inv_s, s;
-    int order;  // tile order (patch_tile)
+    int order;  // tile order: 0, 1 = patch_tile's; 2 = XCD blocks (xcd_block_tile)
+    int nqh, npq;  // order 2: query-group and patch splits of a batch item into XCD blocks
 };
+
+// Tile order 2: tile index t (XCD x owns the contiguous range [x T / 8, (x + 1) T / 8) after
+// xcd_swizzle) enumerates, per batch item, qh x pq blocks (query-group range x patch range),
+// and inside a block the query group slowest and the patch fastest.  With qh x pq = 8 / B
+// blocks per batch item (B < 8), every XCD's L2 holds one block's target patches for its whole
+// life and streams each of its query groups once: each packed operand byte crosses the MALL ->
+// L2 boundary about once per XCD that needs it (DSEC: 2 x 4 blocks).  Measured no faster than
+// order 1 (DSEC 65.8 vs 64.9 us, train 70.2 vs 66.5, MVSEC 137.0 vs 138.7:
+// profiles/r04e_kbench_build_bf16x6_order.txt): the library uses order 1; kbench A/B only.
+__device__ __forceinline__ Tile xcd_block_tile(const Args &p, int t) {
+    Tile o;
+    const int per_b = p.npatch * p.NQG;
+    o.b = t / per_b;
+    int r = t - o.b * per_b;
+    // block (i, j): query groups [i NQG / qh, (i + 1) NQG / qh), patches [j np / pq, (j + 1) np / pq)
+    // — blocks laid out in order, each of size nq_i * np_j
+    int q0 = 0, q1 = 0, p0 = 0, p1 = 0;
+    for (int i = 0; i < p.nqh; ++i) {
+        const int qa = i * p.NQG / p.nqh, qb = (i + 1) * p.NQG / p.nqh;
+        const int rows = (qb - qa) * p.npatch;
+        if (r < rows) {
+            for (int j = 0; j < p.npq; ++j) {
+                const int pa = j * p.npatch / p.npq, pb = (j + 1) * p.npatch / p.npq;
+                const int sz = (qb - qa) * (pb - pa);
+                if (r < sz) {
+                    q0 = qa, q1 = qb, p0 = pa, p1 = pb;
+                    break;
+                }
+                r -= sz;
+            }
+            break;
+        }
+        r -= rows;
+    }
+    (void)q1;
+    const int np = p1 - p0;
+    o.qg = q0 + r / np;
+    const int patch = p0 + r % np;
+    o.py = patch / p.CB;
+    o.cb = patch - o.py * p.CB;
+    return o;
+}
 
 // SS > 0: S = SS K steps, fully unrolled (straight-line code: the compiler's own waits on the
 // query registers are exact and never drain the prefetch).  SS = 0: any S, runtime loop.
@@ -471,7 +514,8 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
 
 template <int SS, bool ACC2 = true, int VF = 0, bool FAST = false>
 __global__ __launch_bounds__(256, 2) void corr_build_bf16_kernel(Args p) {
-    const Tile tl = patch_tile(xcd_swizzle(blockIdx.x, gridDim.x), p.npatch, p.NQG, p.CB, p.order);
+    const int t = xcd_swizzle(blockIdx.x, gridDim.x);
+    const Tile tl = p.order == 2 ? xcd_block_tile(p, t) : patch_tile(t, p.npatch, p.NQG, p.CB, p.order);
     // two whole code paths (no value flows out of either): a half patch runs half the MFMAs
     if (!(VF & 4) && SS > 0 && tl.py * kPatchRows + kPatchRows / 2 >= p.H)
         build_tile<SS, kPatchRows / 2, ACC2, VF, FAST>(p, tl);
@@ -533,7 +577,7 @@ hipError_t launch_pack(const float *f1, int NQ, const float *f2, int B, int D, i
 // arithmetic without stores (measurement).  variant (tools/kbench_build.hip A/B, D = 256 only):
 // 1 = the single-accumulator form (ACC2 = false), 2..4 = VF 1..3, 5 = VF 4.
 hipError_t launch_mfma(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
-                       hipStream_t s, int variant = 0) {
+                       hipStream_t s, int variant = 0, int order = 1) {
     const Geom g = geom(D, NQ, H, W);
     const Ws w = workspace_of(ws, B, g);
     Args p{};
@@ -549,7 +593,12 @@ hipError_t launch_mfma(int NQ, int B, int D, int H, int W, int levels, const Lev
     p.mode0 = p.nlev > 0 ? level_store_mode(W, pyr.p[0]) : 0;
     p.mode1 = p.nlev > 1 ? level_store_mode(W >> 1, pyr.p[1]) : 0;
     p.cons = p.mode1 == 2 && (p.nlev <= 2 || level_store_mode(W >> 2, pyr.p[2]) == 2);
-    p.order = 1;
+    // XCD blocks: split each batch item into 8 / B blocks (2 x 4 for one item), so the 8 XCDs
+    // get disjoint operand sets; B >= 8: one or more whole batch items per XCD
+    p.order = order;
+    const int per = B >= 8 ? 1 : 8 / B;
+    p.nqh = per >= 2 && g.NQG >= 2 ? 2 : 1;
+    p.npq = std::max(1, std::min(per / p.nqh, p.npatch));
     const long tiles = (long)B * p.npatch * g.NQG;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
     const dim3 grid((unsigned)tiles);

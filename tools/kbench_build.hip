@@ -147,6 +147,9 @@ int main(int argc, char **argv) {
                               return bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), wsbf, 0, vv);
                           }, false});
         }
+        vs.push_back({"bf16x6 mfma order2 (XCD blocks)", [&](float *o) {
+                          return bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), wsbf, 0, 0, 2);
+                      }, false});
         vs.push_back({"bf16x6 mfma NOSTORE", [&](float *o) {
                           return launch_build_bf16(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), wsbf, 0, 2);
                       }, false});
@@ -216,10 +219,11 @@ int main(int argc, char **argv) {
             same("1-tile no half path", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 2); });
             same("1-tile nopipe", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 1); });
             if (sh.D == 256) {
-                for (int vv : {2, 3, 5}) {  // bf16x6 variants vs the default bf16x6 kernel
+                for (int vv : {2, 3, 5, 9}) {  // bf16x6 variants vs the default bf16x6 kernel (9: tile order 2)
                     CK(launch_build_bf16(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(ref), wsbf, 0, 0));
                     CK(hipMemset(out, 0xff, tot * 4));
-                    CK(bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), wsbf, 0, vv));
+                    CK(vv == 9 ? bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), wsbf, 0, 0, 2)
+                               : bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), wsbf, 0, vv));
                     std::vector<unsigned> ha(tot), hb(tot);
                     CK(hipMemcpy(ha.data(), out, tot * 4, hipMemcpyDeviceToHost));
                     CK(hipMemcpy(hb.data(), ref, tot * 4, hipMemcpyDeviceToHost));
