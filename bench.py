@@ -94,7 +94,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true",
                     help="row-shard ONE frame pair's query rows over the ranks (SURVEY §8e): RCCL "
-                         "broadcast of fmap2 + slab build + slab lookups; strong scaling")
+                         "broadcast of fmap2 in target-row chunks, each chunk's build starting on its "
+                         "arrival + slab lookups; strong scaling")
+    ap.add_argument("--chunks", type=int, default=4, help="--sharded: fmap2 broadcast chunks")
+    ap.add_argument("--prefetch", action="store_true",
+                    help="--sharded: instead of chunks, double-buffer whole fmap2s across pairs "
+                         "(pair k+1's broadcast during pair k; eager)")
     return ap.parse_args()
 
 
@@ -480,23 +485,30 @@ def main():
         # pair k's RowShardedCorrBlock is built from the buffer whose broadcast was issued one
         # pair earlier, so the broadcast overlaps the build and the 12 lookups.
         pipe = {"pending": None}
+        prefetch = sharded and world > 1 and args.prefetch
         if sharded and world > 1:
             from eraft_amd.sharded import Fmap2DoubleBuffer, RowShardedCorrBlock
+        if prefetch:
             dbuf = Fmap2DoubleBuffer(tuple(f2.shape), dev)
             pipe["pending"] = dbuf.prefetch(f2 if rank == 0 else None)  # prologue: pair 0's fmap2
 
         def pair():
-            if sharded and world > 1:
+            if prefetch:
                 cur = pipe["pending"]
                 pipe["pending"] = dbuf.prefetch(f2 if rank == 0 else None)
                 blk = RowShardedCorrBlock(f1, cur, num_levels=L, radius=r, fmap1_is_slab=True)
+                for c in coords:
+                    blk(c)
+            elif sharded and world > 1:
+                # chunked broadcast: chunk k+1 arrives while chunk k's pyramid rows are built
+                blk = RowShardedCorrBlock(f1, f2, num_levels=L, radius=r, fmap1_is_slab=True, chunks=args.chunks)
                 for c in coords:
                     blk(c)
             else:
                 build_only()
                 run_lookups()
 
-        launch = "eager" if args.eager or (sharded and world > 1) else "hipgraph"
+        launch = "eager" if args.eager or prefetch else "hipgraph"
         step = pair
         if train:
             step = autograd_step
@@ -514,10 +526,19 @@ def main():
                 launch = "eager"
                 step = autograd_step
         elif launch == "hipgraph":
-            g_pair = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_pair, stream=stream):
+            try:  # the sharded pair captures its RCCL chunk broadcasts too
                 pair()
-            step = g_pair.replay
+                torch.cuda.synchronize()
+                g_pair = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g_pair, stream=stream):
+                    pair()
+                step = g_pair.replay
+            except Exception as exc:  # noqa: BLE001 — report and stay eager
+                if not sharded:
+                    raise
+                print(f"sharded: graph capture failed ({exc}); eager", file=sys.stderr)
+                launch = "eager"
+                step = pair
 
         for _ in range(args.warmup):
             step()
@@ -681,9 +702,12 @@ def main():
         if bcast_ms is not None:
             res["sharded_timing"] = {
                 "per_rank": per_rank,
-                "overlap": "eraft_amd.sharded.Fmap2DoubleBuffer: pair k+1's broadcast (async, on the "
-                           "collective stream) runs during pair k's RowShardedCorrBlock build + lookups; "
-                           "per-rank broadcast_ms is the broadcast timed alone",
+                "overlap": ("eraft_amd.sharded.Fmap2DoubleBuffer: pair k+1's broadcast (async, on the "
+                            "collective stream) runs during pair k's RowShardedCorrBlock build + lookups"
+                            if prefetch else
+                            f"fmap2 broadcast in {args.chunks} target-row chunks (all issued async); each "
+                            "chunk's pyramid rows are built (corr_build_region) as soon as it has arrived") +
+                           "; per-rank broadcast_ms is the whole broadcast timed alone",
                 "backend": os.environ.get("ERAFT_AMD_DIST_BACKEND", "nccl")}
         if world == 1 and not args.no_cpu_baseline and wl_name not in CPU_SKIP:
             cb = cpu_baseline(wl, args.cpu_seconds, train)

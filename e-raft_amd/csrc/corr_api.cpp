@@ -135,6 +135,32 @@ int corr_build_ex(int algo, const float *fmap1_rows, int NQ, const float *fmap2,
                       fn);
 }
 
+int corr_build_region(int algo, const float *fmap1_rows, int NQ, const float *fmap2_rows, int y0, int y1, int B,
+                      int D, int H, int W, int levels, float *const *pyr, void *workspace, size_t workspace_bytes,
+                      int flags, void *stream) {
+    static const char *fn = "corr_build_region";
+    g_err[0] = 0;
+    if (algo != CORR_BUILD_BF16X6)
+        return fail(CORR_EUNSUPPORTED, "%s: only CORR_BUILD_BF16X6 builds by target region (got %d)", fn, algo);
+    int rc = check_dims(fn, B, NQ, H, W, levels);
+    if (rc) return rc;
+    if (D < 1) return fail(CORR_EINVAL, "%s: D must be >= 1 (got %d)", fn, D);
+    if (levels > 4) return fail(CORR_EUNSUPPORTED, "%s: levels <= 4 (got %d)", fn, levels);
+    if (y0 < 0 || y0 >= y1 || y1 > H || y0 % 8 || (y1 % 8 && y1 != H))
+        return fail(CORR_EINVAL, "%s: need 0 <= y0 < y1 <= H, y0 %% 8 == 0, y1 %% 8 == 0 or y1 == H (got %d, %d, H %d)",
+                    fn, y0, y1, H);
+    if ((rc = check_ptr(fn, fmap1_rows, "fmap1")) || (rc = check_ptr(fn, fmap2_rows, "fmap2_rows"))) return rc;
+    if ((uintptr_t)workspace % 256) return fail(CORR_EINVAL, "%s: workspace is not 256-byte aligned", fn);
+    const size_t need = build_bf16_workspace(B, D, NQ, H, W);
+    if (workspace_bytes < need || !workspace)
+        return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
+    LevelPtrs lp{};
+    if ((rc = check_levels(fn, pyr, levels, "pyr", lp.p))) return rc;
+    return hip_status(launch_build_bf16_region(fmap1_rows, NQ, fmap2_rows, y0, y1, B, D, H, W, levels, lp, workspace,
+                                               (flags & CORR_REGION_PACK_QUERIES) != 0, (hipStream_t)stream),
+                      fn);
+}
+
 int corr_build(const float *fmap1, const float *fmap2, int B, int D, int H, int W, int levels,
                float *const *pyr, void *stream) {
     return corr_build_rows(fmap1, H * W, fmap2, B, D, H, W, levels, pyr, stream);

@@ -114,30 +114,36 @@ __device__ __forceinline__ void split3(float a, float b, unsigned &hi, unsigned 
 // lane = 16 grp + ci holds the 8 k of its fragment position, splits them and writes 16 B of
 // each piece (each store instruction writes one contiguous 1 KiB piece).
 // ---------------------------------------------------------------------------------------
+// Target region (corr_build_region): the target image's patch-padded rows [y0, y0 + nyp) are
+// packed from a slab holding rows [y0, y1) of fmap2 ([B][D][y1 - y0][W]); the full build is the
+// region [0, H).  z = 0 packs the queries (skipped when z0 = 1), z = 1 the targets.
 struct PackArgs {
     const float *f[2];
     u32x4_t *pk[2];
-    int np[2];    // source pixels per batch item: NQ, H*W
-    int nblk[2];  // blocks per batch item in the image: NQB, Hp*CB
-    int D, S, H, W, CB;
+    int np[2];    // source pixels per batch item: NQ, (y1 - y0) * W
+    int nblk[2];  // blocks per batch item to pack: NQB, nyp * CB
+    int img[2];   // blocks per batch item in the packed image: NQB, Hp * CB
+    int D, S, W, CB, y0, y1, z0;
 };
 
 __global__ __launch_bounds__(256) void bf16_pack_kernel(PackArgs a) {
-    const int z = blockIdx.z, b = blockIdx.y;
+    const int z = blockIdx.z + a.z0, b = blockIdx.y;
     const int nblk = a.nblk[z];
     const int rec = blockIdx.x * 4 + (threadIdx.x >> 6);  // record = s * nblk + blk
     if (rec >= a.S * nblk) return;
     const int s = rec / nblk, blk = rec - s * nblk;
     const int lane = threadIdx.x & 63, ci = lane & 15, grp = lane >> 4;
-    int n;
+    int n, iblk;  // source pixel in the slab, block in the packed image
     bool valid;
     if (z == 0) {
         n = blk * 16 + ci;
         valid = n < a.np[0];
+        iblk = blk;
     } else {
-        const int y = blk / a.CB, x = (blk - y * a.CB) * 16 + ci;
-        valid = y < a.H && x < a.W;
-        n = y * a.W + x;
+        const int ly = blk / a.CB, x = (blk - ly * a.CB) * 16 + ci;
+        valid = a.y0 + ly < a.y1 && x < a.W;
+        n = ly * a.W + x;
+        iblk = a.y0 * a.CB + blk;
     }
     const int NP = a.np[z], k0 = s * kStepK + 8 * grp;
     const float *src = a.f[z] + (size_t)b * a.D * NP + (valid ? n : 0);
@@ -148,7 +154,7 @@ __global__ __launch_bounds__(256) void bf16_pack_kernel(PackArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) split3(v[2 * j], v[2 * j + 1], hh[j], mm[j], ll[j]);
     const u32x4_t h{hh[0], hh[1], hh[2], hh[3]}, m{mm[0], mm[1], mm[2], mm[3]}, l{ll[0], ll[1], ll[2], ll[3]};
-    u32x4_t *out = a.pk[z] + (((size_t)b * a.S + s) * nblk + blk) * kRecU + lane;
+    u32x4_t *out = a.pk[z] + (((size_t)b * a.S + s) * a.img[z] + iblk) * kRecU + lane;
     out[0] = h;
     out[64] = m;
     out[128] = l;
@@ -161,7 +167,8 @@ struct Args {
     const u32x4_t *pq, *pt;
     float *lvl[kFusedLevels];
     int B, H, W, N, NQ, S, nlev;
-    int NQp, NQB, NQG, Hp, CB, npatch;
+    int NQp, NQB, NQG, Hp, CB, npatch;  // npatch: patches of the target region
+    int py0;                            // first patch row of the target region
     int exact;         // 1/sqrt(D) is a power of two (x * 1/s == x / s); else x * RN(1/s), within ~1 ulp
     int mode0, mode1;  // store width of levels 0 / 1: 2 = 16 B, 1 = 8 B, 0 = elements
     int cons;          // levels 1 and 2 as 16-B stores (W/2, W/4 multiples of 4, 16-B aligned bases)
@@ -515,7 +522,8 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
 template <int SS, bool ACC2 = true, int VF = 0, bool FAST = false>
 __global__ __launch_bounds__(256, 2) void corr_build_bf16_kernel(Args p) {
     const int t = xcd_swizzle(blockIdx.x, gridDim.x);
-    const Tile tl = p.order == 2 ? xcd_block_tile(p, t) : patch_tile(t, p.npatch, p.NQG, p.CB, p.order);
+    Tile tl = p.order == 2 ? xcd_block_tile(p, t) : patch_tile(t, p.npatch, p.NQG, p.CB, p.order);
+    tl.py += p.py0;
     // two whole code paths (no value flows out of either): a half patch runs half the MFMAs
     if (!(VF & 4) && SS > 0 && tl.py * kPatchRows + kPatchRows / 2 >= p.H)
         build_tile<SS, kPatchRows / 2, ACC2, VF, FAST>(p, tl);
@@ -558,26 +566,35 @@ size_t workspace_bytes(int B, int D, int NQ, int H, int W) {
     return align256((size_t)B * g.S * g.NQp * kPixBytes) + align256((size_t)B * g.S * g.Hp * g.Wp * kPixBytes);
 }
 
+// Packs the queries (pack_q) and the target rows [y0, y1) (f2 = that slab, [B][D][y1 - y0][W];
+// y0 a multiple of 8, y1 a multiple of 8 or H): the patch rows [y0 / 8, ceil(y1 / 8)).
 hipError_t launch_pack(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, void *ws,
-                            hipStream_t s) {
+                       hipStream_t s, int y0 = 0, int y1 = -1, bool pack_q = true) {
+    if (y1 < 0) y1 = H;
     const Geom g = geom(D, NQ, H, W);
     const Ws w = workspace_of(ws, B, g);
     PackArgs a{};
     a.f[0] = f1, a.f[1] = f2;
     a.pk[0] = w.pq, a.pk[1] = w.pt;
-    a.np[0] = NQ, a.np[1] = H * W;
-    a.nblk[0] = g.NQB, a.nblk[1] = g.Hp * g.CB;
-    a.D = D, a.S = g.S, a.H = H, a.W = W, a.CB = g.CB;
-    const int recs = g.S * std::max(a.nblk[0], a.nblk[1]);
-    hipLaunchKernelGGL(bf16_pack_kernel, dim3((unsigned)((recs + 3) / 4), B, 2), dim3(256), 0, s, a);
+    a.np[0] = NQ, a.np[1] = (y1 - y0) * W;
+    const int nyp = (y1 + kPatchRows - 1) / kPatchRows * kPatchRows - y0;
+    a.nblk[0] = g.NQB, a.nblk[1] = nyp * g.CB;
+    a.img[0] = g.NQB, a.img[1] = g.Hp * g.CB;
+    a.D = D, a.S = g.S, a.W = W, a.CB = g.CB, a.y0 = y0, a.y1 = y1;
+    a.z0 = pack_q ? 0 : 1;
+    const int recs = g.S * std::max(pack_q ? a.nblk[0] : 0, a.nblk[1]);
+    hipLaunchKernelGGL(bf16_pack_kernel, dim3((unsigned)((recs + 3) / 4), B, pack_q ? 2 : 1), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 // The MFMA part (operands already packed in ws).  levels == 0: the MFMAs and epilogue
 // arithmetic without stores (measurement).  variant (tools/kbench_build.hip A/B, D = 256 only):
 // 1 = the single-accumulator form (ACC2 = false), 2..4 = VF 1..3, 5 = VF 4.
+// y0, y1: the target region (as launch_pack), whose pyramid rows [y0 >> l, ceil(y1 / 2^l)) of
+// every level it writes.
 hipError_t launch_mfma(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
-                       hipStream_t s, int variant = 0, int order = 1) {
+                       hipStream_t s, int variant = 0, int order = 1, int y0 = 0, int y1 = -1) {
+    if (y1 < 0) y1 = H;
     const Geom g = geom(D, NQ, H, W);
     const Ws w = workspace_of(ws, B, g);
     Args p{};
@@ -586,7 +603,8 @@ hipError_t launch_mfma(int NQ, int B, int D, int H, int W, int levels, const Lev
     p.nlev = std::min(levels, kFusedLevels);
     for (int l = 0; l < kFusedLevels; ++l) p.lvl[l] = l < p.nlev ? pyr.p[l] : nullptr;
     p.NQp = g.NQp, p.NQB = g.NQB, p.NQG = g.NQG, p.Hp = g.Hp, p.CB = g.CB;
-    p.npatch = (g.Hp / kPatchRows) * g.CB;
+    p.py0 = y0 / kPatchRows;
+    p.npatch = ((y1 + kPatchRows - 1) / kPatchRows - p.py0) * g.CB;
     p.s = std::sqrt((float)D);
     p.inv_s = 1.0f / p.s;
     p.exact = is_pow2(p.s);
@@ -641,6 +659,15 @@ hipError_t launch_build_bf16(const float *f1, int NQ, const float *f2, int B, in
         if (e != hipSuccess || part == 1) return e;
     }
     return bf16b::launch_mfma(NQ, B, D, H, W, levels, pyr, ws, s);
+}
+
+// One target region [y0, y1) of the build (corr_build_region): f2_rows holds those fmap2 rows.
+hipError_t launch_build_bf16_region(const float *f1, int NQ, const float *f2_rows, int y0, int y1, int B, int D,
+                                    int H, int W, int levels, const LevelPtrs &pyr, void *ws, bool pack_q,
+                                    hipStream_t s) {
+    const hipError_t e = bf16b::launch_pack(f1, NQ, f2_rows, B, D, H, W, ws, s, y0, y1, pack_q);
+    if (e != hipSuccess) return e;
+    return bf16b::launch_mfma(NQ, B, D, H, W, levels, pyr, ws, s, 0, 1, y0, y1);
 }
 
 }  // namespace corr

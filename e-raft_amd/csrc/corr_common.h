@@ -66,6 +66,9 @@ hipError_t launch_build_split(const float *f1, int NQ, const float *f2, int B, i
 size_t build_bf16_workspace(int B, int D, int NQ, int H, int W);
 hipError_t launch_build_bf16(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, int levels,
                              const LevelPtrs &pyr, void *ws, hipStream_t s, int part = 0);
+hipError_t launch_build_bf16_region(const float *f1, int NQ, const float *f2_rows, int y0, int y1, int B, int D,
+                                    int H, int W, int levels, const LevelPtrs &pyr, void *ws, bool pack_q,
+                                    hipStream_t s);
 // Ordered split-K sum + 1/sqrt(D) of [splits][per] partial slabs into C (corr_bwd.hip).
 hipError_t launch_splitk_reduce(const float *ws, float *C, int splits, size_t per, float sD, hipStream_t s,
                                 bool vec4 = true);

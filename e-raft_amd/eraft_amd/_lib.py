@@ -29,7 +29,7 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
            "corr_forward_splat", "corr_convex_upsample", "corr_voxel_grid_workspace",
            "corr_voxel_grid", "corr_lookup_conv", "corr_lookup_conv_weights", "corr_lookup_conv_weights_bytes", "corr_voxel_grid_tbilinear_workspace",
            "corr_voxel_grid_tbilinear", "corr_lookup_bwd_multi", "corr_pool_fold", "corr_backward_workspace",
-           "corr_backward", "corr_convex_upsample_bwd_workspace", "corr_convex_upsample_bwd")
+           "corr_backward", "corr_convex_upsample_bwd_workspace", "corr_convex_upsample_bwd", "corr_build_region")
 
 # Build algorithms (include/corr_mi355x.h).  BF16X6 is the default: every fp32 feature split
 # exactly into three bf16 pieces, the six largest piece products on the bf16 MFMA, fp32
@@ -123,7 +123,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.corr_backward_workspace.argtypes = [i, i, i, i, i, i, i]
     lib.corr_backward_workspace.restype = sz
     lib.corr_backward.argtypes = [i, vp, vp, i, vp, i, vp, i, i, i, i, i, i, vp, vp, vp, vp, sz, vp]
-    for f in ("corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd",
+    lib.corr_build_region.argtypes = [i, vp, i, vp, i, i, i, i, i, i, i, vp, vp, sz, i, vp]
+    for f in ("corr_build_region", "corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd",
               "corr_build_rows", "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows",
               "corr_build_ex", "corr_build_bwd_ex", "corr_forward_splat",
               "corr_convex_upsample", "corr_voxel_grid", "corr_lookup_conv", "corr_lookup_conv_weights",
@@ -172,9 +173,10 @@ def _nq(t):
 
 
 def build_workspace(fmap1, fmap2, algo=None):
-    """A device workspace for corr_build_ex (None when the algorithm needs none)."""
+    """A device workspace for corr_build_ex (None when the algorithm needs none).  fmap2: the
+    target map or just its shape [B, D, H, W]."""
     algo = default_algo() if algo is None else algo
-    B, D, H, W = fmap2.shape
+    B, D, H, W = fmap2 if isinstance(fmap2, (tuple, list, torch.Size)) else fmap2.shape
     n = load().corr_build_workspace(algo, B, D, _nq(fmap1), H, W)
     if n == ctypes.c_size_t(-1).value:
         raise CorrError(CORR_EUNSUPPORTED, f"build algorithm {algo} does not support D = {D}")
@@ -197,6 +199,22 @@ def build(fmap1, fmap2, levels, algo=None, workspace=None):
     with torch.cuda.device(fmap1.device):
         _check(load().corr_build_ex(algo, a, _nq(fmap1), b, B, D, H, W, len(levels), pp, wp, wn,
                                     _stream(fmap1)))
+
+
+REGION_PACK_QUERIES = 1
+
+
+def build_region(fmap1, fmap2_rows, y0, y1, H, levels, workspace, pack_queries, algo=BUILD_BF16X6):
+    """corr_build_region: the pyramid entries of target rows [y0, y1) (levels [B*NQ, 1, H>>l, W>>l])
+    from fmap2_rows [B, D, y1 - y0, W]; workspace from build_workspace(fmap1, <full fmap2 shape>)."""
+    B, D, rows, W = fmap2_rows.shape
+    if rows != y1 - y0:
+        raise ValueError(f"fmap2_rows has {rows} rows for the region [{y0}, {y1})")
+    a, b, pp = _dev(fmap1, "fmap1"), _dev(fmap2_rows, "fmap2_rows"), _ptrs(levels, "pyr")
+    with torch.cuda.device(fmap1.device):
+        _check(load().corr_build_region(algo, a, _nq(fmap1), b, y0, y1, B, D, H, W, len(levels), pp,
+                                        workspace.data_ptr(), workspace.numel() * workspace.element_size(),
+                                        REGION_PACK_QUERIES if pack_queries else 0, _stream(fmap1)))
 
 
 def lookup(levels, coords, radius, out, H=None, W=None):

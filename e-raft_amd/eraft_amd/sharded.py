@@ -7,7 +7,10 @@ is O(N^2) (1920x1280: 5.9 GB per pair), so the build partitions the QUERY pixels
   * every query owns its volume row C[n, :] and its pyramid slice, so a row partition needs
     no halo and no exchange in build, pyramid, lookup or lookup-backward;
   * rank g owns query rows [h0, h1) of every batch item (row_partition) and needs its fmap1
-    rows plus the FULL fmap2 -> one RCCL broadcast of fmap2 per frame pair (over xGMI);
+    rows plus the FULL fmap2 -> one RCCL broadcast of fmap2 per frame pair (over xGMI), sent as
+    target-row chunks (chunk_bounds: multiples of the build's 8-row patches) whose broadcasts
+    are all issued at once; each rank builds a chunk's pyramid entries (corr_build_region) as
+    soon as that chunk has arrived, so the transfer of chunk k+1 overlaps the build of chunk k;
   * lookups produce the rank's output rows; an optional all-gather assembles the full
     [B, L*K, H, W] tensor when a replicated consumer needs it;
   * backward (training): every lookup's backward is stashed and the build's backward runs
@@ -50,6 +53,22 @@ class HipRows:
         _lib.build(f1_rows, f2, levels)
         return levels
 
+    # target-row regions of one build (the chunked broadcast): allocate, then build region by region
+    @staticmethod
+    def region_supported(num_levels):
+        return _lib.default_algo() == _lib.BUILD_BF16X6 and num_levels <= 4
+
+    @staticmethod
+    def region_begin(f1_rows, f2_shape, num_levels):
+        B, _, rows, W = f1_rows.shape
+        H = f2_shape[2]
+        levels = _alloc_pyramid_rows(B, rows * W, H, W, num_levels, f1_rows)
+        return levels, _lib.build_workspace(f1_rows, tuple(f2_shape), _lib.BUILD_BF16X6)
+
+    @staticmethod
+    def build_region(f1_rows, f2_chunk, y0, y1, H, levels, ws, first):
+        _lib.build_region(f1_rows, f2_chunk, y0, y1, H, levels, ws, first)
+
     @staticmethod
     def lookup(levels, coords_rows, radius, H, W):
         B, _, rows, Wc = coords_rows.shape
@@ -87,6 +106,36 @@ class HipRows:
         return _lib.backward(coords_list, grad_list, radius, gl, f1_rows, f2)
 
 
+def chunk_bounds(H: int, chunks: int):
+    """Target-row chunks [y0, y1) of the chunked fmap2 broadcast: about H / chunks rows each,
+    rounded up to a multiple of 8 (the build's patch rows, so each chunk's pyramid rows are
+    complete at every level <= 4)."""
+    step = max(8, -(-(-(-H // max(1, chunks))) // 8) * 8)
+    return [(y, min(H, y + step)) for y in range(0, H, step)]
+
+
+def _broadcast_build_chunked(backend, f1_rows, fmap2, num_levels, bounds, src, group, rank):
+    """Broadcast rank src's fmap2 as target-row chunks (all issued asynchronously, in order) and
+    build each chunk's pyramid rows as soon as it has arrived; non-source ranks also assemble the
+    chunks into fmap2 (the broadcast's contract: fmap2 ends as rank src's map everywhere).
+    Returns the pyramid levels of this rank's query slab."""
+    B, D, H, W = fmap2.shape
+    with torch.no_grad():
+        bufs = [fmap2.new_empty((B, D, y1 - y0, W)) for y0, y1 in bounds]
+        if rank == src:
+            for buf, (y0, y1) in zip(bufs, bounds):
+                buf.copy_(fmap2[:, :, y0:y1])
+        works = [dist.broadcast(buf, src=src, group=group, async_op=True) for buf in bufs]
+        levels, ws = backend.region_begin(f1_rows, tuple(fmap2.shape), num_levels)
+        for k, ((y0, y1), buf, work) in enumerate(zip(bounds, bufs, works)):
+            work.wait()  # RCCL: the compute stream waits on chunk k only; chunk k+1 keeps arriving
+            if f1_rows.shape[2] > 0:
+                backend.build_region(f1_rows, buf, y0, y1, H, levels, ws, k == 0)
+            if rank != src:
+                fmap2[:, :, y0:y1].copy_(buf)
+    return levels
+
+
 def _alloc_pyramid_rows(B, NQ, H, W, num_levels, like):
     shapes = [(H >> l, W >> l) for l in range(num_levels)]
     sizes = [B * NQ * h * w for h, w in shapes]
@@ -100,7 +149,7 @@ def _alloc_pyramid_rows(B, NQ, H, W, num_levels, like):
 
 class _ShardState:
     __slots__ = ("levels", "grad_levels", "B", "NQ", "H", "W", "backend", "group", "h0", "h1", "full1", "stash",
-                 "radius")
+                 "radius", "chunked")
 
 
 class _ShardBuildFn(torch.autograd.Function):
@@ -110,7 +159,12 @@ class _ShardBuildFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, f1, f2, num_levels, st):
         f1_rows = f1[:, :, st.h0:st.h1].contiguous() if st.full1 else f1
-        st.levels = st.backend.build(f1_rows, f2, num_levels) if st.NQ > 0 else None
+        if st.chunked is not None:  # the chunked broadcast of f2, each chunk built on arrival
+            bounds, src, rank = st.chunked
+            lv = _broadcast_build_chunked(st.backend, f1_rows, f2, num_levels, bounds, src, st.group, rank)
+            st.levels = lv if st.NQ > 0 else None
+        else:
+            st.levels = st.backend.build(f1_rows, f2, num_levels) if st.NQ > 0 else None
         ctx.save_for_backward(f1_rows, f2)
         ctx.st, ctx.num_levels, ctx.f1_shape = st, num_levels, tuple(f1.shape)
         return f1.new_zeros(())  # autograd anchor of the lookups
@@ -232,9 +286,11 @@ class RowShardedCorrBlock:
 
     fmap1: the full query map [B, D, H, W] (each rank slices its rows) or, with
            ``fmap1_is_slab=True``, already this rank's rows [B, D, h1-h0, W].
-    fmap2: [B, D, H, W] on every rank; the contents on rank `src` are broadcast to all (a
-           blocking broadcast here), or a PendingFmap2 from ``prefetch`` whose broadcast was
-           started earlier and overlapped the previous pair's work (see Fmap2DoubleBuffer).
+    fmap2: [B, D, H, W] on every rank; the contents on rank `src` are broadcast to all — in
+           ``chunks`` target-row chunks whose builds start as each arrives (0 = automatic:
+           4 when the backend builds by region and H >= 32, else one blocking broadcast) — or a
+           PendingFmap2 from ``prefetch`` whose broadcast was started earlier and overlapped the
+           previous pair's work (see Fmap2DoubleBuffer).
     __call__(coords): coords of this rank's rows [B, 2, h1-h0, W] (or the full [B, 2, H, W],
            sliced) -> this rank's lookup rows [B, L*K, h1-h0, W].
     """
@@ -250,7 +306,7 @@ class RowShardedCorrBlock:
         return PendingFmap2(fmap2, work)
 
     def __init__(self, fmap1, fmap2, num_levels=4, radius=4, group=None, src=0,
-                 fmap1_is_slab=False, backend=HipRows, broadcast=True):
+                 fmap1_is_slab=False, backend=HipRows, broadcast=True, chunks=0):
         self.num_levels, self.radius = num_levels, radius
         self.group = group
         self.world = dist.get_world_size(group)
@@ -268,7 +324,12 @@ class RowShardedCorrBlock:
         self.B, self.H, self.W = B, H, W
         self.h0, self.h1 = row_partition(H, self.world, self.rank)
         self.backend = backend
-        if broadcast and self.world > 1:
+        region = hasattr(backend, "build_region") and backend.region_supported(num_levels)
+        if chunks == 0:
+            chunks = 4 if region and H >= 32 else 1
+        bounds = chunk_bounds(H, chunks) if region and chunks > 1 else None
+        chunked = broadcast and self.world > 1 and bounds is not None and len(bounds) > 1
+        if broadcast and self.world > 1 and not chunked:
             with torch.no_grad():
                 dist.broadcast(fmap2, src=src, group=group)
         f1 = fmap1 if fmap1_is_slab else fmap1[:, :, self.h0:self.h1]
@@ -284,13 +345,18 @@ class RowShardedCorrBlock:
             st.backend, st.group, st.grad_levels, st.levels = backend, group, None, None
             st.stash, st.radius = [], radius
             st.h0, st.h1, st.full1 = self.h0, self.h1, not fmap1_is_slab
+            st.chunked = (bounds, src, self.rank) if chunked else None
             self._st = st
             src1 = fmap1 if st.full1 else f1.contiguous()
             self._token = _ShardBuildFn.apply(src1, fmap2, num_levels, st)
             self.corr_pyramid = st.levels if self.h1 > self.h0 else None
             return
-        self.corr_pyramid = (backend.build(f1.contiguous(), fmap2, num_levels)
-                             if self.h1 > self.h0 else None)
+        if chunked:
+            lv = _broadcast_build_chunked(backend, f1.contiguous(), fmap2, num_levels, bounds, src, group, self.rank)
+            self.corr_pyramid = lv if self.h1 > self.h0 else None
+        else:
+            self.corr_pyramid = (backend.build(f1.contiguous(), fmap2, num_levels)
+                                 if self.h1 > self.h0 else None)
 
     @property
     def rows(self):

@@ -102,6 +102,20 @@ int corr_build_ex(int algo, const float *fmap1_rows, int NQ, const float *fmap2,
                   size_t workspace_bytes, void *stream);
 
 /*
+ * One target-row region of corr_build_ex (CORR_BUILD_BF16X6 only): the pyramid entries of target
+ * rows [y0, y1) — level l rows [y0 >> l, ceil(y1 / 2^l)) of every query's maps — from a slab
+ * fmap2_rows [B][D][y1 - y0][W] holding just those rows of fmap2.  y0 a multiple of 8, y1 a
+ * multiple of 8 or H, levels <= 4.  Calls over a partition of [0, H) with the same workspace
+ * give the bits of one corr_build_ex call; the first call of a build sets
+ * CORR_REGION_PACK_QUERIES (the query operand is packed into the workspace once and reused).
+ * Lets a row-sharded caller build from fmap2 chunks as their broadcast arrives.
+ */
+#define CORR_REGION_PACK_QUERIES 1
+int corr_build_region(int algo, const float *fmap1_rows, int NQ, const float *fmap2_rows, int y0, int y1, int B,
+                      int D, int H, int W, int levels, float *const *pyr, void *workspace, size_t workspace_bytes,
+                      int flags, void *stream);
+
+/*
  * Window lookup.  Replaces CorrBlock.__call__ (model/corr.py:29-50) and bilinear_sampler
  * (model/utils.py:7-21):
  *   out[b][l*K + i*(2r+1) + j][h][w] = grid_sample(pyr[l][b*N + h*W + w],

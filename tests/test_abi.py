@@ -105,6 +105,22 @@ def test_build_ex_workspace_and_validation(lib):
         assert rc == -1 and "unknown algorithm" in lib.corr_last_error().decode(), hex(algo)
 
 
+def test_build_region_validation(lib):
+    """corr_build_region: bf16x6 only, region rows on 8-row patch boundaries, <= 4 levels, a
+    workspace as corr_build_ex's — all refused before any HIP call."""
+    pyr = (ctypes.c_void_p * 4)(256, 256, 256, 256)
+    ws = 1 << 40
+    call = lambda algo, y0, y1, L=4, H=60, wsb=ws, wsp=256: lib.corr_build_region(  # noqa: E731
+        algo, 256, 4800, 256, y0, y1, 1, 256, H, 80, L, pyr, wsp, wsb, 1, None)
+    assert call(1, 0, 16) == -2 and "BF16X6" in lib.corr_last_error().decode()
+    assert call(0, 0, 16) == -2
+    for y0, y1 in ((4, 16), (0, 12), (16, 16), (-8, 8), (48, 64)):
+        assert call(2, y0, y1) == -1 and "y0" in lib.corr_last_error().decode(), (y0, y1)
+    assert call(2, 0, 16, L=5) == -2 and "levels" in lib.corr_last_error().decode()
+    assert call(2, 0, 16, wsb=16) == -1 and "workspace" in lib.corr_last_error().decode()
+    assert call(2, 0, 16, wsp=260) == -1 and "aligned" in lib.corr_last_error().decode()
+
+
 def test_build_algo_env(monkeypatch):
     from eraft_amd import _lib
     monkeypatch.delenv("ERAFT_AMD_BUILD", raising=False)

@@ -116,6 +116,36 @@ def test_split_build_phases_compose(shape, algo):
         assert bit_equal(full[l].cpu().numpy(), split[l].cpu().numpy()), l
 
 
+@pytest.mark.parametrize("shape,regions", [
+    ((1, 256, 60, 80), [(0, 16), (16, 32), (32, 48), (48, 60)]),
+    ((1, 256, 60, 80), [(32, 60), (0, 8), (8, 32)]),          # any order: queries packed by the first call
+    ((8, 256, 36, 48), [(0, 8), (8, 24), (24, 36)]),
+    ((2, 200, 17, 23), [(0, 8), (8, 16), (16, 17)]),          # D % 32 != 0, H % 8 != 0, W % 16 != 0
+    ((1, 300, 20, 32), [(0, 16), (16, 20)]),                  # D > 256: the runtime K loop
+    ((3, 64, 24, 40), [(0, 24)]),
+])
+def test_build_region_matches_full(shape, regions):
+    """corr_build_region over a partition of the target rows, each call reading only its slab of
+    fmap2 ([B, D, y1 - y0, W]), writes the pyramid of one corr_build_ex call bit for bit (the
+    chunked fmap2 broadcast of the row-sharded path builds this way)."""
+    from eraft_amd import _lib
+    B, D, H, W = shape
+    t1 = torch.from_numpy(prng.gauss(61, (B, D, H, W))).to(DEV)
+    t2 = torch.from_numpy(prng.gauss(62, (B, D, H, W))).to(DEV)
+    L = min(4, int(np.log2(min(H, W))) + 1)
+    shapes = [(B * H * W, 1, H >> l, W >> l) for l in range(L)]
+    full = [torch.empty(s, device=DEV) for s in shapes]
+    reg = [torch.full(s, float("nan"), device=DEV) for s in shapes]
+    _lib.build(t1, t2, full, _lib.BUILD_BF16X6)
+    ws = _lib.build_workspace(t1, t2, _lib.BUILD_BF16X6)
+    ws.fill_(0x5A)
+    for k, (y0, y1) in enumerate(regions):
+        _lib.build_region(t1, t2[:, :, y0:y1].contiguous(), y0, y1, H, reg, ws, k == 0)
+    torch.cuda.synchronize()
+    for l in range(L):
+        assert bit_equal(full[l].cpu().numpy(), reg[l].cpu().numpy()), l
+
+
 @pytest.mark.parametrize("name", BUILD_CASES)
 def test_lookup_bitexact_on_reference_pyramid(name):
     g = load(name)

@@ -41,6 +41,27 @@ class OracleRows:
     def lookup(levels, coords_rows, radius, H, W):
         return torch.from_numpy(oracle.lookup_rows(levels, np.asarray(coords_rows.detach()), H, W, radius))
 
+    # target-row regions (the chunked broadcast): the chunks are gathered into a full map and
+    # the slab's pyramid is computed when the last one has arrived
+    chunked_regions = 0  # regions built (test bookkeeping)
+
+    @staticmethod
+    def region_supported(num_levels):
+        return True
+
+    @staticmethod
+    def region_begin(f1_rows, f2_shape, num_levels):
+        return [], {"f2": torch.zeros(f2_shape), "rows": 0, "L": num_levels}
+
+    @staticmethod
+    def build_region(f1_rows, f2_chunk, y0, y1, H, levels, st, first):
+        assert first == (st["rows"] == 0) and y0 % 8 == 0
+        st["f2"][:, :, y0:y1] = f2_chunk
+        st["rows"] += y1 - y0
+        OracleRows.chunked_regions += 1
+        if st["rows"] == H:
+            levels[:] = OracleRows.build(f1_rows, st["f2"], st["L"])
+
     # backward: the slab is embedded in a full-size problem whose other query rows carry zero
     # gradient, so the oracle's full-map backward gives exactly the slab's contributions
 
@@ -87,7 +108,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, shape, q):
+def _worker(rank, world, port, shape, q, chunks=1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -99,22 +120,28 @@ def _worker(rank, world, port, shape, q):
         # only rank 0 holds the real fmap2; the others must receive it by broadcast
         f2 = torch.from_numpy(prng.gauss(2, (B, D, H, W))) if rank == 0 else torch.zeros(B, D, H, W)
         OracleRows.h0 = row_partition(H, world, rank)[0]
-        blk = RowShardedCorrBlock(f1, f2, L, r, backend=OracleRows)
+        OracleRows.chunked_regions = 0
+        blk = RowShardedCorrBlock(f1, f2, L, r, backend=OracleRows, chunks=chunks)
         coords = torch.from_numpy(prng.lookup_coords(3, B, H, W, 3.0))
         out_rows = blk(coords)
         full = blk.gather(out_rows)
-        q.put((rank, blk.h0, blk.h1, out_rows.numpy(), full.numpy()))
+        # the broadcast's contract holds with chunks too: every rank's fmap2 is rank 0's
+        assert np.array_equal(f2.numpy(), prng.gauss(2, (B, D, H, W)))
+        q.put((rank, blk.h0, blk.h1, out_rows.numpy(), full.numpy(), OracleRows.chunked_regions))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,shape", [(2, (1, 8, 12, 16, 3, 3)), (3, (2, 6, 10, 12, 2, 2))])
-def test_row_sharded_matches_unsharded(world, shape):
+@pytest.mark.parametrize("world,shape,chunks", [(2, (1, 8, 12, 16, 3, 3), 1), (3, (2, 6, 10, 12, 2, 2), 1),
+                                                (2, (1, 8, 24, 16, 3, 3), 3), (3, (2, 6, 20, 12, 3, 2), 4)])
+def test_row_sharded_matches_unsharded(world, shape, chunks):
+    """Row partition + fmap2 broadcast (one blocking broadcast, or target-row chunks each built
+    on arrival: SURVEY §8e's overlap) + slab lookups + gather, bit-identical to unsharded."""
     B, D, H, W, L, r = shape
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(g, world, port, shape, q)) for g in range(world)]
+    procs = [ctx.Process(target=_worker, args=(g, world, port, shape, q, chunks)) for g in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -124,10 +151,13 @@ def test_row_sharded_matches_unsharded(world, shape):
     f1, f2 = prng.gauss(1, (B, D, H, W)), prng.gauss(2, (B, D, H, W))
     ref = oracle.lookup(oracle.build_pyramid(f1, f2, L), prng.lookup_coords(3, B, H, W, 3.0), r)
     covered = []
-    for rank, h0, h1, rows, full in sorted(res, key=lambda t: t[0]):
+    from eraft_amd.sharded import chunk_bounds
+    for rank, h0, h1, rows, full, regions in sorted(res, key=lambda t: t[0]):
         covered += list(range(h0, h1))
         assert bit_equal(rows, ref[:, :, h0:h1])
         assert bit_equal(full, ref)
+        # the chunked path built every chunk as its own region (ranks with rows)
+        assert regions == (len(chunk_bounds(H, chunks)) if chunks > 1 and h1 > h0 else 0)
     assert covered == list(range(H))
 
 
@@ -236,7 +266,7 @@ def test_row_sharded_prefetch_rejects_training():
         assert bit_equal(out, ref)
 
 
-def _train_worker(rank, world, port, shape, q):
+def _train_worker(rank, world, port, shape, q, chunks=1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -248,7 +278,7 @@ def _train_worker(rank, world, port, shape, q):
         f2 = torch.from_numpy(prng.gauss(2, (B, D, H, W))).requires_grad_(True)
         h0, h1 = row_partition(H, world, rank)
         OracleRows.h0 = h0
-        blk = RowShardedCorrBlock(f1, f2, L, r, backend=OracleRows)
+        blk = RowShardedCorrBlock(f1, f2, L, r, backend=OracleRows, chunks=chunks)
         loss = 0
         for t in range(T):
             c = torch.from_numpy(prng.lookup_coords(10 + t, B, H, W, 3.0))
@@ -260,15 +290,18 @@ def _train_worker(rank, world, port, shape, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,shape", [(2, (1, 8, 12, 16, 3, 3, 2)), (3, (2, 6, 8, 12, 2, 2, 3)),
-                                         (3, (1, 4, 2, 8, 1, 1, 2))])  # last: rank 2 owns no rows
-def test_row_sharded_training_grads(world, shape):
-    """dfmap1 rows are rank-local; dfmap2 = all-reduce of the slab partials == unsharded."""
+@pytest.mark.parametrize("world,shape,chunks", [(2, (1, 8, 12, 16, 3, 3, 2), 1), (3, (2, 6, 8, 12, 2, 2, 3), 1),
+                                                (3, (1, 4, 2, 8, 1, 1, 2), 1),  # rank 2 owns no rows
+                                                (2, (1, 8, 24, 16, 3, 3, 2), 3),  # chunked fmap2 broadcast
+                                                (3, (1, 4, 17, 8, 2, 1, 2), 2)])
+def test_row_sharded_training_grads(world, shape, chunks):
+    """dfmap1 rows are rank-local; dfmap2 = all-reduce of the slab partials == unsharded (also
+    with the chunked fmap2 broadcast inside the build's autograd forward)."""
     B, D, H, W, L, r, T = shape
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_train_worker, args=(g, world, port, shape, q)) for g in range(world)]
+    procs = [ctx.Process(target=_train_worker, args=(g, world, port, shape, q, chunks)) for g in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -349,7 +382,7 @@ def test_row_sharded_encoder_param_grads():
             assert np.abs(a - b).max() <= 1e-5 * np.abs(b).max(), rank
 
 
-def _gpu_worker(rank, world, port, shape, q):
+def _gpu_worker(rank, world, port, shape, q, chunks=1):
     """HIP row kernels in world processes sharing cuda:0 (gloo carries the CUDA tensors: RCCL
     refuses two ranks on one device): broadcast of fmap2, slab build + lookups, the gather, and
     the training backward with both fmap gradients all-reduced."""
@@ -365,7 +398,7 @@ def _gpu_worker(rank, world, port, shape, q):
         f2 = (torch.from_numpy(prng.gauss(2, (B, D, H, W))) if rank == 0 else torch.zeros(B, D, H, W)).to(dev)
         f2.requires_grad_(True)
         h0, h1 = row_partition(H, world, rank)
-        blk = RowShardedCorrBlock(f1, f2, L, r)
+        blk = RowShardedCorrBlock(f1, f2, L, r, chunks=chunks)
         K = (2 * r + 1) ** 2
         loss, outs = 0, []
         for t in range(T):
@@ -383,17 +416,19 @@ def _gpu_worker(rank, world, port, shape, q):
 
 
 @pytest.mark.gpu
-def test_row_sharded_multiprocess_on_gpu():
+@pytest.mark.parametrize("chunks", [1, 2])
+def test_row_sharded_multiprocess_on_gpu(chunks):
     """Two processes on the MI355X through the product backend (HipRows): lookup rows and the
     gathered output bit-identical to the one-process CorrBlock; training gradients (both
-    all-reduced) within 1e-5 of it."""
+    all-reduced) within 1e-5 of it.  chunks = 2: fmap2 broadcast as two target-row chunks, each
+    built by corr_build_region as it arrives."""
     from eraft_amd import CorrBlock
     world, shape = 2, (2, 32, 18, 24, 4, 4, 3)
     B, D, H, W, L, r, T = shape
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gpu_worker, args=(g, world, port, shape, q)) for g in range(world)]
+    procs = [ctx.Process(target=_gpu_worker, args=(g, world, port, shape, q, chunks)) for g in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
