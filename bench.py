@@ -508,7 +508,10 @@ def main():
                 build_only()
                 run_lookups()
 
-        launch = "eager" if args.eager or prefetch else "hipgraph"
+        # gloo collectives on device tensors go through host copies: not capturable (and a failed
+        # capture poisons the stream), so only an RCCL sharded pair is captured
+        host_coll = sharded and world > 1 and dist.get_backend() != "nccl"
+        launch = "eager" if args.eager or prefetch or host_coll else "hipgraph"
         step = pair
         if train:
             step = autograd_step

@@ -77,7 +77,7 @@ using namespace corr;
 
 extern "C" {
 
-int corr_version(void) { return 102; }
+int corr_version(void) { return 103; }
 
 const char *corr_last_error(void) { return g_err; }
 
@@ -369,6 +369,47 @@ int corr_lookup_conv(const float *const *pyr, const float *coords, int B, int H,
         return rc;
     return hip_status(launch_lookup_conv(lp, coords, B, H * W, H, W, levels, radius, packed_weight, bias, relu, out,
                                          (hipStream_t)stream),
+                      fn);
+}
+
+size_t corr_lookup_conv_bwd_workspace(int B, int H, int W, int levels) {
+    if (B < 1 || H < 1 || W < 1 || levels < 1 || levels > 4) return 0;
+    return lookup_conv_bwd_workspace(B, H * W, levels);
+}
+
+int corr_lookup_conv_bwd(const float *const *pyr, const float *coords, int B, int H, int W, int levels, int radius,
+                         const void *packed_weight, const float *out, int relu, const float *grad_out,
+                         float *grad_weight, float *grad_bias, float *grad_lookup, void *workspace,
+                         size_t workspace_bytes, void *stream) {
+    static const char *fn = "corr_lookup_conv_bwd";
+    g_err[0] = 0;
+    int rc = check_dims(fn, B, H * W, H, W, levels);
+    if (rc) return rc;
+    if (radius != 4 || levels > 4)
+        return fail(CORR_EUNSUPPORTED, "%s: built for radius 4 and <= 4 levels (got %d, %d)", fn, radius, levels);
+    if (!pyr) return fail(CORR_EINVAL, "%s: pyr is null", fn);
+    ConstLevelPtrs lp{};
+    for (int l = 0; l < levels; ++l) {
+        if ((rc = check_ptr(fn, pyr[l], "pyr[l]"))) return rc;
+        lp.p[l] = pyr[l];
+    }
+    if ((rc = check_ptr(fn, coords, "coords")) || (rc = check_ptr(fn, packed_weight, "packed_weight")) ||
+        (rc = check_ptr(fn, grad_out, "grad_out")))
+        return rc;
+    if (relu && (rc = check_ptr(fn, out, "out"))) return rc;
+    if (!grad_weight && !grad_bias && !grad_lookup) return CORR_OK;
+    if (grad_weight || grad_bias) {
+        const size_t need = lookup_conv_bwd_workspace(B, H * W, levels);
+        if (!workspace || workspace_bytes < need)
+            return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
+        if ((uintptr_t)workspace % 16)
+            return fail(CORR_EINVAL, "%s: workspace must be 16-byte aligned", fn);
+    }
+    if ((H * W) % 4 == 0 && ((uintptr_t)grad_out % 16 || (relu && (uintptr_t)out % 16)))
+        return fail(CORR_EINVAL, "%s: grad_out and out must be 16-byte aligned when H*W %% 4 == 0", fn);
+    return hip_status(launch_lookup_conv_bwd(lp, coords, B, H * W, H, W, levels, radius, packed_weight, out, relu,
+                                             grad_out, grad_weight, grad_bias, grad_lookup, workspace,
+                                             (hipStream_t)stream),
                       fn);
 }
 

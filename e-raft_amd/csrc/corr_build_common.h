@@ -136,6 +136,40 @@ inline int level_store_mode(int Wl, const float *base) {
     return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// The exact three-piece bf16 split (corr_build_bf16.hip's operands, lookup_conv_bwd's).
+// ---------------------------------------------------------------------------------------
+typedef __bf16 bf16s_pair __attribute__((ext_vector_type(2)));
+typedef float bf16s_f32x2 __attribute__((ext_vector_type(2)));
+
+// bf16 round-to-nearest-even of a pair, as fp32 values and as the packed pair.
+__device__ __forceinline__ unsigned rn_pair(float a, float b, float &ha, float &hb) {
+    const unsigned u = __builtin_bit_cast(unsigned, __builtin_convertvector(bf16s_f32x2{a, b}, bf16s_pair));
+    ha = __builtin_bit_cast(float, u << 16);
+    hb = __builtin_bit_cast(float, u & 0xffff0000u);
+    return u;
+}
+
+// Split a pair of fp32 features into packed bf16 (hi, mid, lo) pairs, x = hi + mid + lo exactly.
+// Guards: an infinite feature keeps hi = x and mid = lo = 0 (its products are x * the other
+// operand, as in fp32); a finite feature whose hi rounds up past the bf16 range (|x| within
+// 2^-9 of FLT_MAX) takes the truncated hi instead.  NaN propagates through hi.
+__device__ __forceinline__ void split3(float a, float b, unsigned &hi, unsigned &mid, unsigned &lo) {
+    float ha, hb;
+    hi = rn_pair(a, b, ha, hb);
+    if (__builtin_expect(__builtin_isinf(ha) | __builtin_isinf(hb), 0)) {
+        const unsigned ua = __builtin_bit_cast(unsigned, a), ub = __builtin_bit_cast(unsigned, b);
+        if (__builtin_isinf(ha) && !__builtin_isinf(a)) ha = __builtin_bit_cast(float, ua & 0xffff0000u);
+        if (__builtin_isinf(hb) && !__builtin_isinf(b)) hb = __builtin_bit_cast(float, ub & 0xffff0000u);
+        hi = (__builtin_bit_cast(unsigned, ha) >> 16) | (__builtin_bit_cast(unsigned, hb) & 0xffff0000u);
+    }
+    float ra = __builtin_isinf(a) ? 0.f : a - ha, rb = __builtin_isinf(b) ? 0.f : b - hb;
+    float ma, mb;
+    mid = rn_pair(ra, rb, ma, mb);
+    float da, db;
+    lo = rn_pair(ra - ma, rb - mb, da, db);  // exact: the residuals have <= 8 significant bits
+}
+
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace corr

@@ -85,6 +85,10 @@ hipError_t launch_lookup_conv_weights(const float *w, int O, int C, void *packed
 hipError_t launch_lookup_conv(const ConstLevelPtrs &pyr, const float *coords, int B, int NQ, int H, int W,
                               int levels, int radius, const void *packed, const float *bias, int relu, float *out,
                               hipStream_t s);
+size_t lookup_conv_bwd_workspace(int B, int NQ, int levels);
+hipError_t launch_lookup_conv_bwd(const ConstLevelPtrs &pyr, const float *coords, int B, int NQ, int H, int W,
+                                  int levels, int radius, const void *packed, const float *out, int relu,
+                                  const float *grad_out, float *dW, float *db, float *dlk, void *ws, hipStream_t s);
 size_t splat_workspace(int B, int H, int W);
 size_t voxel_workspace(int M, int C, int H, int W);
 size_t voxel_tbilinear_workspace(int M, int C, int H, int W);

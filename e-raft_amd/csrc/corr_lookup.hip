@@ -507,6 +507,376 @@ __global__ __launch_bounds__(kLcNT) void lookup_conv_kernel(ConstLevelPtrs pyr, 
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Training backward of the fused lookup + convc1 (autograd of update.py:68,75 through
+// corr.py:29-50).  With g' = dL/dout under ReLU's threshold backward (out <= 0 -> 0; a NaN
+// output passes its gradient, as torch's):
+//   d bias[o]     = sum_{b,n} g'[b][o][n]
+//   d W[o][c]     = sum_{b,n} g'[b][o][n] lk[b][c][n]    lk = the lookup, RECOMPUTED on chip
+//   d lk[b][c][n] = sum_o W[o][c] g'[b][o][n]           the lookup's upstream gradient, which
+//                                                       corr_backward's fold consumes
+// on the bf16 MFMA with the build's exact three-piece split (x = hi + mid + lo, six products
+// per fp32 product, smallest first: no narrower than fp32, no scales).  Workgroup = (query
+// range r, level l), 8 waves; per 32-query block of the range:
+//   1. wave w loads g' rows o in [32 w, 32 w + 32) straight into its dW A fragments;
+//   2. the level-l lookup of the 32 queries (lookup_block: the forward's values bit for bit)
+//      into ct[81][32] — the 324-channel lookup never reaches HBM;
+//   3. split ct -> lkB[piece][c][q] (dW's B operand) and the A fragments -> gB[piece][q][o]
+//      (d lk's B operand);
+//   4. d W: wave w's 2 x 6 tiles (o-tiles 2w, 2w+1 x the level's 81 channels padded to 96) add
+//      the block's six-product sum (its one 32-deep K step) to fp32 registers;
+//   5. d lk: wave w < 6 owns channel tile w, A = the pre-split W^T pieces (L2-resident
+//      weight pack), K = 256 in 8 steps, two accumulators (hi*hi; the rest) summed at the end.
+// The dW tiles stay in registers across the range; each workgroup writes one partial, and
+// lookup_conv_bwd_reduce sums the R partials in range order (deterministic, no atomics).  The
+// L workgroups of one range sit 8 block ids apart, i.e. on one XCD, where they share g' in L2.
+constexpr int kCbQB = 32, kCbNT = 512, kCbCT = 6 /* 96 >= 81 */, kCbKS = kLcO / 32, kCbGS = kLcO + 8;
+constexpr size_t kCbWtU = (size_t)4 * kCbCT * kCbKS * 3 * 64;  // u32x4 of the W^T pack
+// dW kernel: waves per SIMD it is compiled for.  2 = one 8-wave workgroup per CU with the dW
+// tiles, the prefetched next block and the lookup all in registers (~200 VGPRs); 4 (<= 128
+// VGPRs, two workgroups per CU) spills and measured slower.
+constexpr int kCbDwWaves = 2;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x4 mfma_bf16(u32x4 a, u32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                  0, 0, 0);
+}
+
+// W [256][C] -> W^T pieces [level][channel tile][K step][hi, mid, lo][64 lanes] in the 16x16x32
+// A-fragment order: lane = 16 kg + c16 holds W[32 ks + 8 kg + j][81 l + 16 ct + c16], j < 8.
+__global__ __launch_bounds__(64) void lookup_conv_wt_kernel(const float *__restrict__ w, int C,
+                                                            u32x4 *__restrict__ wt) {
+    const int ks = blockIdx.x, ct = blockIdx.y, l = blockIdx.z, lane = threadIdx.x;
+    const int c = 16 * ct + (lane & 15), cg = 81 * l + c, o0 = 32 * ks + 8 * (lane >> 4);
+    const bool ok = c < 81 && cg < C;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = ok ? w[(size_t)(o0 + j) * C + cg] : 0.f;
+    unsigned h[4], m[4], lo[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split3(v[2 * j], v[2 * j + 1], h[j], m[j], lo[j]);
+    u32x4 *dst = wt + (((size_t)l * kCbCT + ct) * kCbKS + ks) * 3 * 64 + lane;
+    dst[0] = u32x4{h[0], h[1], h[2], h[3]};
+    dst[64] = u32x4{m[0], m[1], m[2], m[3]};
+    dst[128] = u32x4{lo[0], lo[1], lo[2], lo[3]};
+}
+
+struct CbArgs {
+    ConstLevelPtrs pyr;
+    const float *coords, *g, *out;
+    const u32x4 *wt;
+    float *dlk;    // [B][C][NQ] or null
+    float *part;   // [R][256][C] dW partials, or null (no dW)
+    float *bpart;  // [R][256] bias partials, or null
+    int B, NQ, H, W, L, C, relu, R, nqb;
+};
+
+// g and the forward output at this lane's 16 fragment positions (t = 0, 1): o = o0 + 16 t + r16,
+// q = 8 kg + j of the block at n0 (g = 0 past N); gprime() applies ReLU's threshold backward.
+struct GRaw {
+    float g[2][8], o[2][8];
+};
+
+__device__ __forceinline__ void load_graw(const CbArgs &a, int b, int n0, int o0, int r16, int kg, bool vec, GRaw &x) {
+    const int N = a.NQ;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const size_t row = ((size_t)b * kLcO + o0 + 16 * t + r16) * N + n0 + 8 * kg;
+        if (vec) {
+            const float4 g0 = *reinterpret_cast<const float4 *>(a.g + row);
+            const float4 g1 = *reinterpret_cast<const float4 *>(a.g + row + 4);
+            x.g[t][0] = g0.x, x.g[t][1] = g0.y, x.g[t][2] = g0.z, x.g[t][3] = g0.w;
+            x.g[t][4] = g1.x, x.g[t][5] = g1.y, x.g[t][6] = g1.z, x.g[t][7] = g1.w;
+            if (a.relu) {
+                const float4 o0v = *reinterpret_cast<const float4 *>(a.out + row);
+                const float4 o1v = *reinterpret_cast<const float4 *>(a.out + row + 4);
+                x.o[t][0] = o0v.x, x.o[t][1] = o0v.y, x.o[t][2] = o0v.z, x.o[t][3] = o0v.w;
+                x.o[t][4] = o1v.x, x.o[t][5] = o1v.y, x.o[t][6] = o1v.z, x.o[t][7] = o1v.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const bool in = n0 + 8 * kg + j < N;
+                x.g[t][j] = in ? a.g[row + j] : 0.f;
+                x.o[t][j] = (in && a.relu) ? a.out[row + j] : 1.f;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void gprime(const CbArgs &a, const GRaw &x, float (&v)[2][8]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[t][j] = (a.relu && x.o[t][j] <= 0.f) ? 0.f : x.g[t][j];
+}
+
+// Lane pair (o, o ^ 1) trades halves of a packed bf16 pair along q: the even lane returns row q
+// = 2j's (o, o + 1) pair, the odd lane row 2j + 1's (DPP quad_perm [1, 0, 3, 2] + v_perm).
+__device__ __forceinline__ unsigned pair_transpose(unsigned own, bool odd) {
+    const unsigned other = (unsigned)__builtin_amdgcn_mov_dpp((int)own, 0xB1, 0xF, 0xF, false);
+    return odd ? __builtin_amdgcn_perm(own, other, 0x07060302u) : __builtin_amdgcn_perm(other, own, 0x05040100u);
+}
+
+// ---- d lk = W^T g' (and nothing else): one workgroup per 32-query block, all levels ----
+// Wave w stages g' rows o in [32 w, 32 w + 32) of the block as bf16 pieces gB[piece][q][o pair]
+// (lane pairs transpose, one dword store per piece and pair of queries); then wave w owns
+// channel tiles w, w + 8, w + 16 of the 4 levels x 6 tiles (A = the pre-split W^T pieces, L2),
+// K = 256 in 8 steps, two accumulators (hi*hi; the rest) summed at the end.
+__global__ __launch_bounds__(kCbNT) void lookup_conv_bwd_dlk_kernel(CbArgs a) {
+    __shared__ unsigned gB[3][kCbQB][kCbGS / 2];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r16 = lane & 15, kg = lane >> 4;
+    const int N = a.NQ;
+    const int blk = blockIdx.x;
+    const int b = blk / a.nqb, n0 = (blk - b * a.nqb) * kCbQB;
+    const bool vec = (N & 3) == 0 && n0 + kCbQB <= N;
+    {
+        GRaw x;
+        load_graw(a, b, n0, 32 * w, r16, kg, vec, x);
+        float v[2][8];
+        gprime(a, x, v);
+        const bool odd = r16 & 1;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int col = 16 * w + 8 * t + (r16 >> 1);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                unsigned h, m, lo;
+                split3(v[t][2 * j], v[t][2 * j + 1], h, m, lo);
+                const int q = 8 * kg + 2 * j + (odd ? 1 : 0);
+                gB[0][q][col] = pair_transpose(h, odd);
+                gB[1][q][col] = pair_transpose(m, odd);
+                gB[2][q][col] = pair_transpose(lo, odd);
+            }
+        }
+    }
+    __syncthreads();
+    constexpr int PS = kCbQB * (kCbGS / 2);  // piece stride (dwords)
+#pragma unroll 1
+    for (int k = 0; k < 3; ++k) {
+        const int ct = w + 8 * k, l = ct / kCbCT, cl = ct - l * kCbCT;
+        if (l >= a.L) break;
+        // two partial sums per query tile (hi*hi + lo*hi + hi*lo; mid*mid + mid*hi + hi*mid) and
+        // two query tiles: four independent MFMA chains.  W^T pieces (L2) run kPf steps ahead.
+        f32x4 acc[2], acs[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[t] = acs[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const u32x4 *wp = a.wt + (size_t)ct * kCbKS * 3 * 64 + lane;
+        constexpr int kPf = 4;
+        u32x4 wq[kPf][3];
+#pragma unroll
+        for (int k2 = 0; k2 < kPf; ++k2)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) wq[k2][p] = wp[(3 * k2 + p) * 64];
+#pragma unroll
+        for (int ks = 0; ks < kCbKS; ++ks) {
+            const u32x4 wh = wq[ks % kPf][0], wm = wq[ks % kPf][1], wl = wq[ks % kPf][2];
+            if (ks + kPf < kCbKS) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) wq[ks % kPf][p] = wp[(3 * (ks + kPf) + p) * 64];
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const unsigned *gq = &gB[0][16 * t + r16][16 * ks + 4 * kg];
+                const u32x4 gh = *reinterpret_cast<const u32x4 *>(gq);
+                const u32x4 gm = *reinterpret_cast<const u32x4 *>(gq + PS);
+                const u32x4 gl = *reinterpret_cast<const u32x4 *>(gq + 2 * PS);
+                acs[t] = mfma_bf16(wl, gh, acs[t]);
+                acc[t] = mfma_bf16(wm, gm, acc[t]);
+                acs[t] = mfma_bf16(wh, gl, acs[t]);
+                acc[t] = mfma_bf16(wm, gh, acc[t]);
+                acs[t] = mfma_bf16(wh, gh, acs[t]);
+                acc[t] = mfma_bf16(wh, gm, acc[t]);
+            }
+        }
+        // C[row = channel 16 cl + 4 kg + i of level l][col = query 16 t + r16]
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int n = n0 + 16 * t + r16;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int c = 16 * cl + 4 * kg + i;
+                if (c < 81 && n < N) a.dlk[((size_t)b * a.C + 81 * l + c) * N + n] = acc[t][i] + acs[t][i];
+            }
+        }
+    }
+}
+
+// ---- dW (and d bias): workgroup (query range r, level l), dW tiles in registers across it ----
+struct CbSmem {
+    LookupSmem<9, kCbQB> lk;                      // the lookup's staging
+    float ct[81][kCbQB];                          // the lookup of the block
+    unsigned lkB[3][kCbCT * 16][kCbQB / 2 + 4];   // its pieces [piece][c][q pair] (+4: no conflicts)
+};
+
+__global__ __launch_bounds__(kCbNT, kCbDwWaves) void lookup_conv_bwd_dw_kernel(CbArgs a) {
+    constexpr int S = 9;
+    __shared__ CbSmem sm;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r16 = lane & 15, kg = lane >> 4;
+    const int bid = blockIdx.x, grp = bid >> 3;
+    const int l = grp % a.L, r = (grp / a.L) * 8 + (bid & 7);
+    const int N = a.NQ, NB = a.B * a.nqb;
+    const int blk0 = (int)((long long)r * NB / a.R), blk1 = (int)((long long)(r + 1) * NB / a.R);
+    const bool do_dw = a.part != nullptr, do_b = a.bpart != nullptr && l == 0;
+    if (!do_dw && !do_b) return;
+    const bool nvec = (N & 3) == 0;
+    f32x4 mW[2][kCbCT];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int c = 0; c < kCbCT; ++c) mW[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float mb[2] = {0.f, 0.f};
+    // The next block's coords (this thread's query of the lookup) and g / out (its A-fragment
+    // positions) are loaded one block ahead, during this block's lookup and MFMAs.
+    const int q = tid % kCbQB;
+    const bool coord_thread = tid / kCbQB < S;
+    float pcx = 0.f, pcy = 0.f;
+    GRaw nx;
+    auto prefetch_coords = [&](int blk) {
+        const int b = blk / a.nqb, n0 = (blk - b * a.nqb) * kCbQB;
+        if (do_dw && coord_thread && n0 + q < N) {
+            pcx = a.coords[((size_t)b * 2 + 0) * N + n0 + q];
+            pcy = a.coords[((size_t)b * 2 + 1) * N + n0 + q];
+        }
+    };
+    auto prefetch_g = [&](int blk) {
+        const int b = blk / a.nqb, n0 = (blk - b * a.nqb) * kCbQB;
+        load_graw(a, b, n0, 32 * w, r16, kg, nvec && n0 + kCbQB <= N, nx);
+    };
+    if (blk0 < blk1) {
+        prefetch_coords(blk0);
+        prefetch_g(blk0);
+    }
+#pragma unroll 1
+    for (int blk = blk0; blk < blk1; ++blk) {
+        const int b = blk / a.nqb, n0 = (blk - b * a.nqb) * kCbQB;
+        const bool more = blk + 1 < blk1;
+        const float cxv = pcx, cyv = pcy;
+        if (more) prefetch_coords(blk + 1);
+        // ---- 1. the level-l lookup of the block -> ct (bit-identical to corr_lookup) ----
+        if (do_dw)
+            lookup_block_v<S, kCbQB, kCbNT, 0>(sm.lk, a.pyr.p[l], cxv, cyv, b, n0, N, a.H, a.W, l, tid,
+                                               [&](int j, float acc) { sm.ct[(tid / kCbQB) * S + j][q] = acc; });
+        float v[2][8];
+        gprime(a, nx, v);
+        // ---- 2. bias: this lane's g' column sums ----
+        if (do_b) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                float s = v[t][0];
+#pragma unroll
+                for (int j = 1; j < 8; ++j) s += v[t][j];
+                mb[t] += s;
+            }
+        }
+        if (!do_dw) {
+            if (more) prefetch_g(blk + 1);
+            continue;
+        }
+        __syncthreads();  // ct complete
+        // ---- 3. ct -> lkB pieces; g' -> A fragments (registers) ----
+        for (int idx = tid; idx < kCbCT * 16 * (kCbQB / 2); idx += kCbNT) {
+            const int c = idx / (kCbQB / 2), qp = idx - c * (kCbQB / 2), q = 2 * qp;
+            float x0 = 0.f, x1 = 0.f;
+            if (c < 81) {
+                if (n0 + q < N) x0 = sm.ct[c][q];
+                if (n0 + q + 1 < N) x1 = sm.ct[c][q + 1];
+            }
+            unsigned h, m, lo;
+            split3(x0, x1, h, m, lo);
+            sm.lkB[0][c][qp] = h;
+            sm.lkB[1][c][qp] = m;
+            sm.lkB[2][c][qp] = lo;
+        }
+        u32x4 ah[2], am[2], al[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            unsigned h[4], m[4], lo[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) split3(v[t][2 * j], v[t][2 * j + 1], h[j], m[j], lo[j]);
+            ah[t] = u32x4{h[0], h[1], h[2], h[3]};
+            am[t] = u32x4{m[0], m[1], m[2], m[3]};
+            al[t] = u32x4{lo[0], lo[1], lo[2], lo[3]};
+        }
+        if (more) prefetch_g(blk + 1);  // in flight during the MFMAs and the next lookup
+        __syncthreads();  // lkB complete (the next block's lookup rewrites ct / lkB only after
+                          // its own barriers, which every wave reaches after these MFMAs)
+        // ---- 4. dW += g'(block) lk(block)^T: A = g' rows (registers), B = lk rows (lkB) ----
+#pragma unroll
+        for (int c = 0; c < kCbCT; ++c) {
+            const u32x4 bh = *reinterpret_cast<const u32x4 *>(&sm.lkB[0][16 * c + r16][4 * kg]);
+            const u32x4 bm = *reinterpret_cast<const u32x4 *>(&sm.lkB[1][16 * c + r16][4 * kg]);
+            const u32x4 bl = *reinterpret_cast<const u32x4 *>(&sm.lkB[2][16 * c + r16][4 * kg]);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                f32x4 s = mfma_bf16(al[t], bh, f32x4{0.f, 0.f, 0.f, 0.f});
+                s = mfma_bf16(ah[t], bl, s);
+                s = mfma_bf16(am[t], bm, s);
+                s = mfma_bf16(am[t], bh, s);
+                s = mfma_bf16(ah[t], bm, s);
+                s = mfma_bf16(ah[t], bh, s);
+                mW[t][c] += s;
+            }
+        }
+    }
+    // ---- partials: C[row = o][col = channel] ----
+    if (do_dw) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int c = 0; c < kCbCT; ++c) {
+                const int ch = 16 * c + r16;
+                if (ch >= 81) continue;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int o = 32 * w + 16 * t + 4 * kg + i;
+                    a.part[((size_t)r * kLcO + o) * a.C + 81 * l + ch] = mW[t][c][i];
+                }
+            }
+    }
+    if (do_b) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            float s = mb[t];  // this lane's 8-query column sums; then the 4 column groups in order
+            const float s1 = __shfl_xor(s, 16), s2 = __shfl_xor(s, 32), s3 = __shfl_xor(s, 48);
+            if (kg == 0) a.bpart[(size_t)r * kLcO + 32 * w + 16 * t + r16] = ((s + s1) + s2) + s3;
+        }
+    }
+}
+
+// dW[o][c] = sum_r part[r][o][c], d bias[o] = sum_r bpart[r][o], r in order (loads 8 deep).
+__global__ __launch_bounds__(256) void lookup_conv_bwd_reduce_kernel(const float *__restrict__ part,
+                                                                     const float *__restrict__ bpart, int R, int C,
+                                                                     float *__restrict__ dW, float *__restrict__ db) {
+    const int i = blockIdx.x * 256 + threadIdx.x, n = kLcO * C;
+    const float *src;
+    size_t stride;
+    float *dst;
+    if (i < n) {
+        src = part + i, stride = (size_t)n, dst = dW ? dW + i : nullptr;
+    } else if (i < n + kLcO) {
+        src = bpart + (i - n), stride = kLcO, dst = db ? db + (i - n) : nullptr;
+    } else {
+        return;
+    }
+    if (!dst) return;
+    float s = 0.f;
+    int r = 0;
+    for (; r + 8 <= R; r += 8) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = src[(size_t)(r + k) * stride];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += v[k];
+    }
+    for (; r < R; ++r) s += src[(size_t)r * stride];
+    *dst = s;
+}
+
 template <int S, int BQ>
 struct LookupBwdSmem {
     static constexpr int WIN = S + 2;
@@ -1304,13 +1674,64 @@ hipError_t launch_lookup(const ConstLevelPtrs &pyr, const float *coords, int B, 
     }
 }
 
-size_t lookup_conv_weights_bytes() { return (size_t)(kLcO / 16) * kLcKC * 2 * 64 * sizeof(u32x4) + kLcO * sizeof(int); }
+// Packed weight buffer: the forward's f16 fragments [O/16][kLcKC][2][64] + shift[O], then (at a
+// 256-B offset) the backward's W^T bf16 pieces (kCbWtU u32x4).
+constexpr size_t kLcFwdBytes = (size_t)(kLcO / 16) * kLcKC * 2 * 64 * sizeof(u32x4) + kLcO * sizeof(int);
+constexpr size_t kLcWtOff = (kLcFwdBytes + 255) / 256 * 256;
+
+size_t lookup_conv_weights_bytes() { return kLcWtOff + kCbWtU * sizeof(u32x4); }
 
 hipError_t launch_lookup_conv_weights(const float *w, int O, int C, void *packed, hipStream_t s) {
     if (O != kLcO || C < 1 || C > kLcKP) return hipErrorInvalidValue;
     u32x4 *frag = static_cast<u32x4 *>(packed);
     int *shift = reinterpret_cast<int *>(frag + (size_t)(kLcO / 16) * kLcKC * 2 * 64);
     hipLaunchKernelGGL(lookup_conv_weights_kernel, dim3(kLcO), dim3(64), 0, s, w, C, frag, shift);
+    hipLaunchKernelGGL(lookup_conv_wt_kernel, dim3(kCbKS, kCbCT, 4), dim3(64), 0, s, w, C,
+                       reinterpret_cast<u32x4 *>(static_cast<char *>(packed) + kLcWtOff));
+    return hipGetLastError();
+}
+
+namespace {
+// Query ranges of the dW kernel: >= ~4 blocks per workgroup (each writes a 256 x C partial),
+// at most the workgroups that are resident at once (256 CUs x kCbDwWaves / 2 over the levels).
+int conv_bwd_ranges(int B, int NQ) {
+    const int nb = B * ((NQ + kCbQB - 1) / kCbQB);
+    const int r = (nb / 4 + 7) / 8 * 8;
+    return std::max(8, std::min(64 * kCbDwWaves / 2, r));
+}
+}  // namespace
+
+size_t lookup_conv_bwd_workspace(int B, int NQ, int levels) {
+    (void)levels;
+    const int R = conv_bwd_ranges(B, NQ);
+    return (size_t)R * kLcO * (4 * 81 + 1) * sizeof(float);
+}
+
+hipError_t launch_lookup_conv_bwd(const ConstLevelPtrs &pyr, const float *coords, int B, int NQ, int H, int W,
+                                  int levels, int radius, const void *packed, const float *out, int relu,
+                                  const float *grad_out, float *dW, float *db, float *dlk, void *ws, hipStream_t s) {
+    if (radius != 4 || levels < 1 || levels > 4) return hipErrorInvalidValue;
+    if (!dW && !db && !dlk) return hipSuccess;
+    CbArgs a{};
+    a.pyr = pyr;
+    a.coords = coords;
+    a.g = grad_out;
+    a.out = out;
+    a.wt = reinterpret_cast<const u32x4 *>(static_cast<const char *>(packed) + kLcWtOff);
+    a.dlk = dlk;
+    a.B = B, a.NQ = NQ, a.H = H, a.W = W, a.L = levels, a.C = levels * 81, a.relu = relu;
+    a.R = conv_bwd_ranges(B, NQ);
+    a.nqb = (NQ + kCbQB - 1) / kCbQB;
+    float *part = static_cast<float *>(ws);
+    a.part = dW ? part : nullptr;
+    a.bpart = db ? part + (size_t)a.R * kLcO * a.C : nullptr;
+    if (dlk) hipLaunchKernelGGL(lookup_conv_bwd_dlk_kernel, dim3(B * a.nqb), dim3(kCbNT), 0, s, a);
+    if (dW || db) hipLaunchKernelGGL(lookup_conv_bwd_dw_kernel, dim3(a.R * levels), dim3(kCbNT), 0, s, a);
+    if (dW || db) {
+        const int n = kLcO * a.C + kLcO;
+        hipLaunchKernelGGL(lookup_conv_bwd_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a.part, a.bpart, a.R,
+                           a.C, dW, db);
+    }
     return hipGetLastError();
 }
 

@@ -29,7 +29,8 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
            "corr_forward_splat", "corr_convex_upsample", "corr_voxel_grid_workspace",
            "corr_voxel_grid", "corr_lookup_conv", "corr_lookup_conv_weights", "corr_lookup_conv_weights_bytes", "corr_voxel_grid_tbilinear_workspace",
            "corr_voxel_grid_tbilinear", "corr_lookup_bwd_multi", "corr_pool_fold", "corr_backward_workspace",
-           "corr_backward", "corr_convex_upsample_bwd_workspace", "corr_convex_upsample_bwd", "corr_build_region")
+           "corr_backward", "corr_convex_upsample_bwd_workspace", "corr_convex_upsample_bwd", "corr_build_region",
+           "corr_lookup_conv_bwd_workspace", "corr_lookup_conv_bwd")
 
 # Build algorithms (include/corr_mi355x.h).  BF16X6 is the default: every fp32 feature split
 # exactly into three bf16 pieces, the six largest piece products on the bf16 MFMA, fp32
@@ -124,12 +125,15 @@ def load(path: str | None = None) -> ctypes.CDLL:
     lib.corr_backward_workspace.restype = sz
     lib.corr_backward.argtypes = [i, vp, vp, i, vp, i, vp, i, i, i, i, i, i, vp, vp, vp, vp, sz, vp]
     lib.corr_build_region.argtypes = [i, vp, i, vp, i, i, i, i, i, i, i, vp, vp, sz, i, vp]
+    lib.corr_lookup_conv_bwd_workspace.argtypes = [i, i, i, i]
+    lib.corr_lookup_conv_bwd_workspace.restype = sz
+    lib.corr_lookup_conv_bwd.argtypes = [vp, vp, i, i, i, i, i, vp, vp, i, vp, vp, vp, vp, vp, sz, vp]
     for f in ("corr_build_region", "corr_build", "corr_lookup", "corr_lookup_bwd", "corr_pool_bwd", "corr_build_bwd",
               "corr_build_rows", "corr_lookup_rows", "corr_lookup_bwd_rows", "corr_build_bwd_rows",
               "corr_build_ex", "corr_build_bwd_ex", "corr_forward_splat",
               "corr_convex_upsample", "corr_voxel_grid", "corr_lookup_conv", "corr_lookup_conv_weights",
               "corr_voxel_grid_tbilinear", "corr_lookup_bwd_multi", "corr_pool_fold", "corr_backward_workspace",
-              "corr_backward", "corr_convex_upsample_bwd"):
+              "corr_backward", "corr_convex_upsample_bwd", "corr_lookup_conv_bwd"):
         getattr(lib, f).restype = i
     if path is None:
         _lib = lib
@@ -414,3 +418,25 @@ def lookup_conv(levels, coords, radius, packed, bias, out, relu=True):
     with torch.cuda.device(coords.device):
         _check(load().corr_lookup_conv(pp, c, B, H, W, len(levels), radius, pw, bs, int(bool(relu)), o,
                                        _stream(coords)))
+
+
+def lookup_conv_bwd(levels, coords, radius, packed, out, relu, grad_out, grad_weight=None, grad_bias=None,
+                    grad_lookup=None):
+    """corr_lookup_conv_bwd: the fused lookup + conv's backward.  grad_weight [256, C] /
+    grad_bias [256] / grad_lookup [B, C, H, W] (fp32, contiguous; None = not computed) are
+    overwritten."""
+    B, _, H, W = coords.shape
+    lib = load()
+    pp, c = _ptrs(levels, "pyr"), _dev(coords, "coords")
+    g = _dev(grad_out, "grad_out")
+    o = _dev(out, "out") if relu else None
+    opt = lambda t, name: None if t is None else _dev(t, name)
+    ws, nbytes = None, 0
+    if grad_weight is not None or grad_bias is not None:
+        nbytes = lib.corr_lookup_conv_bwd_workspace(B, H, W, len(levels))
+        ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=coords.device)
+    with torch.cuda.device(coords.device):
+        _check(lib.corr_lookup_conv_bwd(pp, c, B, H, W, len(levels), radius, _dev(packed, "packed_weight"), o,
+                                        int(bool(relu)), g, opt(grad_weight, "grad_weight"),
+                                        opt(grad_bias, "grad_bias"), opt(grad_lookup, "grad_lookup"),
+                                        None if ws is None else ws.data_ptr(), nbytes, _stream(coords)))

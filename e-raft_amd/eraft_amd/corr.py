@@ -183,11 +183,11 @@ class _LookupFn(torch.autograd.Function):
 
 class _LookupConvFn(torch.autograd.Function):
     """relu(convc1(lookup(coords))) (update.py:68,75) as one fused kernel in the forward; the
-    324-channel lookup output is never written.  Backward (training, config 4): g = dL/dout
-    zeroed where out <= 0 (ReLU's threshold backward); d bias = sum of g; the lookup is recomputed
-    by the lookup kernel (bit-identical to the forward's values) for dW = g lk^T; the lookup's
-    own gradient W^T g goes into the build's stash, exactly as a plain lookup's backward does,
-    so corr_backward folds it with every other lookup."""
+    324-channel lookup output is never written.  Backward (training, config 4): one
+    corr_lookup_conv_bwd call — ReLU's threshold backward, d bias, dW = g' lk^T with the lookup
+    recomputed on chip (never stored), and the lookup's own gradient W^T g', which goes into the
+    build's stash exactly as a plain lookup's backward does, so corr_backward folds it with every
+    other lookup."""
 
     @staticmethod
     def forward(ctx, coords, token, weight, bias, relu, radius, state):
@@ -203,21 +203,18 @@ class _LookupConvFn(torch.autograd.Function):
     def backward(ctx, grad_out):
         coords, weight, out = ctx.saved_tensors
         st = ctx.state
-        g = grad_out.contiguous()
-        if ctx.relu:  # threshold_backward: zero where out <= 0 (a NaN output passes its gradient, as torch.relu's)
-            g = torch.where(out <= 0, torch.zeros((), dtype=g.dtype, device=g.device), g)
+        g = grad_out.contiguous().float()
         B, O, H, W = g.shape
-        C = weight.shape[1]
-        gf = g.view(B, O, H * W)
-        dbias = gf.sum(dim=(0, 2)) if ctx.needs_input_grad[3] else None
-        dW = None
-        if ctx.needs_input_grad[2]:
-            lk = torch.empty((B, C, H, W), dtype=torch.float32, device=coords.device)
-            _lib.lookup(st.levels, coords, ctx.radius, lk)
-            dW = torch.bmm(gf, lk.view(B, C, H * W).transpose(1, 2)).sum(0).view_as(weight)
-        if st.trains:  # the lookup's upstream gradient, for the build's backward
-            dlk = torch.matmul(weight.view(O, C).t(), gf).view(B, C, H, W)
+        C = len(st.levels) * (2 * ctx.radius + 1) ** 2
+        dev = coords.device
+        dW = torch.empty((O, C), dtype=torch.float32, device=dev) if ctx.needs_input_grad[2] else None
+        dbias = torch.empty((O,), dtype=torch.float32, device=dev) if ctx.needs_input_grad[3] else None
+        dlk = torch.empty((B, C, H, W), dtype=torch.float32, device=dev) if st.trains else None
+        _lib.lookup_conv_bwd(st.levels, coords, ctx.radius, _weight_pack(weight), out, ctx.relu, g, dW, dbias, dlk)
+        if dlk is not None:  # the lookup's upstream gradient, for the build's backward
             _LookupFn.stash_backward(st, coords, dlk, ctx.radius)
+        if dW is not None:
+            dW = dW.view_as(weight).to(weight.dtype)
         return None, None, dW, dbias, None, None, None
 
 

@@ -41,7 +41,9 @@ extern "C" {
  *   101: first ABI.
  *   102: corr_lookup_conv's weight argument is the opaque buffer written by
  *        corr_lookup_conv_weights (it was an fp32 [L*K][256] transpose under 101); callers
- *        built against 101 must check this version before calling it. */
+ *        built against 101 must check this version before calling it.
+ *   103: CORR_BUILD_BF16X6, corr_build_region, corr_lookup_conv_bwd (the packed weight buffer
+ *        grew: size it with corr_lookup_conv_weights_bytes()). */
 int corr_version(void);
 
 /* Thread-local description of the last error on this thread ("" if none). */
@@ -242,15 +244,34 @@ size_t corr_forward_splat_workspace(int B, int H, int W);
  * the build's f16x3 contract).  The weight (convc1.weight viewed [256][L*K], fp32) is split once
  * per weight version by corr_lookup_conv_weights into a corr_lookup_conv_weights_bytes() buffer;
  * out [B][256][H][W].  radius 4, levels <= 4 (E-RAFT); CORR_EUNSUPPORTED otherwise.  This call
- * is the forward only; its training backward is composed from the other entry points (the
- * Python side's _LookupConvFn: corr_lookup_conv_bwd for dW / bias and the lookup's gradient
- * W^T g into corr_backward's lookup list).
+ * is the forward; corr_lookup_conv_bwd below is its training backward.
  */
 size_t corr_lookup_conv_weights_bytes(void);
 int corr_lookup_conv_weights(const float *weight, int out_channels, int in_channels, void *packed, void *stream);
 int corr_lookup_conv(const float *const *pyr, const float *coords, int B, int H, int W,
                      int levels, int radius, const void *packed_weight, const float *bias, int relu,
                      float *out, void *stream);
+
+/*
+ * Training backward of corr_lookup_conv (autograd of update.py:68,75 through corr.py:29-50).
+ * grad_out = dL/d out [B][256][H][W]; with relu, g' = grad_out where out > 0 (or out is NaN),
+ * else 0 (torch's threshold backward; `out` is the forward's output, unused without relu).
+ *   grad_weight [256][levels*K] = sum_{b,n} g'[b][o][n] lookup[b][c][n]    (OVERWRITTEN)
+ *   grad_bias   [256]           = sum_{b,n} g'[b][o][n]                    (OVERWRITTEN)
+ *   grad_lookup [B][levels*K][H][W] = sum_o weight[o][c] g'[b][o][n]  — the lookup's upstream
+ *               gradient, to be passed to corr_backward / corr_lookup_bwd like a plain lookup's
+ * Any of the three may be NULL (not computed).  The lookup is recomputed on chip (bit-identical
+ * to corr_lookup's values) and never written.  Both products run on the bf16 MFMA with the
+ * exact three-piece split of CORR_BUILD_BF16X6 (six products per fp32 product, no scales);
+ * dW and the bias sum per-workgroup partials in a fixed order (deterministic).  packed_weight
+ * from corr_lookup_conv_weights; workspace of corr_lookup_conv_bwd_workspace(B, H, W, levels)
+ * bytes (16-B aligned) when grad_weight or grad_bias is requested.  radius 4, levels <= 4.
+ */
+size_t corr_lookup_conv_bwd_workspace(int B, int H, int W, int levels);
+int corr_lookup_conv_bwd(const float *const *pyr, const float *coords, int B, int H, int W, int levels, int radius,
+                         const void *packed_weight, const float *out, int relu, const float *grad_out,
+                         float *grad_weight, float *grad_bias, float *grad_lookup, void *workspace,
+                         size_t workspace_bytes, void *stream);
 
 /*
  * DSEC event -> voxel grid.  Replaces VoxelGrid.convert (utils/dsec_utils.py:26-64) as the DSEC

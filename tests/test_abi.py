@@ -35,7 +35,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 
 def test_version_and_workspace(lib):
-    assert lib.corr_version() == 102
+    assert lib.corr_version() == 103
     # DSEC: 256 x 4800 slabs; at least one slab, deterministic plan
     ws = lib.corr_build_bwd_workspace(1, 256, 60, 80)
     assert ws >= 256 * 4800 * 4 and ws % (256 * 4800 * 4) == 0
@@ -163,3 +163,20 @@ def test_lookup_conv_validation(lib):
     pyr = (ctypes.c_void_p * 4)(16, 16, 16, 16)
     rc = lib.corr_lookup_conv(pyr, 16, 1, 60, 80, 4, 3, 16, 16, 1, 16, None)  # radius 3
     assert rc != 0 and "radius 4" in lib.corr_last_error().decode()
+
+
+def test_lookup_conv_bwd_validation(lib):
+    """corr_lookup_conv_bwd rejects what it cannot run before touching the GPU: radius != 4,
+    a missing `out` under ReLU, a short workspace for dW / bias; with no output requested it is
+    a no-op (no workspace needed)."""
+    pyr = (ctypes.c_void_p * 4)(16, 16, 16, 16)
+    ws_need = lib.corr_lookup_conv_bwd_workspace(8, 36, 48, 4)
+    assert ws_need >= 64 * 256 * 324 * 4
+    rc = lib.corr_lookup_conv_bwd(pyr, 16, 1, 60, 80, 4, 3, 16, 16, 1, 16, 16, 16, 16, 16, ws_need, None)
+    assert rc == -2 and "radius 4" in lib.corr_last_error().decode()
+    rc = lib.corr_lookup_conv_bwd(pyr, 16, 1, 60, 80, 4, 4, 16, None, 1, 16, 16, 16, 16, 16, ws_need, None)
+    assert rc == -1 and "out" in lib.corr_last_error().decode()
+    rc = lib.corr_lookup_conv_bwd(pyr, 16, 8, 36, 48, 4, 4, 16, 16, 1, 16, 16, None, None, 16, ws_need - 4, None)
+    assert rc == -1 and "workspace" in lib.corr_last_error().decode()
+    rc = lib.corr_lookup_conv_bwd(pyr, 16, 8, 36, 48, 4, 4, 16, 16, 1, 16, None, None, None, None, 0, None)
+    assert rc == 0

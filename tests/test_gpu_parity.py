@@ -876,6 +876,58 @@ def test_lookup_conv_autograd_matches_unfused():
         assert norm_rel(a, ref) <= REL_TOL, (name, norm_rel(a, ref))
 
 
+@pytest.mark.parametrize("B,H,W,L,relu", [(2, 17, 23, 3, True), (1, 16, 20, 4, False), (8, 36, 48, 4, True)])
+def test_lookup_conv_bwd_vs_fp64(B, H, W, L, relu):
+    """corr_lookup_conv_bwd (lookup recomputed on chip, bf16x6 products) vs the float64
+    composition from the bit-exact HIP lookup: g' = where(out <= 0, 0, g); d bias = sum g';
+    dW = g' lk^T; d lk = W^T g'.  Each element within 2^-20 of its sum of |products| (the
+    bf16x6 contract is ~2^-23 per product plus fp32 accumulation); partial 32-query blocks
+    (17 x 23), 3 levels, no ReLU, config 4's shape (64 query ranges); bit-identical on a rerun
+    and with any subset of the outputs requested."""
+    import torch.nn.functional as F
+    from eraft_amd import _lib
+    from eraft_amd.corr import _weight_pack
+    D, r = 32, 4
+    K = (2 * r + 1) ** 2
+    C = L * K
+    f1, f2 = prng.gauss(131, (B, D, H, W)), prng.gauss(132, (B, D, H, W))
+    cb = _cb()(torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV), num_levels=L, radius=r)
+    c = torch.from_numpy(prng.lookup_coords(133, B, H, W, 3.0)).to(DEV)
+    w = torch.from_numpy(prng.gauss(134, (256, C, 1, 1), 0.05)).to(DEV)
+    bias = torch.from_numpy(prng.gauss(135, (256,), 0.1)).to(DEV)
+    g = torch.from_numpy(prng.gauss(136, (B, 256, H, W))).to(DEV)
+    out = cb.lookup_conv(c, w, bias, relu=relu)
+    lk = cb(c).double().cpu().reshape(B, C, H * W)
+    gd = g.double().cpu()
+    if relu:
+        gd = torch.where(out.cpu() <= 0, torch.zeros((), dtype=torch.float64), gd)
+    gd = gd.reshape(B, 256, H * W)
+    wd = w.double().cpu().reshape(256, C)
+    ref_b = gd.sum(dim=(0, 2))
+    ref_w = torch.einsum("bon,bcn->oc", gd, lk)
+    mag_w = torch.einsum("bon,bcn->oc", gd.abs(), lk.abs())
+    ref_l = torch.einsum("oc,bon->bcn", wd, gd)
+    mag_l = torch.einsum("oc,bon->bcn", wd.abs(), gd.abs())
+
+    def run(want_w=True, want_b=True, want_l=True):
+        dW = torch.empty((256, C), device=DEV) if want_w else None
+        db = torch.empty((256,), device=DEV) if want_b else None
+        dl = torch.empty((B, C, H, W), device=DEV) if want_l else None
+        _lib.lookup_conv_bwd(cb._state.levels, c, r, _weight_pack(w), out, relu, g, dW, db, dl)
+        return [None if t is None else t.cpu() for t in (dW, db, dl)]
+
+    dW, db, dl = run()
+    tol = 2.0 ** -20
+    assert ((dW.double() - ref_w).abs() <= tol * mag_w + 1e-30).all()
+    assert ((db.double() - ref_b).abs() <= tol * gd.abs().sum(dim=(0, 2)) + 1e-30).all()
+    assert ((dl.double().reshape(B, C, H * W) - ref_l).abs() <= tol * mag_l + 1e-30).all()
+    again = run()
+    assert all(torch.equal(a, b) for a, b in zip((dW, db, dl), again))
+    only_w, _, _ = run(True, False, False)
+    _, _, only_l = run(False, False, True)
+    assert torch.equal(only_w, dW) and torch.equal(only_l, dl)
+
+
 def test_lookup_conv_weight_pack_not_aliased():
     """The packed convc1 split is cached per weight tensor: a second weight that reuses the
     first one's allocation (same data_ptr, same _version) must not see the first one's pack.

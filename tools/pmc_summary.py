@@ -11,7 +11,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("bf16_pack_kernel", "corr_build_bf16_kernel", "lookup_bwd_fold_kernel", "pool_fold_max_kernel", "rowmax2_kernel", "corr_build_split_kernel", "corr_build_split_ring_kernel", "split_pack_reg_kernel", "split_pack_wide_kernel", "split_pack_kernel",
+KERNELS = ("lookup_conv_bwd_dw_kernel", "lookup_conv_bwd_dlk_kernel", "lookup_conv_bwd_reduce_kernel", "lookup_conv_kernel", "bf16_pack_kernel", "corr_build_bf16_kernel", "lookup_bwd_fold_kernel", "pool_fold_max_kernel", "rowmax2_kernel", "corr_build_split_kernel", "corr_build_split_ring_kernel", "split_pack_reg_kernel", "split_pack_wide_kernel", "split_pack_kernel",
            "corr_build_kernel", "lookup_bwd_kernel", "lookup_kernel", "split_gemm_kernel", "gemm_kernel",
            "splitk_reduce_kernel", "pool_bwd_kernel", "pool2x2_kernel", "split_convert_rows_kernel",
            "split_convert_cols_kernel", "absmax_kernel", "split_gemm_f32_kernel", "colmax_reduce_kernel")
