@@ -1225,7 +1225,9 @@ __device__ __forceinline__ int xcd_contiguous(int bid, int n) {
 // groups use a bpermute.
 template <int SLOTS>
 __device__ __forceinline__ float lane_prev(float x, int cx) {
-    if constexpr (SLOTS <= 16) {
+    if constexpr (SLOTS == 16) {  // the group is the DPP row: its lane 0 (cx = 0) reads the 0
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x111, 0xF, 0xF, true));
+    } else if constexpr (SLOTS < 16) {
         const int y = __builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x111, 0xF, 0xF, true);
         return cx == 0 ? 0.f : __int_as_float(y);
     } else {
@@ -1308,29 +1310,37 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     if (tid < BQ) RM[tid] = 0u;
     __syncthreads();
 
-    // the next lookup's coords and upstream gradients are loaded one lookup ahead (registers).
-    // Every lane loads (clamped, always-valid addresses) and non-loaders drop the values at use:
-    // no branch around the loads, so no copy at a control-flow join makes the compiler wait.
+    // the next lookup's coords and upstream gradients are loaded one lookup ahead (registers),
+    // by buffer loads over batch item b's slice: every lane loads, and the lanes that own no
+    // (tap, query) point past the slice, so the range check returns their zeros (no branch
+    // around the loads, no select at use, 32-bit offsets).
     const bool loader = act && cx < S && qok;
-    const int cxl = min(cx, S - 1), nl = min(n, NQ - 1);
+    const int cxl = min(cx, S - 1);
+    constexpr uint32_t kOob = 0x80000000u;
+    const uint32_t coff = loader ? (uint32_t)n * 4u : kOob;
+    const uint32_t goff = loader ? (uint32_t)(((lc * K + cx * S) * NQ + n) * 4) : kOob;
     float pcx, pcy, pv[S];
     auto prefetch = [&](int t) {
         const float *coords, *grad_out;
         kernarg_lookup(t, coords, grad_out);
-        pcx = coords[((size_t)b * 2 + 0) * NQ + nl];
-        pcy = coords[((size_t)b * 2 + 1) * NQ + nl];
-        const float *g = grad_out + (((size_t)b * L + lc) * K + (size_t)cxl * S) * NQ + nl;
+        const auto rc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(coords + (size_t)b * 2 * NQ), 0,
+                                                          2 * NQ * 4, 0x00020000);
+        const auto rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(grad_out + (size_t)b * L * K * NQ), 0,
+                                                          L * K * NQ * 4, 0x00020000);
+        pcx = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, coff, 0, 0));
+        pcy = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rc, coff, NQ * 4, 0));
 #pragma unroll
-        for (int u = 0; u < S; ++u) pv[u] = g[(size_t)u * NQ];
+        for (int u = 0; u < S; ++u)
+            pv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, goff, u * NQ * 4, 0));
     };
     if (act) prefetch(0);
 
     for (int t = 0; !(PROBE & 1) && act && t < lk.T; ++t) {  // absent levels (l >= L) only join the fold
         // ---- 1. tap cx of both axes; the group's taps reach the other lanes by DPP ----
-        const float cxv = loader ? pcx : 0.0f, cyv = loader ? pcy : 0.0f;
+        const float cxv = pcx, cyv = pcy;  // 0 for the lanes without a (tap, query)
         float v[S];
 #pragma unroll
-        for (int u = 0; u < S; ++u) v[u] = loader ? pv[u] : 0.0f;
+        for (int u = 0; u < S; ++u) v[u] = pv[u];
         prefetch(min(t + 1, lk.T - 1));
         const Axis a = tap_axis(cxv, inv_scale, cxl, R, Wl);
         const Axis c = tap_axis(cyv, inv_scale, cxl, R, Hl);

@@ -6,6 +6,7 @@
 #   bench:<args>  bench.py with args (commas -> spaces)
 set -o pipefail
 TAG=${1:-a}; shift || true
+NB=0
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for STEP in "$@"; do
@@ -19,9 +20,9 @@ for STEP in "$@"; do
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/tests_${TAG}.txt 2>&1; rc=$?
       tail -15 gpurun_out/tests_${TAG}.txt; [ $rc -eq 0 ] || exit 5 ;;
-    bench:*) A=${STEP#bench:}; A=${A//,/ }
-      timeout -k 10 300 python -u bench.py $A > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err; rc=$?
-      tail -c 3000 gpurun_out/bench_${TAG}.json; [ $rc -eq 0 ] || { tail -20 gpurun_out/bench_${TAG}.err; exit 6; } ;;
+    bench:*) A=${STEP#bench:}; A=${A//,/ }; NB=$((NB+1)); OUT=gpurun_out/bench_${TAG}_$NB
+      timeout -k 10 300 python -u bench.py $A > $OUT.json 2> $OUT.err; rc=$?
+      tail -c 1500 $OUT.json; echo; [ $rc -eq 0 ] || { tail -20 $OUT.err; exit 6; } ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
 done
