@@ -1240,8 +1240,8 @@ __device__ __forceinline__ float lane_prev(float x, int cx) {
 // VALU move, no LDS); other group sizes use a bpermute.
 template <int SLOTS, int J>
 __device__ __forceinline__ float group_lane(float x, int lane) {
-    if constexpr (SLOTS == 16) {
-        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x150 + J, 0xF, 0xF, false));
+    if constexpr (SLOTS == 16) {  // every lane is written: no old value to initialise
+        return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x150 + J, 0xF, 0xF, false));
     } else {
         return __shfl(x, (lane & ~(SLOTS - 1)) + J, 64);
     }
@@ -1399,21 +1399,29 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
                 const f32x2 yhi = f32x2{yv(2, cy - 1), yv(2, cy)}, ylo = f32x2{yv(1, cy), yv(1, cy + 1)};
                 const f32x2 gpm = f32x2{gpv(cy - 1), gpv(cy)}, gp0 = f32x2{gpv(cy), gpv(cy + 1)};
                 const f32x2 gcm = f32x2{gcv(cy - 1), gcv(cy)}, gc0 = f32x2{gcv(cy), gcv(cy + 1)};
-                f32x2 acc = f32x2{0.f, 0.f} + gpm * (yhi * WH);  // se
+                // se first.  The reference's cell starts at +0 (0 + se): starting at se differs
+                // only when every term is -0, giving -0 instead of +0 — and the map value it is
+                // added to is never -0 (it starts at +0 and no round-to-nearest sum of it is -0),
+                // so old + sv is the same bits either way.
+                f32x2 acc = gpm * (yhi * WH);
                 acc = acc + gp0 * (ylo * WH);                    // ne
                 acc = acc + gcm * (yhi * WL);                    // sw
                 acc = acc + gc0 * (ylo * WL);                    // nw
                 sv[cy] = acc.x;
                 sv[cy + 1] = acc.y;
             }
+            // byte addresses of the column's cells: one compare, one add and one select per cell
+            const int ayc = cx < C ? ayv : -(1 << 30);
+            const unsigned rb = 4u * (unsigned)rowbase, stride = 4u * (unsigned)Wl, db = 4u * (unsigned)dump;
+            char *const lds = reinterpret_cast<char *>(fsm);
             float old[C];
-            int at[C];
+            unsigned at[C];
 #pragma unroll
-            for (int cy = 0; cy < C; ++cy) at[cy] = cx < C ? cell_at(cy) : dump;
+            for (int cy = 0; cy < C; ++cy) at[cy] = (unsigned)(ayc + cy) < (unsigned)Hl ? rb + cy * stride : db;
 #pragma unroll
-            for (int cy = 0; cy < C; ++cy) old[cy] = fsm[at[cy]];  // all reads, then all writes
+            for (int cy = 0; cy < C; ++cy) old[cy] = *reinterpret_cast<float *>(lds + at[cy]);  // all reads, then all writes
 #pragma unroll
-            for (int cy = 0; cy < C; ++cy) fsm[at[cy]] = old[cy] + sv[cy];
+            for (int cy = 0; cy < C; ++cy) *reinterpret_cast<float *>(lds + at[cy]) = old[cy] + sv[cy];
         } else {
             float dy[S];
 #pragma unroll
