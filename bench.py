@@ -685,8 +685,10 @@ def main():
                                    f"{' + autograd backward to both fmaps' if train else ''}, {wl_name} "
                                    f"fmaps [{B},{D},{H},{W}], {L} levels, radius {r}",
                        "global_batch": B * (1 if sharded else world), "launch": launch,
-                       "parallelism": (f"row-sharded x{world} (query rows of one pair per GPU, "
-                                       "fmap2 RCCL broadcast overlapped with the previous pair)") if sharded else
+                       "parallelism": (f"row-sharded x{world} (query rows of one pair per GPU, fmap2 broadcast "
+                                       + ("double-buffered: pair k+1's during pair k)" if prefetch else
+                                          f"in {args.chunks} target-row chunks, each chunk's build on arrival)"))
+                       if sharded else
                                       f"replicas x{world} (independent frame pairs per GPU)"},
             "build_algo": BUILD_ALGO[algo],
             "build_arith": BUILD_ARITH[algo],
