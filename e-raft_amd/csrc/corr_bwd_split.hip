@@ -382,11 +382,12 @@ __device__ __forceinline__ void gemm_wait_vm_barrier() {
 
 // Dynamic LDS of the GEMM: the hi/lo staging (2 stages; DMA: 1), the row exponents, and (DMA)
 // a 2-slot ring of raw fp32 chunks (kTI + kTJ rows x 16 k; BCOL: B as 16 k-rows x 256 columns).
-template <bool DMA, int WI = kWI>
+// PIPE (DMA path): a 3-slot raw ring, so chunk k + 1 can be split while chunk k's MFMAs run.
+template <bool DMA, int WI = kWI, bool PIPE = false>
 constexpr int gemm_lds_bytes() {
     constexpr int rows = 32 * kMI * WI + kTJ;
     return (DMA ? 1 : 2) * rows * 4 * (int)sizeof(u32x4) + rows * (int)sizeof(int) +
-           (DMA ? 2 * rows * kBK * (int)sizeof(float) : 0);
+           (DMA ? (PIPE ? 3 : 2) * rows * kBK * (int)sizeof(float) : 0);
 }
 
 // DMA = true: the raw fp32 chunks arrive by LDS-DMA two chunks ahead (no register staging, so a
@@ -403,7 +404,7 @@ __device__ __forceinline__ unsigned split_lo_mix(unsigned h2, float y0, float y1
     return lo;
 }
 
-template <bool BCOL, bool DMA = false, int WI = kWI>
+template <bool BCOL, bool DMA = false, int WI = kWI, bool PIPE = false>
 __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmParams p) {
     // WI = 4 (DMA path only): 8 waves, a 256 x 256 tile (each wave still 64 x 128), so every
     // staged element feeds twice the MFMAs
@@ -516,11 +517,15 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
             for (int t = 0; t < 16; ++t) rb[t] = k0 + t < p.K ? q[(size_t)t * p.b_sk] : 0.f;
         }
     };
-    auto store_chunk = [&](int st, const float (&ra)[8], const float (&rb)[16]) {
+    using FM0 = std::integral_constant<int, 0>;
+    // FM: 0 = the runtime `fast` choice, 1 = fast split only, 2 = exact split2 only (the pipelined
+    // loop runs one branch-free copy per case, so its MFMAs can be scheduled among the split)
+    auto store_chunk = [&](int st, const float (&ra)[8], const float (&rb)[16], auto fm_tag) {
+        constexpr int FM = decltype(fm_tag)::value;
         u32x4 *S = lds + (size_t)st * ROWS * 4;
         auto split8 = [&](const float *v, int sh, bool guard, float f, u32x4 &hi, u32x4 &lo) {
             half2v h[4], l[4];
-            if (fast) {
+            if (FM == 1 || (FM == 0 && fast)) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     const f32x2v y = f32x2v{v[2 * t], v[2 * t + 1]} * f32x2v{f, f};
@@ -597,6 +602,7 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
             for (int n = 0; n < kNJ; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh[n], acc[m][n], 0, 0, 0);
     };
     if constexpr (DMA) {
+        constexpr int NSLOT = PIPE ? 3 : 2;
         const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
         const uint32_t raw_base = (uint32_t)(uintptr_t)(gemm_lds_t *)raw;
         // this wave's pieces of a chunk: A rows 16 (2w + q) + lane / 4, 16-B piece lane % 4;
@@ -644,49 +650,126 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
                 for (int t = 0; t < 8 * KO; ++t) rb0[t] = RB[(8 * boct0 + t) * kTJ + bcol];
             }
         };
-        if (kc0 < kc1) issue(kc0, 0);
-        if (kc0 + 1 < kc1) issue(kc0 + 1, 1);
-        for (int kc = kc0; kc < kc1; ++kc) {
-            const int slot = (kc - kc0) & 1;
-            if (kc + 1 < kc1) gemm_wait_vm_barrier<2 + PB>();  // chunk kc landed (every wave's pieces)
-            else gemm_wait_vm_barrier<0>();
-            read_raw(slot);
-            store_chunk(0, ra0, rb0);
-            __syncthreads();  // staging complete, ring slot read
-            if (kc + 2 < kc1) issue(kc + 2, slot);
-            mfma_chunk(0);
+        if constexpr (!PIPE) {
+            if (kc0 < kc1) issue(kc0, 0);
+            if (kc0 + 1 < kc1) issue(kc0 + 1, 1);
+            for (int kc = kc0; kc < kc1; ++kc) {
+                const int slot = (kc - kc0) & 1;
+                if (kc + 1 < kc1) gemm_wait_vm_barrier<2 + PB>();  // chunk kc landed (every wave's pieces)
+                else gemm_wait_vm_barrier<0>();
+                read_raw(slot);
+                store_chunk(0, ra0, rb0, FM0{});
+                __syncthreads();  // staging complete, ring slot read
+                if (kc + 2 < kc1) issue(kc + 2, slot);
+                mfma_chunk(0);
+            }
+        } else {
+            // Chunk c's raw fp32 pieces go to ring slot (c - kc0) % 3, issued three chunks ahead.
+            // Iteration kc: read chunk kc's fragments from the staging into registers; barrier
+            // (every wave has read them, chunk kc + 1's pieces have landed); then chunk kc + 1's
+            // split into the staging and chunk kc's MFMAs (from registers) in one region, so the
+            // split's VALU and LDS stores overlap the MFMA pipe within each wave; barrier; issue
+            // chunk kc + 4 into the freed slot.  Same splits, same MFMA order: the same bits.
+            constexpr int G = 2 + PB;  // DMA pieces per wave and chunk
+            auto wait_groups = [&](int n) __attribute__((always_inline)) {  // <= n chunks still in flight
+                if (n >= 2) wait_vmcnt_barrier<2 * G>();
+                else if (n == 1) wait_vmcnt_barrier<G>();
+                else wait_vmcnt_barrier<0>();
+            };
+            for (int c = 0; c < 3; ++c)
+                if (kc0 + c < kc1) issue(kc0 + c, c);
+            if (kc0 < kc1) {
+                wait_groups(min(kc1, kc0 + 3) - kc0 - 1);
+                read_raw(0);
+                store_chunk(0, ra0, rb0, FM0{});
+                __syncthreads();
+                if (kc0 + 3 < kc1) issue(kc0 + 3, 0);
+            }
+            auto frags = [&](half8 (&ah)[kMI], half8 (&al)[kMI], half8 (&bh)[kNJ], half8 (&bl)[kNJ])
+                             __attribute__((always_inline)) {
+                const u32x4 *S = lds;
+#pragma unroll
+                for (int m = 0; m < kMI; ++m) {
+                    ah[m] = __builtin_bit_cast(half8, S[swz(arow0 + 32 * m, 2 * h)]);
+                    al[m] = __builtin_bit_cast(half8, S[swz(arow0 + 32 * m, 2 * h + 1)]);
+                }
+#pragma unroll
+                for (int n = 0; n < kNJ; ++n) {
+                    bh[n] = __builtin_bit_cast(half8, S[swz(brow0 + 32 * n, 2 * h)]);
+                    bl[n] = __builtin_bit_cast(half8, S[swz(brow0 + 32 * n, 2 * h + 1)]);
+                }
+            };
+            auto mfmas = [&](const half8 (&ah)[kMI], const half8 (&al)[kMI], const half8 (&bh)[kNJ],
+                             const half8 (&bl)[kNJ]) __attribute__((always_inline)) {
+#pragma unroll
+                for (int m = 0; m < kMI; ++m)
+#pragma unroll
+                    for (int n = 0; n < kNJ; ++n)
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bh[n], acc[m][n], 0, 0, 0);
+#pragma unroll
+                for (int m = 0; m < kMI; ++m)
+#pragma unroll
+                    for (int n = 0; n < kNJ; ++n)
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bl[n], acc[m][n], 0, 0, 0);
+#pragma unroll
+                for (int m = 0; m < kMI; ++m)
+#pragma unroll
+                    for (int n = 0; n < kNJ; ++n)
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh[n], acc[m][n], 0, 0, 0);
+            };
+            // every iteration but the last: chunk kc + 1 is split (branch-free, one copy per split
+            // mode) in the same region as chunk kc's MFMAs
+            auto body = [&](auto fm_tag) __attribute__((always_inline)) {
+                for (int kc = kc0; kc + 1 < kc1; ++kc) {
+                    half8 ah[kMI], al[kMI], bh[kNJ], bl[kNJ];
+                    frags(ah, al, bh, bl);
+                    wait_groups(min(kc1, kc + 4) - kc - 2);  // chunk kc + 1 landed; fragments read
+                    read_raw((kc + 1 - kc0) % 3);
+                    store_chunk(0, ra0, rb0, fm_tag);
+                    mfmas(ah, al, bh, bl);
+                    __syncthreads();  // chunk kc + 1 staged; its ring slot read by every wave
+                    if (kc + 4 < kc1) issue(kc + 4, (kc + 1 - kc0) % 3);
+                }
+            };
+            if (fast) body(std::integral_constant<int, 1>{});
+            else body(std::integral_constant<int, 2>{});
+            if (kc0 < kc1) {  // the last chunk
+                half8 ah[kMI], al[kMI], bh[kNJ], bl[kNJ];
+                frags(ah, al, bh, bl);
+                mfmas(ah, al, bh, bl);
+            }
         }
     } else if constexpr (!BCOL) {  // row operands: one set (two would spill at 256 VGPRs)
         if (kc0 < kc1) {
             load_chunk(kc0, ra0, rb0);
-            store_chunk(0, ra0, rb0);
+            store_chunk(0, ra0, rb0, FM0{});
         }
         __syncthreads();
         for (int kc = kc0; kc < kc1; ++kc) {
             const int st = (kc - kc0) & 1;
             if (kc + 1 < kc1) load_chunk(kc + 1, ra0, rb0);
             mfma_chunk(st);
-            if (kc + 1 < kc1) store_chunk(st ^ 1, ra0, rb0);
+            if (kc + 1 < kc1) store_chunk(st ^ 1, ra0, rb0, FM0{});
             __syncthreads();
         }
     } else {
     if (kc0 < kc1) {
         load_chunk(kc0, ra0, rb0);
         if (kc0 + 1 < kc1) load_chunk(kc0 + 1, ra1, rb1);
-        store_chunk(0, ra0, rb0);
+        store_chunk(0, ra0, rb0, FM0{});
     }
     __syncthreads();
     for (int kc = kc0; kc < kc1; kc += 2) {
         // even step: chunk kc in stage 0, chunk kc + 1 in set 1, chunk kc + 2 -> set 0
         if (kc + 2 < kc1) load_chunk(kc + 2, ra0, rb0);
         mfma_chunk(0);
-        if (kc + 1 < kc1) store_chunk(1, ra1, rb1);
+        if (kc + 1 < kc1) store_chunk(1, ra1, rb1, FM0{});
         __syncthreads();
         if (kc + 1 >= kc1) break;
         // odd step: chunk kc + 1 in stage 1, chunk kc + 2 in set 0, chunk kc + 3 -> set 1
         if (kc + 3 < kc1) load_chunk(kc + 3, ra1, rb1);
         mfma_chunk(1);
-        if (kc + 2 < kc1) store_chunk(0, ra0, rb0);
+        if (kc + 2 < kc1) store_chunk(0, ra0, rb0, FM0{});
         __syncthreads();
     }
     }
@@ -725,6 +808,7 @@ struct GemmTune {
     bool dma = true;         // LDS-DMA operand ring when the shape allows
     bool wide = true;        // 256 x 256 tiles of 8 waves on the DMA path when NI > 128
     bool reduce_vec4 = true; // the 16-B split-K reduce when aligned
+    bool pipe = true;        // wide DMA path: split chunk k + 1 under chunk k's MFMAs (3-slot ring)
 };
 
 int plan_split_k(int NI, int NJ, int nkc, int batch, const GemmTune &t = GemmTune{}) {
@@ -827,24 +911,27 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     // the MFMAs, a third less split work per MFMA (train: dF1 73 -> 67, dF2 75 -> 67 us)
     const bool wide = dma && t.wide && NI > 32 * kMI * kWI;
     hipError_t e;
-    auto go = [&](auto dma_tag, auto wi_tag) {
+    auto go = [&](auto dma_tag, auto wi_tag, auto pipe_tag) {
         constexpr bool D = decltype(dma_tag)::value;
         constexpr int WI = decltype(wi_tag)::value;
+        constexpr bool P = decltype(pipe_tag)::value;
         FGemmParams q = p;
         q.ti = (NI + 32 * kMI * WI - 1) / (32 * kMI * WI);
         const long grid = (long)q.ti * q.tj * q.splits * B;
         static std::atomic<unsigned long long> done{0};
-        hipError_t e2 = ensure_lds_limit((const void *)split_gemm_f32_kernel<BCOL, D, WI>, gemm_lds_bytes<D, WI>(), done);
+        hipError_t e2 = ensure_lds_limit((const void *)split_gemm_f32_kernel<BCOL, D, WI, P>,
+                                         gemm_lds_bytes<D, WI, P>(), done);
         if (e2 != hipSuccess) return e2;
-        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, D, WI>), dim3((unsigned)grid), dim3(64 * WI * kWJ),
-                           (gemm_lds_bytes<D, WI>()), s, q);
+        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, D, WI, P>), dim3((unsigned)grid), dim3(64 * WI * kWJ),
+                           (gemm_lds_bytes<D, WI, P>()), s, q);
         return hipSuccess;
     };
     using T_ = std::true_type;
     using F_ = std::false_type;
     using W2 = std::integral_constant<int, kWI>;
     using W4 = std::integral_constant<int, 4>;
-    e = wide ? go(T_{}, W4{}) : dma ? go(T_{}, W2{}) : go(F_{}, W2{});
+    e = wide ? (t.pipe ? go(T_{}, W4{}, T_{}) : go(T_{}, W4{}, F_{})) : dma ? go(T_{}, W2{}, F_{})
+                                                                           : go(F_{}, W2{}, F_{});
     if (e != hipSuccess) return e;
     e = hipGetLastError();
     if (e != hipSuccess || p.direct) return e;

@@ -86,10 +86,12 @@ int main(int argc, char **argv) {
         std::vector<float> us;
     };
     std::vector<V> vs;
-    for (int wide : {0, 1}) {
-        const std::string tag = std::string("DMA mix splits plan, ") + (wide ? "256x256 tiles (8 waves)" : "128x256 tiles");
+    for (int cfg : {0, 1, 2}) {  // 128x256; 256x256; 256x256 with the split under the MFMAs
+        const std::string tag = std::string("DMA mix splits plan, ") +
+                                (cfg == 0 ? "128x256 tiles" : cfg == 1 ? "256x256 tiles (8 waves)" : "256x256 pipelined");
         GemmTune t;
-        t.wide = wide;
+        t.wide = cfg >= 1;
+        t.pipe = cfg == 2;
         vs.push_back({"dF1 (rows) " + tag, [&, t] { return g1(o1, t); }, o1, r1, {}});
         vs.push_back({"dF2 (cols) " + tag, [&, t] { return g2(o2, t); }, o2, r2, {}});
     }
