@@ -876,7 +876,8 @@ def test_lookup_conv_autograd_matches_unfused():
         assert norm_rel(a, ref) <= REL_TOL, (name, norm_rel(a, ref))
 
 
-@pytest.mark.parametrize("B,H,W,L,relu", [(2, 17, 23, 3, True), (1, 16, 20, 4, False), (8, 36, 48, 4, True)])
+@pytest.mark.parametrize("B,H,W,L,relu", [(2, 17, 23, 3, True), (1, 16, 20, 4, False), (8, 36, 48, 4, True),
+                                          (1, 8, 12, 3, True)])  # 3 blocks < 8 query ranges: empty ranges
 def test_lookup_conv_bwd_vs_fp64(B, H, W, L, relu):
     """corr_lookup_conv_bwd (lookup recomputed on chip, bf16x6 products) vs the float64
     composition from the bit-exact HIP lookup: g' = where(out <= 0, 0, g); d bias = sum g';
