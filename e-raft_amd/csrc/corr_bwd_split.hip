@@ -602,7 +602,6 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
             for (int n = 0; n < kNJ; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh[n], acc[m][n], 0, 0, 0);
     };
     if constexpr (DMA) {
-        constexpr int NSLOT = PIPE ? 3 : 2;
         const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
         const uint32_t raw_base = (uint32_t)(uintptr_t)(gemm_lds_t *)raw;
         // this wave's pieces of a chunk: A rows 16 (2w + q) + lane / 4, 16-B piece lane % 4;

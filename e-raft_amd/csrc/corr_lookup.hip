@@ -341,73 +341,55 @@ __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
 }
 
 // Lookup fused with the consumer's 1x1 convolution (BasicMotionEncoder.convc1, update.py:68,75:
-// cor = relu(convc1(corr)), L*K = 324 -> 256 channels), on the f16 MFMA pipe with the same
-// fp32-accurate split as the build: x = 2^-s (hi + lo), products lo.hi + hi.lo + hi.hi into an
-// fp32 accumulator.  A workgroup owns 32 queries: two groups of 5 waves look them up, two levels
-// at a time (lookup_block, bit-identical values), into an LDS tile ct[L*K][32]; each query's
-// 324 values get a power-of-two scale from their max and are split into f16 hi/lo rows; 8 waves
-// then multiply by the pre-split weight (corr_lookup_conv_weights: per output channel scale,
-// hi/lo in the 16x16x32 MFMA A-fragment order, streamed from L2) and write
-// relu(2^-(s_o + s_q) acc + bias) as [B][O][NQ].  The 324-channel lookup output never reaches
+// cor = relu(convc1(corr)), L*K = 324 -> 256 channels), on the bf16 MFMA with the build's exact
+// three-piece split (x = hi + mid + lo, six products per fp32 product, smallest first: no
+// narrower than fp32, no scales).  A workgroup owns 32 queries: two groups of 5 waves look them
+// up, two levels at a time (lookup_block, bit-identical values), into an LDS tile ct[L*K][32];
+// the tile is split into bf16 pieces [piece][q][k] (aliasing the lookup staging); 8 waves then
+// multiply by the pre-split weight (corr_lookup_conv_weights: W's pieces in the 16x16x32 MFMA
+// A-fragment order, streamed from L2 one K step ahead) into two accumulators (hi*hi; the rest)
+// and write relu(acc + acs + bias) as [B][O][NQ].  The 324-channel lookup output never reaches
 // HBM.  r = 4, L <= 4, O = 256.
-constexpr int kLcQB = 32, kLcO = 256, kLcKC = 11, kLcKP = 32 * kLcKC /* 352 >= 4*81 */, kLcXS = kLcKP + 8;
+constexpr int kLcQB = 32, kLcO = 256, kLcKC = 11, kLcKP = 32 * kLcKC /* 352 >= 4*81 */, kLcXS = kLcKP / 2 + 4;
 constexpr int kLcGT = lookup_threads(9, kLcQB), kLcNT = 2 * kLcGT;
+constexpr size_t kLcFwdU = (size_t)(kLcO / 16) * kLcKC * 3 * 64;  // u32x4 of the forward W pack
 
-__device__ __forceinline__ int lc_shift(float mm) {  // max * 2^s < 2^15 (split_pack's rule)
-    int s = 0;
-    if (mm > 0.f && mm <= 3.402823466e38f) {
-        int E;
-        (void)frexpf(mm, &E);
-        s = 15 - E;
-    }
-    return s;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x4 mfma_bf16(u32x4 a, u32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                  0, 0, 0);
 }
 
-// weight [O][C] fp32 -> packed fragments [O/16][kLcKC][hi, lo][64 lanes] (half8: row o = 16 ob +
-// (lane & 15), k = 32 kc + 8 (lane >> 4) + j) followed by int shift[O].  One block (64 lanes) per o.
+// weight [O][C] fp32 -> W's pieces [O/16][kLcKC][hi, mid, lo][64 lanes]: lane = 16 kg + r holds
+// W[16 ob + r][32 kc + 8 kg + j], j < 8 (zero past C).  One block of 64 lanes per (ob, kc).
 __global__ __launch_bounds__(64) void lookup_conv_weights_kernel(const float *__restrict__ w, int C,
-                                                                 u32x4 *__restrict__ frag, int *__restrict__ shift) {
-    const int o = blockIdx.x, lane = threadIdx.x;
-    const float *row = w + (size_t)o * C;
-    float m = 0.f;
-    for (int k = lane; k < C; k += 64) m = fmaxf(m, fabsf(row[k]));
+                                                                 u32x4 *__restrict__ frag) {
+    const int kc = blockIdx.x, ob = blockIdx.y, lane = threadIdx.x;
+    const int o = 16 * ob + (lane & 15), k0 = 32 * kc + 8 * (lane >> 4);
+    float v[8];
 #pragma unroll
-    for (int sh = 32; sh >= 1; sh >>= 1) m = fmaxf(m, __shfl_xor(m, sh));
-    const int s = lc_shift(m);
-    if (lane == 0) shift[o] = s;
-    const int ob = o >> 4, fl0 = o & 15;
-    for (int t = lane; t < kLcKC * 4; t += 64) {  // (kc, k-group) of this row
-        const int kc = t >> 2, kg = t & 3;
-        half8 hi8, lo8;
+    for (int j = 0; j < 8; ++j) v[j] = k0 + j < C ? w[(size_t)o * C + k0 + j] : 0.f;
+    unsigned h[4], m[4], lo[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int k = 32 * kc + 8 * kg + j;
-            const float y = k < C ? ldexpf(row[k], s) : 0.f;
-            const _Float16 hi = (_Float16)y;
-            hi8[j] = hi;
-            lo8[j] = __builtin_isinf(y) ? (_Float16)0.f : (_Float16)(y - (float)hi);
-        }
-        const int fl = fl0 + 16 * kg;
-        frag[(((size_t)ob * kLcKC + kc) * 2 + 0) * 64 + fl] = __builtin_bit_cast(u32x4, hi8);
-        frag[(((size_t)ob * kLcKC + kc) * 2 + 1) * 64 + fl] = __builtin_bit_cast(u32x4, lo8);
-    }
+    for (int j = 0; j < 4; ++j) split3(v[2 * j], v[2 * j + 1], h[j], m[j], lo[j]);
+    u32x4 *dst = frag + (((size_t)ob * kLcKC + kc) * 3) * 64 + lane;
+    dst[0] = u32x4{h[0], h[1], h[2], h[3]};
+    dst[64] = u32x4{m[0], m[1], m[2], m[3]};
+    dst[128] = u32x4{lo[0], lo[1], lo[2], lo[3]};
 }
 
 struct LcSmem {
     union {
-        LookupSmem<9, kLcQB> lk[2];                   // lookups
-        struct {
-            _Float16 xh[kLcQB][kLcXS], xl[kLcQB][kLcXS];  // split rows (after the lookups)
-        } x;
+        LookupSmem<9, kLcQB> lk[2];         // lookups
+        unsigned x[3][kLcQB][kLcXS];        // the tile's pieces [piece][q][k pair] (after the lookups)
     } u;
     float ct[4 * 81][kLcQB];
-    unsigned mx[kLcQB];
 };
 
 __global__ __launch_bounds__(kLcNT) void lookup_conv_kernel(ConstLevelPtrs pyr, const float *__restrict__ coords,
                                                              int B, int NQ, int H, int W, int L,
                                                              const u32x4 *__restrict__ frag,
-                                                             const int *__restrict__ wshift,
                                                              const float *__restrict__ bias, int relu,
                                                              float *__restrict__ out) {
     constexpr int S = 9, K = S * S, QB = kLcQB;
@@ -419,7 +401,6 @@ __global__ __launch_bounds__(kLcNT) void lookup_conv_kernel(ConstLevelPtrs pyr, 
     const int tid = threadIdx.x;
     const int g = tid / kLcGT, ltid = tid - g * kLcGT;
     const int KC = L * K;
-    if (tid < QB) sm.mx[tid] = 0u;
     // ---- lookups: levels 2p + g of pass p (groups beyond L repeat the last level, discarded) ----
 #pragma unroll 1
     for (int p = 0; p < 2; ++p) {
@@ -431,40 +412,33 @@ __global__ __launch_bounds__(kLcNT) void lookup_conv_kernel(ConstLevelPtrs pyr, 
                                       });
         __syncthreads();
     }
-    // ---- per-query scale from the max over its L*K values ----
-    {
-        const int q = tid % QB, part = tid / QB, nparts = kLcNT / QB;
-        float m = 0.f;
-        for (int k = part; k < KC; k += nparts) m = fmaxf(m, fabsf(sm.ct[k][q]));
-        if (m > 0.f) atomicMax(&sm.mx[q], __float_as_uint(m));
-    }
-    __syncthreads();
-    // ---- split rows xh / xl [q][k] (zero beyond L*K) ----
-    for (int idx = tid; idx < QB * kLcKP; idx += kLcNT) {
-        const int k = idx / QB, q = idx - k * QB;
-        const int s = lc_shift(__uint_as_float(sm.mx[q]));
-        const float y = k < KC ? ldexpf(sm.ct[k][q], s) : 0.f;
-        const _Float16 hi = (_Float16)y;
-        sm.u.x.xh[q][k] = hi;
-        sm.u.x.xl[q][k] = __builtin_isinf(y) ? (_Float16)0.f : (_Float16)(y - (float)hi);
+    // ---- pieces x[piece][q][k pair] (zero beyond L*K) ----
+    for (int idx = tid; idx < QB * (kLcKP / 2); idx += kLcNT) {
+        const int kp = idx / QB, q = idx - kp * QB, k = 2 * kp;
+        const float y0 = k < KC ? sm.ct[k][q] : 0.f, y1 = k + 1 < KC ? sm.ct[k + 1][q] : 0.f;
+        unsigned h, m, lo;
+        split3(y0, y1, h, m, lo);
+        sm.u.x[0][q][kp] = h;
+        sm.u.x[1][q][kp] = m;
+        sm.u.x[2][q][kp] = lo;
     }
     __syncthreads();
     // ---- 256 x 32 x 352 GEMM: wave w < 8 owns output channels [32 w, 32 w + 32) ----
     const int lane = tid & 63, w = tid >> 6;
     if (w >= 8) return;
-    const int fr = lane & 15, fk = 8 * (lane >> 4);
-    f32x4 acc[2][2];
+    const int fr = lane & 15, fk = 4 * (lane >> 4);  // B fragment: query fr, k pairs fk .. fk + 3
+    f32x4 acc[2][2], acs[2][2];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int c = 0; c < 2; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    u32x4 ah[2][2], al[2][2];  // [buffer][o-tile]
+        for (int c = 0; c < 2; ++c) acc[a][c] = acs[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    u32x4 wa[2][2][3];  // [buffer][o-tile][piece]
     auto load_a = [&](int buf, int kc) {
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-            const size_t base = (((size_t)(2 * w + t) * kLcKC + kc) * 2) * 64 + lane;
-            ah[buf][t] = frag[base];
-            al[buf][t] = frag[base + 64];
+            const size_t base = (((size_t)(2 * w + t) * kLcKC + kc) * 3) * 64 + lane;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) wa[buf][t][p] = frag[base + 64 * p];
         }
     };
     load_a(0, 0);
@@ -472,20 +446,23 @@ __global__ __launch_bounds__(kLcNT) void lookup_conv_kernel(ConstLevelPtrs pyr, 
     for (int kc = 0; kc < kLcKC; ++kc) {
         const int cur = kc & 1;
         if (kc + 1 < kLcKC) load_a(cur ^ 1, kc + 1);
-        half8 bh[2], bl[2];
+        u32x4 xb[2][3];
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            bh[c] = *reinterpret_cast<const half8 *>(&sm.u.x.xh[16 * c + fr][32 * kc + fk]);
-            bl[c] = *reinterpret_cast<const half8 *>(&sm.u.x.xl[16 * c + fr][32 * kc + fk]);
-        }
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                xb[c][p] = *reinterpret_cast<const u32x4 *>(&sm.u.x[p][16 * c + fr][16 * kc + fk]);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-            const half8 a_h = __builtin_bit_cast(half8, ah[cur][t]), a_l = __builtin_bit_cast(half8, al[cur][t]);
+            const u32x4 wh = wa[cur][t][0], wm = wa[cur][t][1], wl = wa[cur][t][2];
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-                acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_l, bh[c], acc[t][c], 0, 0, 0);
-                acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h, bl[c], acc[t][c], 0, 0, 0);
-                acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_h, bh[c], acc[t][c], 0, 0, 0);
+                acs[t][c] = mfma_bf16(wl, xb[c][0], acs[t][c]);
+                acs[t][c] = mfma_bf16(wh, xb[c][2], acs[t][c]);
+                acs[t][c] = mfma_bf16(wm, xb[c][1], acs[t][c]);
+                acs[t][c] = mfma_bf16(wm, xb[c][0], acs[t][c]);
+                acs[t][c] = mfma_bf16(wh, xb[c][1], acs[t][c]);
+                acc[t][c] = mfma_bf16(wh, xb[c][0], acc[t][c]);
             }
         }
     }
@@ -494,13 +471,12 @@ __global__ __launch_bounds__(kLcNT) void lookup_conv_kernel(ConstLevelPtrs pyr, 
     for (int c = 0; c < 2; ++c) {
         const int q = 16 * c + fr, n = n0 + q;
         if (n >= N) continue;
-        const int sq = lc_shift(__uint_as_float(sm.mx[q]));
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int o = 32 * w + 16 * t + 4 * (lane >> 4) + r;
-                float v = ldexpf(acc[t][c][r], -(wshift[o] + sq)) + bias[o];
+                float v = (acc[t][c][r] + acs[t][c][r]) + bias[o];
                 if (relu && v < 0.0f) v = 0.0f;  // torch.relu: a NaN stays a NaN (fmaxf would drop it)
                 out[((size_t)b * kLcO + o) * N + n] = v;
             }
@@ -536,13 +512,6 @@ constexpr size_t kCbWtU = (size_t)4 * kCbCT * kCbKS * 3 * 64;  // u32x4 of the W
 // tiles, the prefetched next block and the lookup all in registers (~200 VGPRs); 4 (<= 128
 // VGPRs, two workgroups per CU) spills and measured slower.
 constexpr int kCbDwWaves = 2;
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ f32x4 mfma_bf16(u32x4 a, u32x4 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
-                                                  0, 0, 0);
-}
 
 // W [256][C] -> W^T pieces [level][channel tile][K step][hi, mid, lo][64 lanes] in the 16x16x32
 // A-fragment order: lane = 16 kg + c16 holds W[32 ks + 8 kg + j][81 l + 16 ct + c16], j < 8.
@@ -1692,18 +1661,16 @@ hipError_t launch_lookup(const ConstLevelPtrs &pyr, const float *coords, int B, 
     }
 }
 
-// Packed weight buffer: the forward's f16 fragments [O/16][kLcKC][2][64] + shift[O], then (at a
-// 256-B offset) the backward's W^T bf16 pieces (kCbWtU u32x4).
-constexpr size_t kLcFwdBytes = (size_t)(kLcO / 16) * kLcKC * 2 * 64 * sizeof(u32x4) + kLcO * sizeof(int);
-constexpr size_t kLcWtOff = (kLcFwdBytes + 255) / 256 * 256;
+// Packed weight buffer: the forward's W pieces (kLcFwdU u32x4), then the backward's W^T pieces
+// (kCbWtU u32x4).
+constexpr size_t kLcWtOff = kLcFwdU * sizeof(u32x4);
 
 size_t lookup_conv_weights_bytes() { return kLcWtOff + kCbWtU * sizeof(u32x4); }
 
 hipError_t launch_lookup_conv_weights(const float *w, int O, int C, void *packed, hipStream_t s) {
     if (O != kLcO || C < 1 || C > kLcKP) return hipErrorInvalidValue;
-    u32x4 *frag = static_cast<u32x4 *>(packed);
-    int *shift = reinterpret_cast<int *>(frag + (size_t)(kLcO / 16) * kLcKC * 2 * 64);
-    hipLaunchKernelGGL(lookup_conv_weights_kernel, dim3(kLcO), dim3(64), 0, s, w, C, frag, shift);
+    hipLaunchKernelGGL(lookup_conv_weights_kernel, dim3(kLcKC, kLcO / 16), dim3(64), 0, s, w, C,
+                       static_cast<u32x4 *>(packed));
     hipLaunchKernelGGL(lookup_conv_wt_kernel, dim3(kCbKS, kCbCT, 4), dim3(64), 0, s, w, C,
                        reinterpret_cast<u32x4 *>(static_cast<char *>(packed) + kLcWtOff));
     return hipGetLastError();
@@ -1758,10 +1725,9 @@ hipError_t launch_lookup_conv(const ConstLevelPtrs &pyr, const float *coords, in
                               hipStream_t s) {
     if (radius != 4 || levels < 1 || levels > 4) return hipErrorInvalidValue;  // E-RAFT: r = 4, L <= 4
     const u32x4 *frag = static_cast<const u32x4 *>(packed);
-    const int *shift = reinterpret_cast<const int *>(frag + (size_t)(kLcO / 16) * kLcKC * 2 * 64);
     const int nqb = (NQ + kLcQB - 1) / kLcQB;
     hipLaunchKernelGGL(lookup_conv_kernel, dim3(nqb * B), dim3(kLcNT), 0, s, pyr, coords, B, NQ, H, W, levels, frag,
-                       shift, bias, relu, out);
+                       bias, relu, out);
     return hipGetLastError();
 }
 

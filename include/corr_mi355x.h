@@ -239,9 +239,8 @@ size_t corr_forward_splat_workspace(int B, int H, int W);
  * Lookup fused with its consumer, BasicMotionEncoder's cor = relu(convc1(corr))
  * (model/update.py:68,75; a 1x1 convolution L*(2r+1)^2 -> 256): the window lookup of
  * corr_lookup into an on-chip tile, then out[b][o][h][w] = (relu?)(bias[o] +
- * sum_c weight[o][c] * corr[b][c][h][w]) on the f16 MFMA with the fp32-accurate 3-product split
- * (per-query and per-output-channel power-of-two scales; |error| ~ 2^-22 of the larger operands,
- * the build's f16x3 contract).  The weight (convc1.weight viewed [256][L*K], fp32) is split once
+ * sum_c weight[o][c] * corr[b][c][h][w]) on the bf16 MFMA with CORR_BUILD_BF16X6's exact
+ * three-piece split (six products per fp32 product, no scales: no narrower than fp32).  The weight (convc1.weight viewed [256][L*K], fp32) is split once
  * per weight version by corr_lookup_conv_weights into a corr_lookup_conv_weights_bytes() buffer;
  * out [B][256][H][W].  radius 4, levels <= 4 (E-RAFT); CORR_EUNSUPPORTED otherwise.  This call
  * is the forward; corr_lookup_conv_bwd below is its training backward.
