@@ -1,5 +1,6 @@
-"""Time the fused lookup + convc1 backward (corr_lookup_conv_bwd) against the round-3 torch
-composition it replaces (HIP lookup into a 324-channel tensor, threshold backward, bias sum,
+"""Time the fused lookup + convc1 forward (corr_lookup_conv) and backward (corr_lookup_conv_bwd)
+against the compositions they replace (forward: lookup, MIOpen conv2d, ReLU; backward: the round-3 torch
+composition (HIP lookup into a 324-channel tensor, threshold backward, bias sum,
 torch.bmm for dW, torch.matmul for W^T g) at config 4's shape (B 8, 36 x 48, 4 levels).
 GPU only; prints one JSON line."""
 import json
@@ -48,8 +49,18 @@ def main():
         gl = torch.matmul(w.view(256, C).t(), gf)
         return gb, gw, gl
 
+    import torch.nn.functional as F
+    fout = torch.empty(B, 256, H, W, device=dev)
+
+    def fwd_fused():  # corr_lookup_conv (what CorrBlock.lookup_conv runs at inference)
+        _lib.lookup_conv(cb._state.levels, coords, r, packed, bias, fout, True)
+
+    def fwd_composed():  # the reference composition: lookup, then convc1 (MIOpen) and ReLU
+        torch.relu(F.conv2d(cb(coords), w, bias))
+
     res = {"shape": [B, D, H, W, L, r], "lib": os.path.basename(_lib.load()._name)}
-    for name, fn in (("fused_us", fused), ("torch_composition_us", composed)):
+    for name, fn in (("fused_us", fused), ("torch_composition_us", composed), ("fwd_fused_us", fwd_fused),
+                     ("fwd_lookup_conv2d_relu_us", fwd_composed)):
         for _ in range(5):
             fn()
         torch.cuda.synchronize()
