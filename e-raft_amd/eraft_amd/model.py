@@ -213,9 +213,9 @@ class ERAFT(nn.Module):
     context_dim = 128
     corr_levels = 4
     corr_radius = 4
-    # lookup fused with convc1 at inference (corr_lookup_conv, bf16x6 MFMA); ERAFT_AMD_FUSE_CONV=0
-    # keeps lookup + MIOpen convc1.  DSEC: 19.1 vs 31.7 us per GRU iteration, e2e 80.5 vs 80.0
-    # frame pairs/s (profiles/r02d_*)
+    # lookup fused with convc1 (corr_lookup_conv, bf16x6 MFMA; in training its backward is
+    # corr_lookup_conv_bwd); ERAFT_AMD_FUSE_CONV=0 keeps lookup + MIOpen convc1.  DSEC: 20.1 vs
+    # 38.9 us per GRU iteration (profiles/r04k_conv_fwd_bwd_timing.jsonl)
     fuse_lookup_conv = os.environ.get("ERAFT_AMD_FUSE_CONV", "1") == "1"
 
     def __init__(self, config, n_first_channels):
