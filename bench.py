@@ -53,8 +53,8 @@ BUILD_ARITH = {0: "fp32 MFMA (exact fp32 products, fp32 accumulate; the referenc
                   "(hi.hi + hi.lo + lo.hi, ~2^-22 relative: NARROWER than fp32), fp32 accumulate",
                2: "bf16x6, no narrower than fp32: every fp32 feature split EXACTLY into three bf16 pieces "
                   "(hi + mid + lo, fp32's exponent range, no scale or flush), the 6 piece products of "
-                  "weight >= 2^-16 on the bf16 MFMA (dropped terms <= 2^-23 |ab|), fp32 accumulate "
-                  "(6D/32 roundings per dot product vs D for an fp32 fmaf chain); per-row error vs fp64 "
+                  "weight >= 2^-16 on the bf16 MFMA (dropped terms <= 2^-23 |ab|), two fp32 accumulators "
+                  "(hi.hi: D/32 roundings per dot product vs D for an fp32 fmaf chain); per-row error vs fp64 "
                   "<= the fp32 MFMA build's (tests/test_gpu_parity.py::test_build_bf16x6_not_narrower_than_fp32)"}
 BUILD_NOTE = {
     0: "fp32 operands on v_mfma_f32_32x32x2_f32: achieved = 2*B*N^2*D flops / build kernel time, "
@@ -68,6 +68,13 @@ BUILD_NOTE = {
        "kernel time, each kernel timed alone: kernel_us), against the dense bf16 MFMA peak; the "
        "fp32-equivalent rate (2*B*N^2*D / time) is fp32_equivalent_tflops",
 }
+# The backward GEMMs' arithmetic per backward algorithm (corr_bwd_split.hip / corr_bwd.hip).
+BWD_ARITH = {0: "fp32 operands on the fp32 MFMA",
+             1: "f16x3: per-row 2^e (hi + lo) f16 split, 3 f16 MFMAs per product (~2^-22 relative: NARROWER "
+                "than fp32)",
+             2: "bf16x6, no narrower than fp32: both operands split EXACTLY into three bf16 pieces while staging "
+                "(no scales), the 6 piece products of weight >= 2^-16 on the bf16 MFMA, fp32 accumulate "
+                "(6 roundings per 16 k vs 16 for an fp32 fmaf chain)"}
 
 WORKLOADS = {
     # name: (B, D, H, W, levels, radius, iters)
@@ -482,6 +489,9 @@ def main():
         def run_bwd_kernels():  # corr_backward alone: all lookup backwards + fold + GEMMs
             return _lib.backward(coords, gouts, r, gpyr, f1, f2)
 
+        def run_bwd_f16x3():  # the same with the narrower f16x3 split GEMMs (+ the maxima they need)
+            return _lib.backward(coords, gouts, r, gpyr, f1, f2, _lib.BUILD_F16X3)
+
         def run_bwd_staged():  # round-1 sequence: zero + lookup_bwd per lookup + pool_bwd + GEMMs
             gbuf.zero_()
             for c, go in zip(coords, gouts):
@@ -629,6 +639,7 @@ def main():
         x3_ms = graph_time_ms(build_f16x3, stream, rep=4) if algo == _lib.BUILD_BF16X6 else None
         bwd_ms = graph_time_ms(run_bwd_kernels, stream, rep=4) if train else None
         bwd_staged_ms = graph_time_ms(run_bwd_staged, stream, rep=4) if train else None
+        bwd_x3_ms = graph_time_ms(run_bwd_f16x3, stream, rep=4) if train and algo == _lib.BUILD_BF16X6 else None
         if sharded and world > 1:  # per-rank broadcast time (eager, events on the stream)
             ts = []
             for _ in range(5):
@@ -722,13 +733,20 @@ def main():
                                       "(round 3's step: at B16 their 394 MB stream past the MALL)")
         if train:
             res["backward_kernels"] = {
-                "phase": f"corr_backward: {iters} lookup backwards in one launch + pool fold with dC "
-                         "row/column maxima + 2 split GEMMs (dF1 = dC F2^T, dF2 = F1^T dC), library call alone",
+                "phase": f"corr_backward: {iters} lookup backwards in one launch + pool fold into dC + 2 "
+                         f"{BUILD_ALGO[_lib.backward_algo(algo)]} split GEMMs (dF1 = dC F2^T, dF2 = F1^T dC, "
+                         "split-K with an ordered reduce), library call alone",
+                "arith": BWD_ARITH[_lib.backward_algo(algo)],
                 "avg_us": round(bwd_ms * 1e3, 2), "gemm_flops": 2 * fl,
                 "staged_avg_us": round(bwd_staged_ms * 1e3, 2),
-                "staged_phase": f"zero + {iters} lookup_bwd + pool_bwd + absmax + GEMMs (round-1 sequence)"}
+                "staged_phase": f"zero + {iters} lookup_bwd + pool_bwd + GEMMs (round-1 sequence)"}
+            if bwd_x3_ms is not None:
+                res["backward_kernels"]["f16x3_avg_us"] = round(bwd_x3_ms * 1e3, 2)
+                res["backward_kernels"]["f16x3_arith"] = BWD_ARITH[1]
             res["train_step_note"] = ("value times the autograd step through CorrBlock (forward, 12 "
-                                      "lookups, loss.backward() to both fmaps), as training runs it")
+                                      "lookups, loss.backward() to both fmaps), as training runs it; forward "
+                                      "build and backward GEMMs both no narrower than fp32 (build_arith, "
+                                      "backward_kernels.arith)")
         if bcast_ms is not None:
             res["sharded_timing"] = {
                 "per_rank": per_rank,

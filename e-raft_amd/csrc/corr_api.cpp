@@ -77,7 +77,7 @@ using namespace corr;
 
 extern "C" {
 
-int corr_version(void) { return 103; }
+int corr_version(void) { return 104; }
 
 const char *corr_last_error(void) { return g_err; }
 
@@ -247,7 +247,7 @@ int corr_build_bwd_rows(const float *grad_c, const float *fmap1_rows, int NQ, co
 size_t corr_build_bwd_ex_workspace(int algo, int B, int D, int NQ, int H, int W) {
     if (B < 1 || D < 1 || NQ < 1 || H < 1 || W < 1) return 0;
     if (algo == CORR_BUILD_FP32) return build_bwd_workspace(B, D, NQ, H, W);
-    if (algo == CORR_BUILD_F16X3) return build_bwd_split_workspace(B, D, NQ, H, W);
+    if (algo == CORR_BUILD_F16X3 || algo == CORR_BUILD_BF16X6) return build_bwd_split_workspace(B, D, NQ, H, W);
     return (size_t)-1;
 }
 
@@ -259,7 +259,8 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
         return corr_build_bwd_rows(grad_c, fmap1_rows, NQ, fmap2, B, D, H, W, dfmap1_rows, dfmap2, workspace,
                                    workspace_bytes, stream);
     g_err[0] = 0;
-    if (algo != CORR_BUILD_F16X3) return fail(CORR_EUNSUPPORTED, "%s: unknown algorithm %d", fn, algo);
+    if (algo != CORR_BUILD_F16X3 && algo != CORR_BUILD_BF16X6)
+        return fail(CORR_EUNSUPPORTED, "%s: unknown algorithm %d", fn, algo);
     int rc = check_dims(fn, B, NQ, H, W, 1);
     if (rc) return rc;
     if (D < 1) return fail(CORR_EINVAL, "%s: D must be >= 1 (got %d)", fn, D);
@@ -271,7 +272,7 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
     if (workspace_bytes < need || !workspace)
         return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
     return hip_status(launch_build_bwd_split(grad_c, fmap1_rows, NQ, fmap2, B, D, H, W, dfmap1_rows, dfmap2,
-                                             workspace, (hipStream_t)stream),
+                                             workspace, (hipStream_t)stream, algo == CORR_BUILD_BF16X6),
                       fn);
 }
 
@@ -314,7 +315,7 @@ int corr_backward(int algo, const float *const *coords_rows, const float *const 
                   size_t workspace_bytes, void *stream) {
     static const char *fn = "corr_backward";
     g_err[0] = 0;
-    if (algo != CORR_BUILD_FP32 && algo != CORR_BUILD_F16X3)
+    if (algo != CORR_BUILD_FP32 && algo != CORR_BUILD_F16X3 && algo != CORR_BUILD_BF16X6)
         return fail(CORR_EUNSUPPORTED, "%s: unknown algorithm %d", fn, algo);
     int rc = check_dims(fn, B, NQ, H, W, levels);
     if (rc || (rc = check_radius(fn, radius))) return rc;

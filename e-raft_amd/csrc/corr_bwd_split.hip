@@ -14,7 +14,13 @@
 // split over workgroups (partial slabs, summed in split order by splitk_reduce_kernel of
 // corr_bwd.hip, which applies 1/sqrt(D)) — deterministic, no atomics.
 //
-// Row maxima: F1 / F2 from rowmax2_kernel; dC's row and column maxima from the fused backward
+// BF16X6 (BF = true, the default build's backward): every operand element is split EXACTLY into
+// three bf16 pieces while staging (split3 of corr_build_common.h: no scales, no row maxima), and
+// the six largest piece products go on v_mfma_f32_32x32x16_bf16 — lo.hi + hi.lo + mid.mid +
+// mid.hi + hi.mid into a second accumulator, hi.hi into the first, the two added once in the
+// epilogue (the build's bf16x6 scheme): no narrower than an fp32 GEMM.
+//
+// Row maxima (f16x3 only): F1 / F2 from rowmax2_kernel; dC's row and column maxima from the fused backward
 // (corr_lookup.hip) or, for a caller-supplied dC, from absmax_kernel (unsigned atomicMax on the
 // bits of non-negative floats: exact and order free).  Also here: the pool-backward fold with
 // dC's maxima (pool_fold_max_kernel) and the column-maxima reduce of the fused backward.
@@ -28,6 +34,7 @@
 namespace corr {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8g __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
@@ -321,6 +328,22 @@ __device__ __forceinline__ void split2(float x0, float x1, int s, bool guard, ha
     }
 }
 
+// The exact three-piece bf16 split of a pair, branch-free (the GEMM's staging runs it on every
+// element it reads): hi = bf16_rn of x clamped to +-M (M = 0x7F7F7FFF, the largest float that
+// rounds to a finite bf16), mid = bf16_rn(x - hi), lo = x - hi - mid.  Finite x: x - hi is exact
+// (same binade, or |x| <= 2^-126 ... ), and so is the last difference, so x = hi + mid + lo bit for
+// bit — the same pieces as split3 wherever hi does not overflow; past M, hi = the bf16 maximum
+// and the residual carries the rest (split3 truncates there instead).  inf / NaN give non-finite
+// pieces, so every product with them is non-finite, as in fp32.
+__device__ __forceinline__ void split3_bwd(float a, float b, unsigned &hi, unsigned &mid, unsigned &lo) {
+    constexpr float M = 3.3961775e38f;  // 0x7F7F7FFF
+    float ha, hb, ma, mb, da, db;
+    hi = rn_pair(__builtin_amdgcn_fmed3f(a, -M, M), __builtin_amdgcn_fmed3f(b, -M, M), ha, hb);
+    const float ra = a - ha, rb = b - hb;
+    mid = rn_pair(ra, rb, ma, mb);
+    lo = rn_pair(ra - ma, rb - mb, da, db);
+}
+
 // ---------------------------------------------------------------------------------------
 // The GEMM: C[b][i][j] (+)= sum_k A[b][i][k] B[b][j][k].  4 waves (2 along i x 2 along j),
 // each 64 i x 128 j (2 x 4 blocks of 32 x 32), workgroup 128 x 256; K chunks staged through
@@ -383,10 +406,12 @@ __device__ __forceinline__ void gemm_wait_vm_barrier() {
 // Dynamic LDS of the GEMM: the hi/lo staging (2 stages; DMA: 1), the row exponents, and (DMA)
 // a 2-slot ring of raw fp32 chunks (kTI + kTJ rows x 16 k; BCOL: B as 16 k-rows x 256 columns).
 // PIPE (DMA path): a 3-slot raw ring, so chunk k + 1 can be split while chunk k's MFMAs run.
-template <bool DMA, int WI = kWI, bool PIPE = false>
+// BF: each stage holds (hi, mid) in the hi/lo layout plus a kTJ-row plane of the lo pieces (A
+// row i's in unit slot 2o, B row j's in slot 2o + 1), and there are no row exponents.
+template <bool DMA, int WI = kWI, bool PIPE = false, bool BF = false>
 constexpr int gemm_lds_bytes() {
     constexpr int rows = 32 * kMI * WI + kTJ;
-    return (DMA ? 1 : 2) * rows * 4 * (int)sizeof(u32x4) + rows * (int)sizeof(int) +
+    return (DMA ? 1 : 2) * (rows + (BF ? kTJ : 0)) * 4 * (int)sizeof(u32x4) + (BF ? 0 : rows * (int)sizeof(int)) +
            (DMA ? (PIPE ? 3 : 2) * rows * kBK * (int)sizeof(float) : 0);
 }
 
@@ -404,7 +429,7 @@ __device__ __forceinline__ unsigned split_lo_mix(unsigned h2, float y0, float y1
     return lo;
 }
 
-template <bool BCOL, bool DMA = false, int WI = kWI, bool PIPE = false>
+template <bool BCOL, bool DMA = false, int WI = kWI, bool PIPE = false, bool BF = false>
 __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmParams p) {
     // WI = 4 (DMA path only): 8 waves, a 256 x 256 tile (each wave still 64 x 128), so every
     // staged element feeds twice the MFMAs
@@ -413,11 +438,13 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
     constexpr int UB = 2 * kTJ / NT;      // B row-octets per thread (BCOL = false)
     constexpr int KO = 2 * kTJ / NT;      // B k-octets per thread (BCOL = true; column tid % kTJ)
     constexpr int NW = NT / 64, PB = 16 / NW;  // waves; B DMA pieces per wave and chunk
+    constexpr int STG = (ROWS + (BF ? kTJ : 0)) * 4;  // u32x4 units per staging stage
     static_assert(TI == NT / 2, "one A row-octet per thread");
+    static_assert(TI <= kTJ, "the BF lo plane holds kTJ rows");
     extern __shared__ __attribute__((aligned(16))) u32x4 gemm_smem[];
     u32x4 *lds = gemm_smem;
-    int *lex = reinterpret_cast<int *>(gemm_smem + (DMA ? 1 : 2) * ROWS * 4);
-    float *raw = reinterpret_cast<float *>(lex + ROWS);
+    int *lex = reinterpret_cast<int *>(gemm_smem + (DMA ? 1 : 2) * STG);
+    float *raw = reinterpret_cast<float *>(lex + (BF ? 0 : ROWS));
     int id = xcd_swizzle(blockIdx.x, gridDim.x);
     const int tj = id % p.tj;
     id /= p.tj;
@@ -431,19 +458,21 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
     const int wv = tid >> 6, wi = wv / kWJ, wj = wv % kWJ;
 
-    for (int row = tid; row < ROWS; row += NT) {
-        const unsigned m = row < TI ? p.mxA[(size_t)b * p.NI + min(i0 + row, p.NI - 1)]
-                                     : p.mxB[(size_t)b * p.NJ + min(j0 + row - TI, p.NJ - 1)];
-        lex[row] = -split_shift(__uint_as_float(m));
+    if constexpr (!BF) {
+        for (int row = tid; row < ROWS; row += NT) {
+            const unsigned m = row < TI ? p.mxA[(size_t)b * p.NI + min(i0 + row, p.NI - 1)]
+                                         : p.mxB[(size_t)b * p.NJ + min(j0 + row - TI, p.NJ - 1)];
+            lex[row] = -split_shift(__uint_as_float(m));
+        }
+        __syncthreads();
     }
-    __syncthreads();
 
     // staging tasks
     const int arow = tid >> 1, aoct = tid & 1;
     const float *ap = p.A + (size_t)b * p.a_sb + (size_t)min(i0 + arow, p.NI - 1) * p.a_sr + aoct * 8;
-    const int sa = -lex[arow];
+    const int sa = BF ? 0 : -lex[arow];
     auto row_inf = [&](const unsigned *mx, int row, int n) {
-        return __uint_as_float(mx[(size_t)b * n + min(row, n - 1)]) > 3.402823466e38f;
+        return !BF && __uint_as_float(mx[(size_t)b * n + min(row, n - 1)]) > 3.402823466e38f;
     };
     const bool ga = row_inf(p.mxA, i0 + arow, p.NI);
     const float *bp[2];
@@ -456,12 +485,12 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
         for (int u = 0; u < UB; ++u) {
             brow[u] = (tid >> 1) + (NT / 2) * u;
             bp[u] = p.Bm + (size_t)b * p.b_sb + (size_t)min(j0 + brow[u], p.NJ - 1) * p.b_sr + aoct * 8;
-            sb[u] = -lex[TI + brow[u]];
+            sb[u] = BF ? 0 : -lex[TI + brow[u]];
             gb[u] = row_inf(p.mxB, j0 + brow[u], p.NJ);
         }
     } else {
         bp[0] = p.Bm + (size_t)b * p.b_sb;  // + n * b_sk + j
-        sb[0] = -lex[TI + bcol];
+        sb[0] = BF ? 0 : -lex[TI + bcol];
         gb[0] = row_inf(p.mxB, j0 + bcol, p.NJ);
     }
     const bool vec = p.vec;
@@ -522,7 +551,47 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
     // loop runs one branch-free copy per case, so its MFMAs can be scheduled among the split)
     auto store_chunk = [&](int st, const float (&ra)[8], const float (&rb)[16], auto fm_tag) {
         constexpr int FM = decltype(fm_tag)::value;
-        u32x4 *S = lds + (size_t)st * ROWS * 4;
+        u32x4 *S = lds + (size_t)st * STG;
+        if constexpr (BF) {
+            // (hi, mid) into the hi/lo layout's two slots, lo into the lo plane: A rows in slot 2o,
+            // B rows in slot 2o + 1 (the same bank pattern as the hi / lo writes of those rows)
+            u32x4 *S1 = S + ROWS * 4;
+            auto split8 = [&](const float *v, u32x4 &hi, u32x4 &mid, u32x4 &lo) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    unsigned h_, m_, l_;
+                    split3_bwd(v[2 * t], v[2 * t + 1], h_, m_, l_);
+                    hi[t] = h_, mid[t] = m_, lo[t] = l_;
+                }
+            };
+            {
+                u32x4 hi, mid, lo;
+                split8(ra, hi, mid, lo);
+                S[swz(arow, 2 * aoct)] = hi;
+                S[swz(arow, 2 * aoct + 1)] = mid;
+                S1[swz(arow, 2 * aoct)] = lo;
+            }
+            if (!BCOL) {
+#pragma unroll
+                for (int u = 0; u < UB; ++u) {
+                    u32x4 hi, mid, lo;
+                    split8(rb + 8 * u, hi, mid, lo);
+                    S[swz(TI + brow[u], 2 * aoct)] = hi;
+                    S[swz(TI + brow[u], 2 * aoct + 1)] = mid;
+                    S1[swz(brow[u], 2 * aoct + 1)] = lo;
+                }
+            } else {
+#pragma unroll
+                for (int o = 0; o < KO; ++o) {
+                    u32x4 hi, mid, lo;
+                    split8(rb + 8 * o, hi, mid, lo);
+                    S[swz(TI + bcol, 2 * (boct0 + o))] = hi;
+                    S[swz(TI + bcol, 2 * (boct0 + o) + 1)] = mid;
+                    S1[swz(bcol, 2 * (boct0 + o) + 1)] = lo;
+                }
+            }
+            return;
+        }
         auto split8 = [&](const float *v, int sh, bool guard, float f, u32x4 &hi, u32x4 &lo) {
             half2v h[4], l[4];
             if (FM == 1 || (FM == 0 && fast)) {
@@ -575,31 +644,80 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
             for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
 
     const int arow0 = wi * (32 * kMI) + l32, brow0 = TI + wj * (32 * kNJ) + l32;
-    auto mfma_chunk = [&](int st) {
-        const u32x4 *S = lds + (size_t)st * ROWS * 4;
-        half8 ah[kMI], al[kMI], bh[kNJ], bl[kNJ];
+    // One chunk's fragments (the staged pieces of this wave's rows); m* only for BF.
+    struct Frags {
+        u32x4 ah[kMI], am[kMI], al[kMI], bh[kNJ], bm[kNJ], bl[kNJ];
+    };
+    auto frags = [&](int st, Frags &f) __attribute__((always_inline)) {
+        const u32x4 *S = lds + (size_t)st * STG;
 #pragma unroll
         for (int m = 0; m < kMI; ++m) {
-            ah[m] = __builtin_bit_cast(half8, S[swz(arow0 + 32 * m, 2 * h)]);
-            al[m] = __builtin_bit_cast(half8, S[swz(arow0 + 32 * m, 2 * h + 1)]);
+            f.ah[m] = S[swz(arow0 + 32 * m, 2 * h)];
+            if (BF) f.am[m] = S[swz(arow0 + 32 * m, 2 * h + 1)], f.al[m] = S[ROWS * 4 + swz(arow0 + 32 * m, 2 * h)];
+            else f.al[m] = S[swz(arow0 + 32 * m, 2 * h + 1)];
         }
 #pragma unroll
         for (int n = 0; n < kNJ; ++n) {
-            bh[n] = __builtin_bit_cast(half8, S[swz(brow0 + 32 * n, 2 * h)]);
-            bl[n] = __builtin_bit_cast(half8, S[swz(brow0 + 32 * n, 2 * h + 1)]);
+            f.bh[n] = S[swz(brow0 + 32 * n, 2 * h)];
+            if (BF) f.bm[n] = S[swz(brow0 + 32 * n, 2 * h + 1)], f.bl[n] = S[ROWS * 4 + swz(brow0 - TI + 32 * n, 2 * h + 1)];
+            else f.bl[n] = S[swz(brow0 + 32 * n, 2 * h + 1)];
         }
+    };
+    auto mfmas = [&](const Frags &f) __attribute__((always_inline)) {
+        if constexpr (BF) {
+            auto mm = [](u32x4 a, u32x4 b, f32x16 c) {
+                return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8g, a),
+                                                               __builtin_bit_cast(bf16x8g, b), c, 0, 0, 0);
+            };
+            // smallest first: lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi (one accumulator: the
+            // register budget of two waves per SIMD holds one 64 x 128 set)
 #pragma unroll
-        for (int m = 0; m < kMI; ++m)
+            for (int m = 0; m < kMI; ++m)
 #pragma unroll
-            for (int n = 0; n < kNJ; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bh[n], acc[m][n], 0, 0, 0);
+                for (int n = 0; n < kNJ; ++n) acc[m][n] = mm(f.al[m], f.bh[n], acc[m][n]);
 #pragma unroll
-        for (int m = 0; m < kMI; ++m)
+            for (int m = 0; m < kMI; ++m)
 #pragma unroll
-            for (int n = 0; n < kNJ; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bl[n], acc[m][n], 0, 0, 0);
+                for (int n = 0; n < kNJ; ++n) acc[m][n] = mm(f.ah[m], f.bl[n], acc[m][n]);
 #pragma unroll
-        for (int m = 0; m < kMI; ++m)
+            for (int m = 0; m < kMI; ++m)
 #pragma unroll
-            for (int n = 0; n < kNJ; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh[n], acc[m][n], 0, 0, 0);
+                for (int n = 0; n < kNJ; ++n) acc[m][n] = mm(f.am[m], f.bm[n], acc[m][n]);
+#pragma unroll
+            for (int m = 0; m < kMI; ++m)
+#pragma unroll
+                for (int n = 0; n < kNJ; ++n) acc[m][n] = mm(f.am[m], f.bh[n], acc[m][n]);
+#pragma unroll
+            for (int m = 0; m < kMI; ++m)
+#pragma unroll
+                for (int n = 0; n < kNJ; ++n) acc[m][n] = mm(f.ah[m], f.bm[n], acc[m][n]);
+#pragma unroll
+            for (int m = 0; m < kMI; ++m)
+#pragma unroll
+                for (int n = 0; n < kNJ; ++n) acc[m][n] = mm(f.ah[m], f.bh[n], acc[m][n]);
+        } else {
+            auto mm = [](u32x4 a, u32x4 b, f32x16 c) {
+                return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(half8, a), __builtin_bit_cast(half8, b),
+                                                              c, 0, 0, 0);
+            };
+#pragma unroll
+            for (int m = 0; m < kMI; ++m)
+#pragma unroll
+                for (int n = 0; n < kNJ; ++n) acc[m][n] = mm(f.al[m], f.bh[n], acc[m][n]);
+#pragma unroll
+            for (int m = 0; m < kMI; ++m)
+#pragma unroll
+                for (int n = 0; n < kNJ; ++n) acc[m][n] = mm(f.ah[m], f.bl[n], acc[m][n]);
+#pragma unroll
+            for (int m = 0; m < kMI; ++m)
+#pragma unroll
+                for (int n = 0; n < kNJ; ++n) acc[m][n] = mm(f.ah[m], f.bh[n], acc[m][n]);
+        }
+    };
+    auto mfma_chunk = [&](int st) {
+        Frags f;
+        frags(st, f);
+        mfmas(f);
     };
     if constexpr (DMA) {
         const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -684,61 +802,25 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
                 __syncthreads();
                 if (kc0 + 3 < kc1) issue(kc0 + 3, 0);
             }
-            auto frags = [&](half8 (&ah)[kMI], half8 (&al)[kMI], half8 (&bh)[kNJ], half8 (&bl)[kNJ])
-                             __attribute__((always_inline)) {
-                const u32x4 *S = lds;
-#pragma unroll
-                for (int m = 0; m < kMI; ++m) {
-                    ah[m] = __builtin_bit_cast(half8, S[swz(arow0 + 32 * m, 2 * h)]);
-                    al[m] = __builtin_bit_cast(half8, S[swz(arow0 + 32 * m, 2 * h + 1)]);
-                }
-#pragma unroll
-                for (int n = 0; n < kNJ; ++n) {
-                    bh[n] = __builtin_bit_cast(half8, S[swz(brow0 + 32 * n, 2 * h)]);
-                    bl[n] = __builtin_bit_cast(half8, S[swz(brow0 + 32 * n, 2 * h + 1)]);
-                }
-            };
-            auto mfmas = [&](const half8 (&ah)[kMI], const half8 (&al)[kMI], const half8 (&bh)[kNJ],
-                             const half8 (&bl)[kNJ]) __attribute__((always_inline)) {
-#pragma unroll
-                for (int m = 0; m < kMI; ++m)
-#pragma unroll
-                    for (int n = 0; n < kNJ; ++n)
-                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[m], bh[n], acc[m][n], 0, 0, 0);
-#pragma unroll
-                for (int m = 0; m < kMI; ++m)
-#pragma unroll
-                    for (int n = 0; n < kNJ; ++n)
-                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bl[n], acc[m][n], 0, 0, 0);
-#pragma unroll
-                for (int m = 0; m < kMI; ++m)
-#pragma unroll
-                    for (int n = 0; n < kNJ; ++n)
-                        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[m], bh[n], acc[m][n], 0, 0, 0);
-            };
             // every iteration but the last: chunk kc + 1 is split (branch-free, one copy per split
             // mode) in the same region as chunk kc's MFMAs
             auto body = [&](auto fm_tag) __attribute__((always_inline)) {
                 for (int kc = kc0; kc + 1 < kc1; ++kc) {
-                    half8 ah[kMI], al[kMI], bh[kNJ], bl[kNJ];
-                    frags(ah, al, bh, bl);
+                    Frags f;
+                    frags(0, f);
                     wait_groups(min(kc1, kc + 4) - kc - 2);  // chunk kc + 1 landed; fragments read
                     read_raw((kc + 1 - kc0) % 3);
                     store_chunk(0, ra0, rb0, fm_tag);
-                    mfmas(ah, al, bh, bl);
+                    mfmas(f);
                     __syncthreads();  // chunk kc + 1 staged; its ring slot read by every wave
                     if (kc + 4 < kc1) issue(kc + 4, (kc + 1 - kc0) % 3);
                 }
             };
-            if (fast) body(std::integral_constant<int, 1>{});
+            if (BF || fast) body(std::integral_constant<int, 1>{});
             else body(std::integral_constant<int, 2>{});
-            if (kc0 < kc1) {  // the last chunk
-                half8 ah[kMI], al[kMI], bh[kNJ], bl[kNJ];
-                frags(ah, al, bh, bl);
-                mfmas(ah, al, bh, bl);
-            }
+            if (kc0 < kc1) mfma_chunk(0);  // the last chunk
         }
-    } else if constexpr (!BCOL) {  // row operands: one set (two would spill at 256 VGPRs)
+    } else if constexpr (!BCOL || BF) {  // row operands (and BF): one set (two would spill at 256 VGPRs)
         if (kc0 < kc1) {
             load_chunk(kc0, ra0, rb0);
             store_chunk(0, ra0, rb0, FM0{});
@@ -779,14 +861,14 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
     for (int n = 0; n < kNJ; ++n) {
         const int jl = wj * (32 * kNJ) + 32 * n + l32;
         const int j = j0 + jl;
-        const int ej = lex[TI + jl];
+        const int ej = BF ? 0 : lex[TI + jl];
 #pragma unroll
         for (int m = 0; m < kMI; ++m) {
 #pragma unroll
             for (int g = 0; g < 16; ++g) {
                 const int il = wi * (32 * kMI) + 32 * m + (g & 3) + 8 * (g >> 2) + 4 * h;
                 const int i = i0 + il;
-                float x = ldexpf(acc[m][n][g], lex[il] + ej);
+                float x = BF ? acc[m][n][g] : ldexpf(acc[m][n][g], lex[il] + ej);
                 if (p.direct) x = x * p.alpha;
                 if (i < p.NI && j < p.NJ) C[(size_t)i * p.NJ + j] = x;
             }
@@ -881,12 +963,13 @@ size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W) {
     return bwd_split_workspace_tuned(B, D, NQ, H, W, GemmTune{});
 }
 
-// The GEMMs once dC's row maxima (w.mxB) and column maxima (w.mxC) are in the workspace.
+// The GEMMs once dC's row maxima (w.mxB) and column maxima (w.mxC) are in the workspace (f16x3;
+// bf: the exact bf16x6 split, no maxima read).
 // C[b] (NI x NJ) = A[b] B[b]^T / sqrt(D) straight from the fp32 operands (split while staging).
 template <bool BCOL>
 hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long b_sb, long b_sr, long b_sk,
                     const unsigned *mxA, const unsigned *mxB, int B, int NI, int NJ, int K, float sD, float *C,
-                    float *slab, hipStream_t s, const GemmTune &t = GemmTune{}) {
+                    float *slab, hipStream_t s, const GemmTune &t = GemmTune{}, bool bf = false) {
     FGemmParams p{};
     p.A = A, p.a_sb = a_sb, p.a_sr = a_sr;
     p.Bm = Bm, p.b_sb = b_sb, p.b_sr = b_sr, p.b_sk = b_sk;
@@ -910,25 +993,29 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     // the MFMAs, a third less split work per MFMA (train: dF1 73 -> 67, dF2 75 -> 67 us)
     const bool wide = dma && t.wide && NI > 32 * kMI * kWI;
     hipError_t e;
-    auto go = [&](auto dma_tag, auto wi_tag, auto pipe_tag) {
+    auto go1 = [&](auto dma_tag, auto wi_tag, auto pipe_tag, auto bf_tag) {
         constexpr bool D = decltype(dma_tag)::value;
         constexpr int WI = decltype(wi_tag)::value;
         constexpr bool P = decltype(pipe_tag)::value;
+        constexpr bool BF = decltype(bf_tag)::value;
         FGemmParams q = p;
         q.ti = (NI + 32 * kMI * WI - 1) / (32 * kMI * WI);
         const long grid = (long)q.ti * q.tj * q.splits * B;
         static std::atomic<unsigned long long> done{0};
-        hipError_t e2 = ensure_lds_limit((const void *)split_gemm_f32_kernel<BCOL, D, WI, P>,
-                                         gemm_lds_bytes<D, WI, P>(), done);
+        hipError_t e2 = ensure_lds_limit((const void *)split_gemm_f32_kernel<BCOL, D, WI, P, BF>,
+                                         gemm_lds_bytes<D, WI, P, BF>(), done);
         if (e2 != hipSuccess) return e2;
-        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, D, WI, P>), dim3((unsigned)grid), dim3(64 * WI * kWJ),
-                           (gemm_lds_bytes<D, WI, P>()), s, q);
+        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, D, WI, P, BF>), dim3((unsigned)grid), dim3(64 * WI * kWJ),
+                           (gemm_lds_bytes<D, WI, P, BF>()), s, q);
         return hipSuccess;
     };
     using T_ = std::true_type;
     using F_ = std::false_type;
     using W2 = std::integral_constant<int, kWI>;
     using W4 = std::integral_constant<int, 4>;
+    auto go = [&](auto dma_tag, auto wi_tag, auto pipe_tag) {
+        return bf ? go1(dma_tag, wi_tag, pipe_tag, T_{}) : go1(dma_tag, wi_tag, pipe_tag, F_{});
+    };
     e = wide ? (t.pipe ? go(T_{}, W4{}, T_{}) : go(T_{}, W4{}, F_{})) : dma ? go(T_{}, W2{}, F_{})
                                                                            : go(F_{}, W2{}, F_{});
     if (e != hipSuccess) return e;
@@ -938,29 +1025,32 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
 }
 
 // rowmax_done: F2's and F1's row maxima are already in w.mxA / w.mxA2 (computed by the fold
-// launch's appended workgroups).
+// launch's appended workgroups).  bf: the bf16x6 GEMMs (no maxima at all).
 hipError_t bwd_split_gemms(const float *grad_c, const float *f1, int NQ, const float *f2, int B, int D, int H, int W,
-                           float *df1, float *df2, const BwdWs &w, hipStream_t s, bool rowmax_done = false) {
+                           float *df1, float *df2, const BwdWs &w, hipStream_t s, bool rowmax_done = false,
+                           bool bf = false) {
     const int N = H * W;
     const float sD = std::sqrt((float)D);
     hipError_t e;
 #define CK_(x)                          \
     if ((e = (x)) != hipSuccess) return e;
-    if (!rowmax_done) CK_(rowmax2(f2, N, w.mxA, f1, NQ, w.mxA2, B, D, s));
+    if (!rowmax_done && !bf) CK_(rowmax2(f2, N, w.mxA, f1, NQ, w.mxA2, B, D, s));
     // dF1 = F2 . dC^T : A = F2 rows d (k = m), B = dC rows n (k = m)
-    CK_(gemm_f32<false>(f2, (long)D * N, N, grad_c, (long)NQ * N, N, 1, w.mxA, w.mxB, B, D, NQ, N, sD, df1, w.slab, s));
+    CK_(gemm_f32<false>(f2, (long)D * N, N, grad_c, (long)NQ * N, N, 1, w.mxA, w.mxB, B, D, NQ, N, sD, df1, w.slab, s,
+                        GemmTune{}, bf));
     // dF2 = F1 . dC : A = F1 rows d (k = n), B = dC columns m (k = n)
     CK_(gemm_f32<true>(f1, (long)D * NQ, NQ, grad_c, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, df2, w.slab,
-                       s));
+                       s, GemmTune{}, bf));
 #undef CK_
     return hipSuccess;
 }
 
-// grad_c [B][NQ][N]; f1 [B][D][NQ]; f2 [B][D][N].
+// grad_c [B][NQ][N]; f1 [B][D][NQ]; f2 [B][D][N].  bf: the bf16x6 GEMMs (no maxima pass).
 hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, const float *f2, int B, int D, int H,
-                                  int W, float *df1, float *df2, void *ws, hipStream_t s) {
+                                  int W, float *df1, float *df2, void *ws, hipStream_t s, bool bf) {
     const int N = H * W;
     const BwdWs w = carve(ws, B, D, NQ, N);
+    if (bf) return bwd_split_gemms(grad_c, f1, NQ, f2, B, D, H, W, df1, df2, w, s, true, true);
     hipError_t e = hipMemsetAsync(w.mx0, 0, w.mx_bytes, s);
     if (e == hipSuccess) e = absmax(grad_c, B, NQ, N, w.mxB, w.mxC, s);  // one pass: dC row and column maxima
     if (e != hipSuccess) return e;
@@ -971,6 +1061,7 @@ hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, 
 // column maxima ([B][groups][H*W] floats, 256-B aligned after the GEMM workspace).
 size_t backward_workspace(int algo, int B, int D, int NQ, int H, int W, int radius) {
     if (algo == CORR_BUILD_FP32) return build_bwd_workspace(B, D, NQ, H, W);
+    if (algo == CORR_BUILD_BF16X6) return build_bwd_split_workspace(B, D, NQ, H, W);
     if (algo != CORR_BUILD_F16X3) return (size_t)-1;
     const size_t base = (build_bwd_split_workspace(B, D, NQ, H, W) + 255) / 256 * 256;
     return base + (size_t)B * std::max(1, lookup_bwd_fold_groups(NQ, radius)) * H * W * sizeof(float);
@@ -1029,6 +1120,9 @@ hipError_t launch_backward(int algo, const float *const *coords, const float *co
         e = launch_lookup_bwd_fold(coords, grad_out, T, B, NQ, H, W, levels, radius, gpyr.p[0], rmax, cmax, cpart, s,
                                    rm);
         if (e == hipSuccess) {
+            if (algo == CORR_BUILD_BF16X6)
+                return bwd_split_gemms(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, carve(ws, B, D, NQ, N), s, true,
+                                       true);
             if (algo == CORR_BUILD_F16X3) {
                 hipLaunchKernelGGL(colmax_reduce_kernel, dim3((unsigned)((N + kCmCols - 1) / kCmCols), (unsigned)B),
                                    dim3(kCmCols * kCmSlices), 0, s, cpart, G, N, cmax);
@@ -1042,6 +1136,11 @@ hipError_t launch_backward(int algo, const float *const *coords, const float *co
     }
     e = launch_lookup_bwd_multi(coords, grad_out, T, B, NQ, H, W, levels, radius, gpyr, s);
     if (e != hipSuccess) return e;
+    if (algo == CORR_BUILD_BF16X6) {
+        e = launch_pool_fold(gpyr, B, NQ, H, W, levels, nullptr, D, s);
+        if (e != hipSuccess) return e;
+        return bwd_split_gemms(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, carve(ws, B, D, NQ, H * W), s, true, true);
+    }
     if (algo == CORR_BUILD_F16X3) {
         e = launch_pool_fold(gpyr, B, NQ, H, W, levels, ws, D, s);
         if (e != hipSuccess) return e;

@@ -74,7 +74,7 @@ hipError_t launch_splitk_reduce(const float *ws, float *C, int splits, size_t pe
                                 bool vec4 = true);
 size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W);
 hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, const float *f2, int B, int D, int H,
-                                  int W, float *df1, float *df2, void *ws, hipStream_t s);
+                                  int W, float *df1, float *df2, void *ws, hipStream_t s, bool bf);
 hipError_t launch_convex_upsample(const float *flow, const float *mask, int N, int h, int w, float *out,
                                   hipStream_t s);
 size_t convex_upsample_bwd_workspace(int N, int h, int w);

@@ -53,10 +53,10 @@ def default_algo() -> int:
 
 
 def backward_algo(algo=None) -> int:
-    """The backward GEMMs' algorithm for a build algorithm: the f16x3 split GEMMs serve the
-    f16x3 and bf16x6 builds, the fp32 GEMMs the fp32 build."""
-    algo = default_algo() if algo is None else algo
-    return BUILD_FP32 if algo == BUILD_FP32 else BUILD_F16X3
+    """The backward GEMMs' algorithm for a build algorithm: each build's own arithmetic (bf16x6:
+    the exact three-piece bf16 split GEMMs, no narrower than fp32; f16x3: the two-piece f16 split;
+    fp32: the fp32-operand MFMA GEMMs)."""
+    return default_algo() if algo is None else algo
 
 _lib = None
 
@@ -253,7 +253,7 @@ def pool_bwd(grad_levels, H, W):
 def build_bwd(grad_c, fmap1, fmap2, algo=None):
     """Returns (dfmap1, dfmap2) for grad_c = dLoss/dcorr ([B*NQ, H*W] or any view of it).
     With a row slab fmap1, dfmap1 is the slab's and dfmap2 is this slab's partial sum.
-    algo: BUILD_F16X3 (default, see backward_algo) or BUILD_FP32 (corr_build_bwd_ex)."""
+    algo: BUILD_BF16X6 (default, see backward_algo), BUILD_F16X3 or BUILD_FP32 (corr_build_bwd_ex)."""
     algo = backward_algo() if algo is None else algo
     B, D, H, W = fmap2.shape
     for t, nm in ((grad_c, "grad_c"), (fmap1, "fmap1"), (fmap2, "fmap2")):

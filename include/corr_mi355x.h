@@ -43,7 +43,9 @@ extern "C" {
  *        corr_lookup_conv_weights (it was an fp32 [L*K][256] transpose under 101); callers
  *        built against 101 must check this version before calling it.
  *   103: CORR_BUILD_BF16X6, corr_build_region, corr_lookup_conv_bwd (the packed weight buffer
- *        grew: size it with corr_lookup_conv_weights_bytes()). */
+ *        grew: size it with corr_lookup_conv_weights_bytes()).
+ *   104: corr_build_bwd_ex / corr_backward accept CORR_BUILD_BF16X6 (backward GEMMs no narrower
+ *        than fp32); E-RAFT's default backward for the BF16X6 build. */
 int corr_version(void);
 
 /* Thread-local description of the last error on this thread ("" if none). */
@@ -69,10 +71,11 @@ int corr_build(const float *fmap1, const float *fmap2, int B, int D, int H, int 
  *                     lo (bf16 keeps fp32's exponent range: no scale, no flush — the one floor
  *                     is lo's bf16 subnormal range, |x| < ~2^-110); six bf16 MFMAs per product
  *                     (every piece pair of weight >= 2^-16: lo*hi + hi*lo + mid*mid + mid*hi +
- *                     hi*mid + hi*hi) into one fp32 accumulator.  The dropped terms are <= 2^-23
- *                     of |x_t x_q| and the accumulator rounds 6D/32 times per dot product (an fp32
- *                     fmaf chain: D times): no narrower than CORR_BUILD_FP32 (checked per query
- *                     row against an fp64 oracle).  Needs a workspace for the split operands.
+ *                     hi*mid + hi*hi) into two fp32 accumulators (hi*hi; the five smaller ones),
+ *                     added once.  The dropped terms are <= 2^-23 of |x_t x_q| and the main
+ *                     accumulator rounds D/32 times per dot product (an fp32 fmaf chain: D
+ *                     times): no narrower than CORR_BUILD_FP32 (checked per query row against
+ *                     an fp64 oracle).  Needs a workspace for the split operands.
  *                     ~2x faster than CORR_BUILD_FP32 on gfx950.
  *   CORR_BUILD_F16X3  each fp32 feature x of pixel n is split as 2^e_n * (hi + lo), f16 hi/lo,
  *                     e_n putting the pixel's largest |x| in [2^14, 2^15); three f16 MFMAs
@@ -185,9 +188,15 @@ int corr_build_bwd_rows(const float *grad_c, const float *fmap1_rows, int NQ, co
 /*
  * Backward GEMMs with an explicit algorithm (the corr_build_ex counterpart of
  * corr_build_bwd_rows; same outputs and contract).  CORR_BUILD_FP32 is corr_build_bwd_rows;
- * CORR_BUILD_F16X3 packs F1, F2 (per feature row d) and dC (per query row for dfmap1, per
- * target column for dfmap2) as 2^e (hi + lo) f16 pairs and runs three f16 MFMAs per product
- * into fp32 accumulators, split-K partial sums reduced in split order (deterministic).
+ * CORR_BUILD_BF16X6 splits every element of F1 / F2 / dC EXACTLY into three bf16 pieces while
+ * staging it (no scales, no maxima; the one floor as for the build: |x| < ~2^-110) and runs the
+ * six piece products of weight >= 2^-16 per product on the bf16 MFMA into one fp32 accumulator
+ * (6 roundings per 16 k, an fp32 fmaf chain 16): no narrower than CORR_BUILD_FP32 (every element
+ * within (3 + 6 ceil(K/16) + splits) u sum|ab|; worst and mean row error below the fp32 GEMMs',
+ * checked against fp64).  CORR_BUILD_F16X3 packs F1, F2 (per feature row d) and dC (per query
+ * row for dfmap1, per target column for dfmap2) as 2^e (hi + lo) f16 pairs and runs three f16
+ * MFMAs per product (~2^-22 relative: narrower than fp32).  Split-K partial sums are reduced in
+ * split order (deterministic).
  * Workspace: corr_build_bwd_ex_workspace(algo, ...) bytes ((size_t)-1: unknown algo).
  * Replaces the autograd of model/corr.py:58-60 (bmm + division by sqrt(D)).
  */
@@ -212,7 +221,7 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
  *     workgroup's LDS image fits (levels <= 4, T <= 32, BQ = 64 / pow2ceil(2r+3) queries' maps of
  *     every level in 160 KiB: e.g. r = 4 up to 60x80 fmaps), the lookups and the fold run as ONE
  *     kernel whose gradient maps live in LDS and which writes only dC (plus dC's row maxima and
- *     per-workgroup column maxima for the F16X3 packs); otherwise corr_lookup_bwd_multi +
+ *     per-workgroup column maxima for the F16X3 packs; BF16X6 needs none); otherwise corr_lookup_bwd_multi +
  *     corr_pool_fold.  Both give the same bits.  Workspace: corr_backward_workspace (radius
  *     sizes the column-maxima partials).
  */

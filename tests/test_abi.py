@@ -35,7 +35,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 
 def test_version_and_workspace(lib):
-    assert lib.corr_version() == 103
+    assert lib.corr_version() == 104
     # DSEC: 256 x 4800 slabs; at least one slab, deterministic plan
     ws = lib.corr_build_bwd_workspace(1, 256, 60, 80)
     assert ws >= 256 * 4800 * 4 and ws % (256 * 4800 * 4) == 0
@@ -125,7 +125,7 @@ def test_build_algo_env(monkeypatch):
     from eraft_amd import _lib
     monkeypatch.delenv("ERAFT_AMD_BUILD", raising=False)
     assert _lib.default_algo() == _lib.BUILD_BF16X6
-    assert _lib.backward_algo() == _lib.BUILD_F16X3
+    assert _lib.backward_algo() == _lib.BUILD_BF16X6
     monkeypatch.setenv("ERAFT_AMD_BUILD", "fp32")
     assert _lib.default_algo() == _lib.BUILD_FP32
     assert _lib.backward_algo() == _lib.BUILD_FP32
@@ -146,6 +146,10 @@ def test_backward_workspace_and_validation(lib):
     assert ws >= lib.corr_build_bwd_ex_workspace(1, B, D, N, H, W) + B * (N // 4) * N * 4
     assert lib.corr_backward_workspace(0, B, D, N, H, W, r) == lib.corr_build_bwd_ex_workspace(0, B, D, N, H, W)
     assert lib.corr_backward_workspace(1, 0, D, N, H, W, r) == 0
+    # bf16x6 (algo 2): the GEMM slabs only (no maxima partials), as corr_build_bwd_ex's
+    assert lib.corr_backward_workspace(2, B, D, N, H, W, r) == lib.corr_build_bwd_ex_workspace(2, B, D, N, H, W)
+    assert lib.corr_backward_workspace(2, B, D, N, H, W, r) < ws
+    assert lib.corr_build_bwd_ex_workspace(3, B, D, N, H, W) == ctypes.c_size_t(-1).value
     ptrs = (ctypes.c_void_p * 1)(16)
     gp = (ctypes.c_void_p * 4)(16, 16, 16, 16)
     rc = lib.corr_backward(1, ptrs, ptrs, 1, 16, N, 16, B, D, H, W, 4, r, gp, 16, 16, 16, 4, None)

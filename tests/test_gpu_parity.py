@@ -382,6 +382,65 @@ def test_build_bf16x6_not_narrower_than_fp32(case):
     assert rel_bf.mean() <= rel_f32.mean()
 
 
+def _bwd_fp64(gc, f1, f2):
+    """fp64 restatement of autograd of corr.py:58-60: dF1 = F2 dC^T / sqrt(D), dF2 = F1 dC / sqrt(D)
+    and the same products of magnitudes (the a-priori error bound's sum |a b|)."""
+    B, D, H, W = f2.shape
+    N = H * W
+    c = gc.reshape(B, N, N).astype(np.float64)
+    a1, a2 = f1.reshape(B, D, N).astype(np.float64), f2.reshape(B, D, N).astype(np.float64)
+    s = np.sqrt(np.float64(D))
+    d1 = np.einsum("bdm,bnm->bdn", a2, c) / s
+    d2 = np.einsum("bdn,bnm->bdm", a1, c) / s
+    m1 = np.einsum("bdm,bnm->bdn", np.abs(a2), np.abs(c)) / s
+    m2 = np.einsum("bdn,bnm->bdm", np.abs(a1), np.abs(c)) / s
+    return d1, d2, m1, m2
+
+
+@pytest.mark.parametrize("case", ["gauss", "row_scales", "train"])
+def test_build_bwd_bf16x6_not_narrower_than_fp32(case):
+    """The backward GEMMs on bf16x6 (the default for the bf16x6 build: both operands split
+    exactly into three bf16 pieces while staging, six piece products, one accumulator) against
+    the fp32-operand MFMA GEMMs, both vs an fp64 restatement: every element is within the
+    a-priori bound (3 + 6 ceil(K/16) + 16) u sum|ab| (dropped piece products, one rounding per
+    MFMA, the split-K sum, the output) — about 0.38 K u against the K u of an fp32 fmaf chain —
+    and over the output rows (feature d) the worst and the mean row error are at most the fp32
+    GEMMs'.  Unlike the build (two accumulators), single rows are not dominated: with one
+    accumulator per register budget the per-row errors are two draws of similar rounding noise
+    (6 vs 8 roundings per 16 k), so a row can land above fp32's; the fraction is printed."""
+    from eraft_amd import _lib
+    B, D, H, W = {"gauss": (2, 64, 24, 32), "row_scales": (1, 96, 20, 24), "train": (1, 256, 36, 48)}[case]
+    N = H * W
+    f1, f2 = prng.gauss(171, (B, D, H, W)), prng.gauss(172, (B, D, H, W))
+    gc = prng.gauss(173, (B * N, N))
+    if case == "row_scales":  # dC rows and columns over 1e-6..1e6, feature rows over 1e-3..1e3
+        gc *= (10.0 ** ((prng.uniform(174, (B * N, 1)) - 0.5) * 12)).astype(np.float32)
+        gc *= (10.0 ** ((prng.uniform(175, (1, N)) - 0.5) * 12)).astype(np.float32)
+        f1 *= (10.0 ** ((prng.uniform(176, (B, D, 1, 1)) - 0.5) * 6)).astype(np.float32)
+        f2 *= (10.0 ** ((prng.uniform(177, (B, D, 1, 1)) - 0.5) * 6)).astype(np.float32)
+    d1, d2, m1, m2 = _bwd_fp64(gc, f1, f2)
+    tg, t1, t2 = (torch.from_numpy(x).to(DEV) for x in (gc, f1, f2))
+    out = {algo: [g.cpu().numpy().reshape(B, D, N).astype(np.float64) for g in _lib.build_bwd(tg, t1, t2, algo)]
+           for algo in (_lib.BUILD_BF16X6, _lib.BUILD_FP32)}
+    u = 2.0 ** -24
+    for k, (ref, mag) in enumerate(((d1, m1), (d2, m2))):
+        bf, f32 = out[_lib.BUILD_BF16X6][k], out[_lib.BUILD_FP32][k]
+        assert np.isfinite(bf).all()
+        K = N
+        bound = (3 + 6 * ((K + 15) // 16) + 16) * u * mag
+        assert (np.abs(bf - ref) <= bound).all(), (k, (np.abs(bf - ref) / np.maximum(bound, 1e-300)).max())
+        e_bf = np.abs(bf - ref).max(axis=2).ravel()
+        e_32 = np.abs(f32 - ref).max(axis=2).ravel()
+        scale = np.abs(ref).max(axis=2).ravel()
+        ok = scale > 0
+        rb, r32 = e_bf[ok] / scale[ok], e_32[ok] / scale[ok]
+        print(f"{case} dF{k + 1}: bf16x6 row error max {rb.max():.3e} mean {rb.mean():.3e}; "
+              f"fp32 max {r32.max():.3e} mean {r32.mean():.3e}")
+        dom = float(np.mean(e_bf <= e_32 + scale * 2.0 ** -23))
+        print(f"  rows at or below fp32's (+1 ulp): {dom:.3f}")
+        assert rb.max() <= r32.max() and rb.mean() <= r32.mean()
+
+
 def _bf16_to_f32(u16):
     return (u16.astype(np.uint32) << 16).view(np.float32)
 
@@ -523,7 +582,7 @@ def test_lookup_bwd_multi_and_fold_bitexact(T, B, H, W, L, r):
     assert bit_equal(got[0].cpu().numpy(), ref[0].cpu().numpy())
 
 
-@pytest.mark.parametrize("algo", ["f16x3", "fp32"])
+@pytest.mark.parametrize("algo", ["bf16x6", "f16x3", "fp32"])
 @pytest.mark.parametrize("B,D,H,W,L,r,T", [(2, 32, 18, 24, 4, 4, 5), (1, 20, 17, 23, 3, 3, 2), (8, 64, 36, 48, 4, 4, 12),
                                            (1, 16, 12, 16, 4, 4, 33), (1, 16, 60, 80, 4, 4, 3),
                                            (1, 16, 64, 96, 5, 2, 2), (1, 8, 120, 160, 4, 4, 2)])
@@ -597,7 +656,7 @@ def test_autograd_fused_backward_equals_per_lookup(monkeypatch):
 
 
 @pytest.mark.parametrize("B,D,H,W", [(1, 256, 60, 80), (2, 200, 16, 24), (2, 32, 18, 24), (1, 20, 17, 23), (8, 16, 12, 16)])
-@pytest.mark.parametrize("algo", ["f16x3", "fp32"])
+@pytest.mark.parametrize("algo", ["bf16x6", "f16x3", "fp32"])
 @pytest.mark.parametrize("spread", [False, True])
 def test_build_bwd_vs_oracle(B, D, H, W, algo, spread):
     """Backward GEMMs (both algorithms) vs the fp64-accumulating oracle.  spread: rows and
@@ -620,27 +679,32 @@ def test_build_bwd_vs_oracle(B, D, H, W, algo, spread):
     assert norm_rel(g2.cpu().numpy(), d2) < REL_TOL
 
 
-def test_build_bwd_special_rows_vs_oracle():
-    """The f16x3 backward GEMMs' exact staging path: waves that stage a row whose max is below
+@pytest.mark.parametrize("algo,tiny", [("f16x3", 1e-36), ("bf16x6", 1e-30), ("bf16x6", 1e150)])
+def test_build_bwd_special_rows_vs_oracle(algo, tiny):
+    """Special rows through the backward GEMMs.  f16x3: waves that stage a row whose max is below
     2^-112 (shift > 127: 2^s is not a float, so the split keeps ldexp) or whose max is inf (the
-    lo-half guard) take it; the others the fast one-multiply split.  dC rows / columns and fmap
-    feature rows at 1e-36, one inf and a few NaN entries, against the fp64 oracle: the same
-    non-finite pattern, and every finite output column / row within 1e-5 of its OWN scale (so
-    the tiny outputs are checked, not hidden under the global max)."""
+    lo-half guard) take the exact staging path; the others the fast one-multiply split.
+    bf16x6: no scales at all — dC rows / columns and feature rows at 1e-30 (above the split's
+    absolute floor of ~2^-110, where `lo` would leave the bf16 subnormal range), or (tiny > 1)
+    dC rows / columns at 1e18 with feature rows at 1e-20.  One inf and a few NaN entries in dC,
+    against the fp64 oracle: the same non-finite
+    pattern, and every finite output column / row within 1e-5 of its OWN scale (so the tiny
+    outputs are checked, not hidden under the global max)."""
     from eraft_amd import _lib
     B, D, H, W = 1, 64, 12, 16
     N = H * W
     f1, f2 = prng.gauss(21, (B, D, H, W)), prng.gauss(22, (B, D, H, W))
     gc = prng.gauss(23, (B * N, N))
-    gc[[5, 77, 150]] *= np.float32(1e-36)     # tiny dC rows (dF1 columns)
-    gc[:, [9, 100]] *= np.float32(1e-36)      # tiny dC columns (dF2 columns)
-    f1[0, 3] *= np.float32(1e-36)             # tiny feature rows of both operands
-    f2[0, 7] *= np.float32(1e-36)
+    sg, sf = (np.float32(tiny), np.float32(tiny)) if tiny < 1 else (np.float32(1e18), np.float32(1e-20))
+    gc[[5, 77, 150]] *= sg                    # scaled dC rows (dF1 columns)
+    gc[:, [9, 100]] *= sg                     # scaled dC columns (dF2 columns)
+    f1[0, 3] *= sf                            # scaled feature rows of both operands
+    f2[0, 7] *= sf
     gc[40, 60] = np.float32(np.inf)
     gc[120, [3, 4]] = np.float32(np.nan)
     d1, d2 = oracle.corr_bwd(gc.reshape(B * N, 1, H, W), f1, f2)
     g1, g2 = _lib.build_bwd(torch.from_numpy(gc).to(DEV), torch.from_numpy(f1).to(DEV),
-                            torch.from_numpy(f2).to(DEV), _lib.BUILD_F16X3)
+                            torch.from_numpy(f2).to(DEV), _lib._ALGOS[algo])
     g1, g2 = g1.cpu().numpy().reshape(D, N), g2.cpu().numpy().reshape(D, N)
     r1, r2 = np.asarray(d1).reshape(D, N), np.asarray(d2).reshape(D, N)
     for got, ref in ((g1, r1), (g2, r2)):

@@ -48,7 +48,7 @@ __global__ void maxdiff(const float *a, const float *b, size_t n, unsigned *dmax
 int main(int argc, char **argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 10;
     const int B = 8, D = 256, H = 36, W = 48, N = H * W, NQ = N;
-    float *f1, *f2, *dc, *o1, *o2, *r1, *r2;
+    float *f1, *f2, *dc, *o1, *o2, *r1, *r2, *b1, *b2;
     CK(hipMalloc(&f1, (size_t)B * D * N * 4));
     CK(hipMalloc(&f2, (size_t)B * D * N * 4));
     CK(hipMalloc(&dc, (size_t)B * NQ * N * 4));
@@ -56,6 +56,8 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&o2, (size_t)B * D * N * 4));
     CK(hipMalloc(&r1, (size_t)B * D * N * 4));
     CK(hipMalloc(&r2, (size_t)B * D * N * 4));
+    CK(hipMalloc(&b1, (size_t)B * D * N * 4));
+    CK(hipMalloc(&b2, (size_t)B * D * N * 4));
     hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f1, (size_t)B * D * N, 1u);
     hipLaunchKernelGGL(fill, dim3(1024), dim3(256), 0, 0, f2, (size_t)B * D * N, 2u);
     hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, dc, (size_t)B * NQ * N, 3u);
@@ -69,16 +71,22 @@ int main(int argc, char **argv) {
     CK(absmax(dc, B, NQ, N, w.mxB, w.mxC, 0));
     CK(rowmax2(f2, N, w.mxA, f1, NQ, w.mxA2, B, D, 0));
     const float sD = 16.0f;
-    auto g1 = [&](float *out, const GemmTune &t) {
-        return gemm_f32<false>(f2, (long)D * N, N, dc, (long)NQ * N, N, 1, w.mxA, w.mxB, B, D, NQ, N, sD, out, w.slab, 0, t);
+    // bf: the bf16x6 GEMMs (exact three-piece split, six products), checked against their own
+    // register-staged plan
+    auto g1 = [&](float *out, const GemmTune &t, bool bf = false) {
+        return gemm_f32<false>(f2, (long)D * N, N, dc, (long)NQ * N, N, 1, w.mxA, w.mxB, B, D, NQ, N, sD, out, w.slab, 0, t,
+                               bf);
     };
-    auto g2 = [&](float *out, const GemmTune &t) {
-        return gemm_f32<true>(f1, (long)D * NQ, NQ, dc, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, out, w.slab, 0, t);
+    auto g2 = [&](float *out, const GemmTune &t, bool bf = false) {
+        return gemm_f32<true>(f1, (long)D * NQ, NQ, dc, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, out, w.slab, 0, t,
+                              bf);
     };
     GemmTune ref;  // reference: register-staged, 128-row tiles, scalar reduce
     ref.dma = false, ref.wide = false, ref.reduce_vec4 = false;
     CK(g1(r1, ref));
     CK(g2(r2, ref));
+    CK(g1(b1, ref, true));
+    CK(g2(b2, ref, true));
     struct V {
         std::string name;
         std::function<hipError_t()> run;
@@ -95,6 +103,23 @@ int main(int argc, char **argv) {
         vs.push_back({"dF1 (rows) " + tag, [&, t] { return g1(o1, t); }, o1, r1, {}});
         vs.push_back({"dF2 (cols) " + tag, [&, t] { return g2(o2, t); }, o2, r2, {}});
     }
+    for (int cfg : {1, 2}) {
+        const std::string tag = std::string("bf16x6 ") + (cfg == 1 ? "256x256 tiles" : "256x256 pipelined");
+        GemmTune t;
+        t.pipe = cfg == 2;
+        vs.push_back({"dF1 (rows) " + tag, [&, t] { return g1(o1, t, true); }, o1, b1, {}});
+        vs.push_back({"dF2 (cols) " + tag, [&, t] { return g2(o2, t, true); }, o2, b2, {}});
+    }
+    for (int sp : {4, 6, 8, 12}) {  // bf16x6 split-K counts (the plan's is 9 at this shape)
+        GemmTune t;
+        t.pipe = false;
+        t.splits = sp;
+        const std::string tag = "bf16x6 256x256 splits " + std::to_string(sp);
+        vs.push_back({"dF1 (rows) " + tag, [&, t] { return g1(o1, t, true); }, o1, b1, {}});
+        vs.push_back({"dF2 (cols) " + tag, [&, t] { return g2(o2, t, true); }, o2, b2, {}});
+    }
+    vs.push_back({"bf16x6 ref vs f16x3 ref dF1", [&] { return g1(o1, ref, true); }, o1, r1, {}});
+    vs.push_back({"bf16x6 ref vs f16x3 ref dF2", [&] { return g2(o2, ref, true); }, o2, r2, {}});
     if (argc > 2) {  // only the variant named exactly argv[2] (PMC passes)
         std::vector<V> keep;
         for (auto &v : vs)
@@ -133,8 +158,9 @@ int main(int argc, char **argv) {
     for (auto &v : vs) {
         std::sort(v.us.begin(), v.us.end());
         const float med = v.us[v.us.size() / 2];
-        printf("%-32s median %8.2f us  min %8.2f us  %6.3f of 2.5 PF f16 pipe (x3)\n", v.name.c_str(), med, v.us[0],
-               3.0 * fl / (med * 1e-6) / 2.5e15);
+        const bool bf = v.name.find("bf16x6") != std::string::npos;
+        printf("%-32s median %8.2f us  min %8.2f us  %6.3f of 2.5 PF %s\n", v.name.c_str(), med, v.us[0],
+               (bf ? 6.0 : 3.0) * fl / (med * 1e-6) / 2.5e15, bf ? "bf16 pipe (x6)" : "f16 pipe (x3)");
     }
     return 0;
 }
