@@ -408,11 +408,15 @@ __device__ __forceinline__ void gemm_wait_vm_barrier() {
 // PIPE (DMA path): a 3-slot raw ring, so chunk k + 1 can be split while chunk k's MFMAs run.
 // BF: each stage holds (hi, mid) in the hi/lo layout plus a kTJ-row plane of the lo pieces (A
 // row i's in unit slot 2o, B row j's in slot 2o + 1), and there are no row exponents.
+// BF + PIPE: two staging stages and a 2-slot ring (chunk k + 1 split into the other stage while
+// chunk k's fragments are read and multiplied): 160 KiB at the 256-row tile.
+template <bool DMA, int WI = kWI, bool PIPE = false, bool BF = false>
+constexpr int gemm_stages() { return DMA && !(PIPE && BF) ? 1 : 2; }
 template <bool DMA, int WI = kWI, bool PIPE = false, bool BF = false>
 constexpr int gemm_lds_bytes() {
     constexpr int rows = 32 * kMI * WI + kTJ;
-    return (DMA ? 1 : 2) * (rows + (BF ? kTJ : 0)) * 4 * (int)sizeof(u32x4) + (BF ? 0 : rows * (int)sizeof(int)) +
-           (DMA ? (PIPE ? 3 : 2) * rows * kBK * (int)sizeof(float) : 0);
+    return gemm_stages<DMA, WI, PIPE, BF>() * (rows + (BF ? kTJ : 0)) * 4 * (int)sizeof(u32x4) +
+           (BF ? 0 : rows * (int)sizeof(int)) + (DMA ? (PIPE && !BF ? 3 : 2) * rows * kBK * (int)sizeof(float) : 0);
 }
 
 // DMA = true: the raw fp32 chunks arrive by LDS-DMA two chunks ahead (no register staging, so a
@@ -443,7 +447,7 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
     static_assert(TI <= kTJ, "the BF lo plane holds kTJ rows");
     extern __shared__ __attribute__((aligned(16))) u32x4 gemm_smem[];
     u32x4 *lds = gemm_smem;
-    int *lex = reinterpret_cast<int *>(gemm_smem + (DMA ? 1 : 2) * STG);
+    int *lex = reinterpret_cast<int *>(gemm_smem + gemm_stages<DMA, WI, PIPE, BF>() * STG);
     float *raw = reinterpret_cast<float *>(lex + (BF ? 0 : ROWS));
     int id = xcd_swizzle(blockIdx.x, gridDim.x);
     const int tj = id % p.tj;
@@ -767,7 +771,37 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
                 for (int t = 0; t < 8 * KO; ++t) rb0[t] = RB[(8 * boct0 + t) * kTJ + bcol];
             }
         };
-        if constexpr (!PIPE) {
+        if constexpr (PIPE && BF) {
+            // Chunk c: ring slot (c - kc0) & 1, staged into stage (c - kc0) & 1.  Iteration kc:
+            // one barrier (chunk kc + 1 landed; every wave done with iteration kc - 1, so stage
+            // st ^ 1 and ring slot st are free), chunk kc + 2's DMA into slot st, then one region
+            // holding chunk kc's fragment reads and MFMAs together with chunk kc + 1's split into
+            // stage st ^ 1.  Same splits, same MFMA order: the same bits as the other plans.
+            constexpr int G = 2 + PB;
+            if (kc0 < kc1) issue(kc0, 0);
+            if (kc0 + 1 < kc1) issue(kc0 + 1, 1);
+            if (kc0 < kc1) {
+                if (kc0 + 1 < kc1) wait_vmcnt_barrier<G>();
+                else wait_vmcnt_barrier<0>();
+                read_raw(0);
+                store_chunk(0, ra0, rb0, FM0{});
+            }
+            int kc = kc0;
+            for (; kc + 1 < kc1; ++kc) {
+                const int st = (kc - kc0) & 1;
+                wait_vmcnt_barrier<0>();
+                if (kc + 2 < kc1) issue(kc + 2, st);
+                Frags f;
+                frags(st, f);
+                read_raw(st ^ 1);
+                store_chunk(st ^ 1, ra0, rb0, FM0{});
+                mfmas(f);
+            }
+            if (kc < kc1) {  // the last chunk
+                __syncthreads();
+                mfma_chunk((kc - kc0) & 1);
+            }
+        } else if constexpr (!PIPE) {
             if (kc0 < kc1) issue(kc0, 0);
             if (kc0 + 1 < kc1) issue(kc0 + 1, 1);
             for (int kc = kc0; kc < kc1; ++kc) {
