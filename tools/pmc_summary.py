@@ -17,9 +17,16 @@ KERNELS = ("lookup_conv_bwd_dw_kernel", "lookup_conv_bwd_dlk_kernel", "lookup_co
            "split_convert_cols_kernel", "absmax_kernel", "split_gemm_f32_kernel", "colmax_reduce_kernel")
 
 
+# Kernels whose template instantiations are reported apart (e.g. the f16x3 and bf16x6 GEMMs).
+BY_TEMPLATE = ("split_gemm_f32_kernel",)
+
+
 def short(name):
     for k in KERNELS:
         if k in name:
+            if k in BY_TEMPLATE and k + "<" in name:
+                i = name.index(k + "<") + len(k)
+                return k + name[i:name.index(">", i) + 1]
             return k
     return None
 
