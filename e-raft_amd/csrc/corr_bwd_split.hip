@@ -385,7 +385,33 @@ struct FGemmParams {
     int ti, tj, splits, kc_per;
     float alpha;
     int direct, vec;  // vec: 16-B loads legal (strides / bases / K multiples of 4)
+    // Tail reduce: the previous GEMM's ordered split-K sum (splitk_reduce_vec4_kernel's
+    // arithmetic), run by `tail_wgs` extra workgroups appended after the `gemm_wgs` GEMM ones —
+    // they land on the CUs the GEMM's grid leaves idle.  tail_wgs = 0: none.
+    const float4 *tail_ws;
+    float4 *tail_C;
+    size_t tail_per4;
+    int tail_splits, tail_exact, tail_wgs, gemm_wgs;
+    float tail_alpha, tail_s;
 };
+
+// The tail reduce's share of workgroup t of p.tail_wgs (bit-identical to the separate reduce).
+template <int NT>
+__device__ __forceinline__ void gemm_tail_reduce(const FGemmParams &p, int t) {
+    for (size_t i = (size_t)t * NT + threadIdx.x; i < p.tail_per4; i += (size_t)p.tail_wgs * NT) {
+        float4 acc = p.tail_ws[i];
+        for (int k = 1; k < p.tail_splits; ++k) {
+            const float4 v = p.tail_ws[(size_t)k * p.tail_per4 + i];
+            acc.x = acc.x + v.x, acc.y = acc.y + v.y, acc.z = acc.z + v.z, acc.w = acc.w + v.w;
+        }
+        if (p.tail_exact)
+            acc.x = acc.x * p.tail_alpha, acc.y = acc.y * p.tail_alpha, acc.z = acc.z * p.tail_alpha,
+            acc.w = acc.w * p.tail_alpha;
+        else
+            acc.x = acc.x / p.tail_s, acc.y = acc.y / p.tail_s, acc.z = acc.z / p.tail_s, acc.w = acc.w / p.tail_s;
+        p.tail_C[i] = acc;
+    }
+}
 
 typedef __attribute__((address_space(3))) void gemm_lds_t;
 
@@ -449,7 +475,11 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
     u32x4 *lds = gemm_smem;
     int *lex = reinterpret_cast<int *>(gemm_smem + gemm_stages<DMA, WI, PIPE, BF>() * STG);
     float *raw = reinterpret_cast<float *>(lex + (BF ? 0 : ROWS));
-    int id = xcd_swizzle(blockIdx.x, gridDim.x);
+    if ((int)blockIdx.x >= p.gemm_wgs) {  // appended tail-reduce workgroups
+        gemm_tail_reduce<NT>(p, (int)blockIdx.x - p.gemm_wgs);
+        return;
+    }
+    int id = xcd_swizzle(blockIdx.x, p.gemm_wgs);
     const int tj = id % p.tj;
     id /= p.tj;
     const int ti = id % p.ti;
@@ -940,10 +970,12 @@ struct BwdWs {
     unsigned *mxA, *mxB, *mxC, *mxA2;  // row max of F2, of dC rows, column max of dC, row max of F1
     unsigned *mx0;                     // start of the four (contiguous, zeroed once per call)
     size_t mx_bytes;
-    float *slab;                       // split-K partial sums
+    float *slab, *slab2;               // split-K partial sums of dF1 and dF2
 };
 
-// The maxima (B rows up to max(N, NQ)), then the split-K slabs.
+size_t slab_floats(int B, int D, int NQ, int N, const GemmTune &t);
+
+// The maxima (B rows up to max(N, NQ)), then the split-K slabs of dF1 and of dF2.
 BwdWs carve(void *ws, int B, int D, int NQ, int N) {
     const size_t R = std::max(NQ, N);
     char *w = (char *)ws;
@@ -958,10 +990,11 @@ BwdWs carve(void *ws, int B, int D, int NQ, int N) {
     w += al256((size_t)B * D * 4);
     r.mx_bytes = (size_t)(w - (char *)r.mx0);
     r.slab = (float *)w;
+    r.slab2 = (float *)(w + al256(slab_floats(B, D, NQ, N, GemmTune{}) * sizeof(float)));
     return r;
 }
 
-size_t slab_floats(int B, int D, int NQ, int N, const GemmTune &t = GemmTune{}) {
+size_t slab_floats(int B, int D, int NQ, int N, const GemmTune &t) {
     const int K1 = (N + kBK - 1) / kBK, K2 = (NQ + kBK - 1) / kBK;
     const size_t s1 = (size_t)plan_split_k(D, NQ, K1, B, t) * B * D * NQ;
     const size_t s2 = (size_t)plan_split_k(D, N, K2, B, t) * B * D * N;
@@ -990,7 +1023,8 @@ hipError_t rowmax2(const float *X0, int cols0, unsigned *rmax0, const float *X1,
 size_t bwd_split_workspace_tuned(int B, int D, int NQ, int H, int W, const GemmTune &t) {
     const int N = H * W;
     const size_t R = std::max(NQ, N);
-    return 2 * al256((size_t)B * D * 4) + 2 * al256((size_t)B * R * 4) + slab_floats(B, D, NQ, N, t) * sizeof(float);
+    return 2 * al256((size_t)B * D * 4) + 2 * al256((size_t)B * R * 4) +
+           al256(slab_floats(B, D, NQ, N, GemmTune{}) * sizeof(float)) + slab_floats(B, D, NQ, N, t) * sizeof(float);
 }
 
 size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W) {
@@ -1000,10 +1034,37 @@ size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W) {
 // The GEMMs once dC's row maxima (w.mxB) and column maxima (w.mxC) are in the workspace (f16x3;
 // bf: the exact bf16x6 split, no maxima read).
 // C[b] (NI x NJ) = A[b] B[b]^T / sqrt(D) straight from the fp32 operands (split while staging).
+// A GEMM's split-K sum not launched yet: the next GEMM runs it as appended tail workgroups
+// (vec4 layout only: per % 4 == 0, 16-B aligned slab and C).
+struct PendingReduce {
+    const float *ws = nullptr;
+    float *C = nullptr;
+    int splits = 0;
+    size_t per = 0;
+    float sD = 1.f;
+};
+
+inline int device_cus() {
+    static std::atomic<int> n{0};
+    int v = n.load(std::memory_order_relaxed);
+    if (v == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            v = 256;
+        n.store(v, std::memory_order_relaxed);
+    }
+    return v;
+}
+
+// defer: if non-null and the sum is vec4-able, it is returned there instead of launched; tail: a
+// previous GEMM's deferred sum, run by workgroups appended to this GEMM's grid (on the CUs its
+// tiles leave idle) — the same bits as the separate reduce either way.
 template <bool BCOL>
 hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long b_sb, long b_sr, long b_sk,
                     const unsigned *mxA, const unsigned *mxB, int B, int NI, int NJ, int K, float sD, float *C,
-                    float *slab, hipStream_t s, const GemmTune &t = GemmTune{}, bool bf = false) {
+                    float *slab, hipStream_t s, const GemmTune &t = GemmTune{}, bool bf = false,
+                    PendingReduce *defer = nullptr, const PendingReduce *tail = nullptr) {
     FGemmParams p{};
     p.A = A, p.a_sb = a_sb, p.a_sr = a_sr;
     p.Bm = Bm, p.b_sb = b_sb, p.b_sr = b_sr, p.b_sk = b_sk;
@@ -1035,12 +1096,29 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
         FGemmParams q = p;
         q.ti = (NI + 32 * kMI * WI - 1) / (32 * kMI * WI);
         const long grid = (long)q.ti * q.tj * q.splits * B;
+        q.gemm_wgs = (int)grid;
+        long tail_wgs = 0;
+        if (tail && tail->ws) {
+            // resident workgroups per CU: LDS-bound (160 KiB) and wave-bound (32 waves per CU)
+            constexpr int lds = gemm_lds_bytes<D, WI, P, BF>();
+            constexpr int per_cu = std::min(163840 / lds, 32 / (WI * kWJ));
+            const long slots = (long)device_cus() * per_cu, rem = grid % slots;
+            tail_wgs = rem && slots - rem >= 16 ? slots - rem : 32;
+            q.tail_ws = reinterpret_cast<const float4 *>(tail->ws);
+            q.tail_C = reinterpret_cast<float4 *>(tail->C);
+            q.tail_per4 = tail->per / 4;
+            q.tail_splits = tail->splits;
+            q.tail_exact = is_pow2(tail->sD) ? 1 : 0;
+            q.tail_alpha = 1.0f / tail->sD;
+            q.tail_s = tail->sD;
+            q.tail_wgs = (int)tail_wgs;
+        }
         static std::atomic<unsigned long long> done{0};
         hipError_t e2 = ensure_lds_limit((const void *)split_gemm_f32_kernel<BCOL, D, WI, P, BF>,
                                          gemm_lds_bytes<D, WI, P, BF>(), done);
         if (e2 != hipSuccess) return e2;
-        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, D, WI, P, BF>), dim3((unsigned)grid), dim3(64 * WI * kWJ),
-                           (gemm_lds_bytes<D, WI, P, BF>()), s, q);
+        hipLaunchKernelGGL((split_gemm_f32_kernel<BCOL, D, WI, P, BF>), dim3((unsigned)(grid + tail_wgs)),
+                           dim3(64 * WI * kWJ), (gemm_lds_bytes<D, WI, P, BF>()), s, q);
         return hipSuccess;
     };
     using T_ = std::true_type;
@@ -1055,7 +1133,12 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     if (e != hipSuccess) return e;
     e = hipGetLastError();
     if (e != hipSuccess || p.direct) return e;
-    return launch_splitk_reduce(slab, C, p.splits, (size_t)B * NI * NJ, sD, s, t.reduce_vec4);
+    const size_t per = (size_t)B * NI * NJ;
+    if (defer && t.reduce_vec4 && per % 4 == 0 && al16(slab) && al16(C)) {
+        defer->ws = slab, defer->C = C, defer->splits = p.splits, defer->per = per, defer->sD = sD;
+        return hipSuccess;
+    }
+    return launch_splitk_reduce(slab, C, p.splits, per, sD, s, t.reduce_vec4);
 }
 
 // rowmax_done: F2's and F1's row maxima are already in w.mxA / w.mxA2 (computed by the fold
@@ -1070,11 +1153,13 @@ hipError_t bwd_split_gemms(const float *grad_c, const float *f1, int NQ, const f
     if ((e = (x)) != hipSuccess) return e;
     if (!rowmax_done && !bf) CK_(rowmax2(f2, N, w.mxA, f1, NQ, w.mxA2, B, D, s));
     // dF1 = F2 . dC^T : A = F2 rows d (k = m), B = dC rows n (k = m)
+    // (its split-K sum deferred: dF2's grid carries it on the CUs its tiles leave idle)
+    PendingReduce pend;
     CK_(gemm_f32<false>(f2, (long)D * N, N, grad_c, (long)NQ * N, N, 1, w.mxA, w.mxB, B, D, NQ, N, sD, df1, w.slab, s,
-                        GemmTune{}, bf));
-    // dF2 = F1 . dC : A = F1 rows d (k = n), B = dC columns m (k = n)
-    CK_(gemm_f32<true>(f1, (long)D * NQ, NQ, grad_c, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, df2, w.slab,
-                       s, GemmTune{}, bf));
+                        GemmTune{}, bf, &pend));
+    // dF2 = F1 . dC : A = F1 rows d (k = n), B = dC columns m (k = n); its own slabs
+    CK_(gemm_f32<true>(f1, (long)D * NQ, NQ, grad_c, (long)NQ * N, 1, N, w.mxA2, w.mxC, B, D, N, NQ, sD, df2, w.slab2,
+                       s, GemmTune{}, bf, nullptr, &pend));
 #undef CK_
     return hipSuccess;
 }
