@@ -1098,12 +1098,16 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
         const long grid = (long)q.ti * q.tj * q.splits * B;
         q.gemm_wgs = (int)grid;
         long tail_wgs = 0;
-        if (tail && tail->ws) {
-            // resident workgroups per CU: LDS-bound (160 KiB) and wave-bound (32 waves per CU)
-            constexpr int lds = gemm_lds_bytes<D, WI, P, BF>();
-            constexpr int per_cu = std::min(163840 / lds, 32 / (WI * kWJ));
-            const long slots = (long)device_cus() * per_cu, rem = grid % slots;
-            tail_wgs = rem && slots - rem >= 16 ? slots - rem : 32;
+        // resident workgroups per CU: LDS-bound (160 KiB) and wave-bound (32 waves per CU)
+        constexpr int lds = gemm_lds_bytes<D, WI, P, BF>();
+        constexpr int per_cu = std::min(163840 / lds, 32 / (WI * kWJ));
+        const long slots = (long)device_cus() * per_cu;
+        if (tail && tail->ws && grid + 16 > slots) {
+            // no idle slots in the first round: the sum runs as its own launch, before this GEMM
+            hipError_t e3 = launch_splitk_reduce(tail->ws, tail->C, tail->splits, tail->per, tail->sD, s, true);
+            if (e3 != hipSuccess) return e3;
+        } else if (tail && tail->ws) {
+            tail_wgs = slots - grid;
             q.tail_ws = reinterpret_cast<const float4 *>(tail->ws);
             q.tail_C = reinterpret_cast<float4 *>(tail->C);
             q.tail_per4 = tail->per / 4;
