@@ -385,6 +385,7 @@ struct FGemmParams {
     int ti, tj, splits, kc_per;
     float alpha;
     int direct, vec;  // vec: 16-B loads legal (strides / bases / K multiples of 4)
+    int nt;           // non-temporal epilogue stores
     // Tail reduce: the previous GEMM's ordered split-K sum (splitk_reduce_vec4_kernel's
     // arithmetic), run by `tail_wgs` extra workgroups appended after the `gemm_wgs` GEMM ones —
     // they land on the CUs the GEMM's grid leaves idle.  tail_wgs = 0: none.
@@ -934,7 +935,10 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
                 const int i = i0 + il;
                 float x = BF ? acc[m][n][g] : ldexpf(acc[m][n][g], lex[il] + ej);
                 if (p.direct) x = x * p.alpha;
-                if (i < p.NI && j < p.NJ) C[(size_t)i * p.NJ + j] = x;
+                if (i < p.NI && j < p.NJ) {
+                    if (p.nt) __builtin_nontemporal_store(x, &C[(size_t)i * p.NJ + j]);
+                    else C[(size_t)i * p.NJ + j] = x;
+                }
             }
         }
     }
@@ -954,6 +958,7 @@ struct GemmTune {
     bool wide = true;        // 256 x 256 tiles of 8 waves on the DMA path when NI > 128
     bool reduce_vec4 = true; // the 16-B split-K reduce when aligned
     bool pipe = true;        // wide DMA path: split chunk k + 1 under chunk k's MFMAs (3-slot ring)
+    bool nt = true;          // non-temporal epilogue (slab / direct output) stores: ~1 us per GEMM, same bits
 };
 
 int plan_split_k(int NI, int NJ, int nkc, int batch, const GemmTune &t = GemmTune{}) {
@@ -1080,6 +1085,7 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     p.alpha = 1.0f / sD;
     p.direct = p.splits == 1 && exact;
     p.C = p.direct ? C : slab;
+    p.nt = t.nt ? 1 : 0;
     auto al16 = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
     p.vec = al16(A) && al16(Bm) && a_sb % 4 == 0 && a_sr % 4 == 0 && b_sb % 4 == 0 &&
             (BCOL ? b_sk % 4 == 0 : b_sr % 4 == 0);

@@ -192,7 +192,8 @@ struct LookupSmem {
 constexpr int lookup_threads(int S, int QB) { return (QB * S + 63) / 64 * 64; }
 
 // ABL: diagnostic ablations for tools/kbench_lookup.hip only (0 in the library): bit 0 = no
-// neighbourhood loads, bit 1 = no output stores, bit 2 = no coords load.
+// neighbourhood loads, bit 1 = no output stores, bit 2 = no coords load, bit 3 = plain (L2-cached)
+// output stores instead of the non-temporal ones (lookup_kernel).
 // One pyramid level of one block of QB queries (NT threads): the whole lookup of
 // lookup_kernel below.  emit(j, acc) receives output tap (i, j) of this thread's window column
 // i = tid / QB for query q = tid % QB (called only for live queries).  Shared by lookup_kernel
@@ -336,8 +337,13 @@ __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
     const int l = blockIdx.y;
     const int i = threadIdx.x / QB, n = n0 + threadIdx.x % QB;
     float *o = out + (((size_t)b * L + l) * K + (size_t)i * S) * N + n;
-    lookup_block<S, QB, NT, ABL>(sm, pyr.p[l], coords, b, n0, N, H, W, l, (int)threadIdx.x,
-                                 [&](int j, float acc) { o[(size_t)j * N] = acc; });
+    lookup_block<S, QB, NT, ABL>(sm, pyr.p[l], coords, b, n0, N, H, W, l, (int)threadIdx.x, [&](int j, float acc) {
+        // non-temporal: the output streams past L2 (nothing in this kernel re-reads it), so the
+        // kernel's end has no dirty lines of it to write back (DSEC 5.8 -> 5.4 us, train 12.2 ->
+        // 11.4 us, same bits; profiles/r04q_kbench_lookup_nt.txt)
+        if constexpr ((ABL & 8) != 0) o[(size_t)j * N] = acc;
+        else __builtin_nontemporal_store(acc, &o[(size_t)j * N]);
+    });
 }
 
 // Lookup fused with the consumer's 1x1 convolution (BasicMotionEncoder.convc1, update.py:68,75:
@@ -1239,7 +1245,8 @@ __device__ __forceinline__ void kernarg_lookup(int t, const float *&c, const flo
 }
 
 // PROBE (measurement builds only, tools/kbench_bwd.hip; the library uses 0): bit 0 = no lookup
-// loop, bit 1 = no fold (no dC / maxima), bit 2 = no LDS zero-init (wrong results, timing only).
+// loop, bit 1 = no fold (no dC / maxima), bit 2 = no LDS zero-init (wrong results, timing only),
+// bit 3 = plain (L2-cached) dC stores instead of the non-temporal ones.
 template <int S, int PROBE = 0>
 __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLookups lk, FusedOut o) {
     using ST = FusedStage<S>;
@@ -1521,8 +1528,13 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
                     cm[j] = fmaxf(cm[j], av);
                     rq[k] = fmaxf(rq[k], av);
                 }
-                *reinterpret_cast<float4 *>(o.dc + ((size_t)b * NQ + n0 + k) * N + m) =
-                    make_float4(res[0], res[1], res[2], res[3]);
+                // dC streams past the caches (non-temporal): same bits; in back-to-back launches of
+                // this kernel alone the upstream gradients then stay cache-resident (T = 12: 153 ->
+                // 135 us, profiles/r04q_kbench_bwd_nt.txt); in the training step, where the forward
+                // runs in between, neutral (corr_backward 336-337 us)
+                f32x4 *dst = reinterpret_cast<f32x4 *>(o.dc + ((size_t)b * NQ + n0 + k) * N + m);
+                if constexpr ((PROBE & 8) != 0) *dst = f32x4{res[0], res[1], res[2], res[3]};
+                else __builtin_nontemporal_store(f32x4{res[0], res[1], res[2], res[3]}, dst);
             }
             if (o.cpart)
                 *reinterpret_cast<float4 *>(o.cpart + ((size_t)b * nqb + (blk - b * nqb)) * N + m) =
@@ -1557,7 +1569,8 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
                     up = gv;
                     have = v > 0 && ((rc >> (v - 1)) & 1u);
                 }
-                o.dc[((size_t)b * NQ + n0 + k) * N + m] = up;
+                if constexpr ((PROBE & 8) != 0) o.dc[((size_t)b * NQ + n0 + k) * N + m] = up;
+                else __builtin_nontemporal_store(up, &o.dc[((size_t)b * NQ + n0 + k) * N + m]);
                 const float av = fabsf(up);
                 cm = fmaxf(cm, av);
                 rq[k] = fmaxf(rq[k], av);

@@ -89,16 +89,22 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL(fill_grid, dim3(256), dim3(256), 0, 0, cgrid, B, H, W);
     // lds > bytes: the same kernel with its LDS padded, i.e. fewer workgroups per CU (the
     // occupancy sensitivity of the lookup loop)
-    auto launch = [&](auto kern, int t_count, bool grid0 = false, size_t lds = 0) {
+    FusedOut onm = o;  // the bf16x6 backward's fold: dC only, no maxima
+    onm.rmax = nullptr, onm.cpart = nullptr;
+    auto launch = [&](auto kern, int t_count, bool grid0 = false, size_t lds = 0, const FusedOut *oo = nullptr) {
         BwdLookups l2 = lk;
         l2.T = t_count;
         if (grid0) l2.coords[0] = cgrid;
         const size_t b = lds ? lds : bytes;
         CK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b));
-        hipLaunchKernelGGL(kern, dim3((unsigned)(G * B)), dim3(64 * kFusedLv), b, 0, l2, o);
+        hipLaunchKernelGGL(kern, dim3((unsigned)(G * B)), dim3(64 * kFusedLv), b, 0, l2, oo ? *oo : o);
     };
     std::vector<V> vs;
     vs.push_back({"full T=12", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12); }, {}});
+    vs.push_back({"full T=12, no maxima (bf16x6)", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12, false, 0, &onm); }, {}});
+    vs.push_back({"full T=12, no maxima, cached dC", [&] { launch(lookup_bwd_fold_kernel<S, 8>, 12, false, 0, &onm); }, {}});
+    vs.push_back({"no lookups, no maxima", [&] { launch(lookup_bwd_fold_kernel<S, 1>, 12, false, 0, &onm); }, {}});
+    vs.push_back({"no lookups, no maxima, cached dC", [&] { launch(lookup_bwd_fold_kernel<S, 9>, 12, false, 0, &onm); }, {}});
     vs.push_back({"full T=1", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 1); }, {}});
     vs.push_back({"full T=12, 2 WG/CU (LDS padded to 64 KB)", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12, false, 64 * 1024); }, {}});
     vs.push_back({"full T=1, 2 WG/CU", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 1, false, 64 * 1024); }, {}});

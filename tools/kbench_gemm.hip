@@ -110,7 +110,14 @@ int main(int argc, char **argv) {
         vs.push_back({"dF1 (rows) " + tag, [&, t] { return g1(o1, t, true); }, o1, b1, {}});
         vs.push_back({"dF2 (cols) " + tag, [&, t] { return g2(o2, t, true); }, o2, b2, {}});
     }
-    for (int sp : {4, 6, 8, 12}) {  // bf16x6 split-K counts (the plan's is 9 at this shape)
+    for (int cfg : {0, 1}) {  // L2-cached epilogue stores (the default is non-temporal)
+        GemmTune t;
+        t.nt = false;
+        const std::string tag = cfg ? "bf16x6 pipelined cached slabs" : "f16x3 pipelined cached slabs";
+        vs.push_back({"dF1 (rows) " + tag, [&, t, cfg] { return g1(o1, t, cfg == 1); }, o1, cfg ? b1 : r1, {}});
+        vs.push_back({"dF2 (cols) " + tag, [&, t, cfg] { return g2(o2, t, cfg == 1); }, o2, cfg ? b2 : r2, {}});
+    }
+    for (int sp : {4, 6, 8, 12}) {  // bf16x6 split-K counts (the plan's is 4 at this shape)
         GemmTune t;
         t.pipe = false;
         t.splits = sp;

@@ -119,6 +119,8 @@ int main(int argc, char **argv) {
         vs.push_back({"prod grid (integer)", [=](float *o) { return launch_lookup(lp, coords_g, B, H * W, H, W, 4, 4, o, 0); }, {}});
         vs.push_back({"QB16 smooth-flow", [=](float *o) { return launch_qb<16>(lp, coords_s, B, H, W, o); }, {}});
         vs.push_back({"abl QB32 noload", [=](float *o) { return launch_qb<32, 1>(lp, coords, B, H, W, o); }, {}});
+        vs.push_back({"QB16 cached-stores", [=](float *o) { return launch_qb<16, 8>(lp, coords, B, H, W, o); }, {}});
+        vs.push_back({"QB32 cached-stores", [=](float *o) { return launch_qb<32, 8>(lp, coords, B, H, W, o); }, {}});
         CK(vs[0].launch(ref));
         for (auto &v : vs) {
             CK(hipMemset(out, 0, n_out * 4));
