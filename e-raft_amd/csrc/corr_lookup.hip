@@ -126,7 +126,7 @@ __device__ __forceinline__ void gather_window(float *win, const int *ax, const i
 // Forward gather: one wave per query at a time, lane -> fixed neighbourhood cells, so the
 // (row, col) of each lane's cells is computed once and every load's address is
 // anchor + constant (no per-element integer division).
-template <int S, int QB, int NT, bool NOLOAD = false>
+template <int S, int QB, int NT, bool NOLOAD = false, bool NTLOAD = false>
 __device__ __forceinline__ void gather_window_wave(float *win, const int *ax, const int *ay,
                                                    const float *P, size_t qbase, size_t mapsz,
                                                    int n0, int N, int Wl, int Hl, int tid) {
@@ -166,7 +166,8 @@ __device__ __forceinline__ void gather_window_wave(float *win, const int *ax, co
         for (int v = 0; v < EPL; ++v) {
             const int X = X0 + rx[v], Y = Y0 + ry[v];
             const bool ok = (lane + 64 * v < WS) && (unsigned)X < (unsigned)Wl && (unsigned)Y < (unsigned)Hl;
-            vals[k][v] = (ok && !NOLOAD) ? Pq[(unsigned)(Y * Wl + X)] : 0.0f;
+            if constexpr (NTLOAD) vals[k][v] = (ok && !NOLOAD) ? __builtin_nontemporal_load(&Pq[(unsigned)(Y * Wl + X)]) : 0.0f;
+            else vals[k][v] = (ok && !NOLOAD) ? Pq[(unsigned)(Y * Wl + X)] : 0.0f;
         }
     }
 #pragma unroll
@@ -193,7 +194,7 @@ constexpr int lookup_threads(int S, int QB) { return (QB * S + 63) / 64 * 64; }
 
 // ABL: diagnostic ablations for tools/kbench_lookup.hip only (0 in the library): bit 0 = no
 // neighbourhood loads, bit 1 = no output stores, bit 2 = no coords load, bit 3 = plain (L2-cached)
-// output stores instead of the non-temporal ones (lookup_kernel).
+// output stores instead of the non-temporal ones (lookup_kernel), bit 4 = non-temporal window loads.
 // One pyramid level of one block of QB queries (NT threads): the whole lookup of
 // lookup_kernel below.  emit(j, acc) receives output tap (i, j) of this thread's window column
 // i = tid / QB for query q = tid % QB (called only for live queries).  Shared by lookup_kernel
@@ -246,7 +247,8 @@ __device__ __forceinline__ void lookup_block_v(LookupSmem<S, QB> &sm, const floa
     }
 
     // ---- 2. neighbourhoods -> LDS ----
-    gather_window_wave<S, QB, NT, (ABL & 1) != 0>(sm.win, sm.ax, sm.ay, P, qbase, mapsz, n0, N, Wl, Hl, tid);
+    gather_window_wave<S, QB, NT, (ABL & 1) != 0, (ABL & 16) != 0>(sm.win, sm.ax, sm.ay, P, qbase, mapsz, n0, N, Wl, Hl,
+                                                                    tid);
     __syncthreads();
     const int mode = sm.flags;
     if (!act) return;

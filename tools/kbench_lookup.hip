@@ -121,6 +121,8 @@ int main(int argc, char **argv) {
         vs.push_back({"abl QB32 noload", [=](float *o) { return launch_qb<32, 1>(lp, coords, B, H, W, o); }, {}});
         vs.push_back({"QB16 cached-stores", [=](float *o) { return launch_qb<16, 8>(lp, coords, B, H, W, o); }, {}});
         vs.push_back({"QB32 cached-stores", [=](float *o) { return launch_qb<32, 8>(lp, coords, B, H, W, o); }, {}});
+        vs.push_back({"QB16 nt-loads", [=](float *o) { return launch_qb<16, 16>(lp, coords, B, H, W, o); }, {}});
+        vs.push_back({"QB32 nt-loads", [=](float *o) { return launch_qb<32, 16>(lp, coords, B, H, W, o); }, {}});
         CK(vs[0].launch(ref));
         for (auto &v : vs) {
             CK(hipMemset(out, 0, n_out * 4));
