@@ -1281,13 +1281,6 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     auto gg = [&](int k) -> float & { return st[ST::GG + k * BQ + q]; };
     unsigned *RM = reinterpret_cast<unsigned *>(fsm + o.aux + kFusedLv * ST::SIZE);  // [BQ]
 
-    if (!(PROBE & 4))
-        // every map of the workgroup, 16 B per store (o.aux is a multiple of 64 floats:
-        // BQ query strides of 64k + 64 / BQ)
-        for (int i = 4 * tid; i < o.aux; i += 4 * NT) *reinterpret_cast<float4 *>(fsm + i) = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (tid < BQ) RM[tid] = 0u;
-    __syncthreads();
-
     // the next lookup's coords and upstream gradients are loaded one lookup ahead (registers),
     // by buffer loads over batch item b's slice: every lane loads, and the lanes that own no
     // (tap, query) point past the slice, so the range check returns their zeros (no branch
@@ -1311,7 +1304,13 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         for (int u = 0; u < S; ++u)
             pv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, goff, u * NQ * 4, 0));
     };
-    if (act) prefetch(0);
+    if (act) prefetch(0);  // issued before the LDS zeroing, so its latency hides behind it
+    if (!(PROBE & 4))
+        // every map of the workgroup, 16 B per store (o.aux is a multiple of 64 floats:
+        // BQ query strides of 64k + 64 / BQ)
+        for (int i = 4 * tid; i < o.aux; i += 4 * NT) *reinterpret_cast<float4 *>(fsm + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < BQ) RM[tid] = 0u;
+    __syncthreads();
 
     for (int t = 0; !(PROBE & 1) && act && t < lk.T; ++t) {  // absent levels (l >= L) only join the fold
         // ---- 1. tap cx of both axes; the group's taps reach the other lanes by DPP ----
