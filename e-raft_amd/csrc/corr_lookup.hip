@@ -486,7 +486,7 @@ __global__ __launch_bounds__(kLcNT) void lookup_conv_kernel(ConstLevelPtrs pyr, 
                 const int o = 32 * w + 16 * t + 4 * (lane >> 4) + r;
                 float v = (acc[t][c][r] + acs[t][c][r]) + bias[o];
                 if (relu && v < 0.0f) v = 0.0f;  // torch.relu: a NaN stays a NaN (fmaxf would drop it)
-                out[((size_t)b * kLcO + o) * N + n] = v;
+                __builtin_nontemporal_store(v, &out[((size_t)b * kLcO + o) * N + n]);  // streams past L2
             }
     }
 }
@@ -676,7 +676,8 @@ __global__ __launch_bounds__(kCbNT) void lookup_conv_bwd_dlk_kernel(CbArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int c = 16 * cl + 4 * kg + i;
-                if (c < 81 && n < N) a.dlk[((size_t)b * a.C + 81 * l + c) * N + n] = acc[t][i] + acs[t][i];
+                if (c < 81 && n < N)  // non-temporal, as the lookup's output
+                    __builtin_nontemporal_store(acc[t][i] + acs[t][i], &a.dlk[((size_t)b * a.C + 81 * l + c) * N + n]);
             }
         }
     }
