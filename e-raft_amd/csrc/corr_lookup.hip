@@ -1617,11 +1617,12 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const float *__restrict__
 template <int S>
 hipError_t launch_lookup_s(const ConstLevelPtrs &pyr, const float *coords, int B, int NQ, int H,
                            int W, int L, float *out, hipStream_t s) {
-    // queries per workgroup: 32 (>= 2 workgroups per CU at DSEC size); 16 for r = 4 on maps of
-    // <= 2048 cells, where the smaller workgroups pack the CUs better (same bits; tools/kbench_lookup:
-    // train 36x48 12.5 vs 12.8 us, MVSEC 36x44 B16 19.6 vs 20.3, DSEC 60x80 equal, 1280x960 23.8
-    // vs 22.4)
-    if (S == 9 && H * W <= 2048) {
+    // queries per workgroup: 32; 16 for r = 4 on maps of <= 2048 cells with >= 20,000 queries in
+    // all, where the smaller workgroups pack the CUs better over several rounds (same bits;
+    // tools/kbench_lookup with the non-temporal output stores, profiles/r04t_kbench_lookup_qb2.txt:
+    // QB 16 / 32 = MVSEC 36x44 B16 19.0 / 19.6 us, B12 36x48 16.1 / 16.1; train B8 12.0 / 11.7,
+    // MVSEC crop 32x32 B16 12.3 / 11.3, DSEC 5.5 / 5.4, 1280x960 22.6 / 22.1)
+    if (S == 9 && H * W <= 2048 && (long)B * NQ >= 20000) {
         constexpr int QB = 16;
         const int nqb = (NQ + QB - 1) / QB;
         hipLaunchKernelGGL((lookup_kernel<S, QB>), dim3(nqb * B, L), dim3(lookup_threads(S, QB)), 0, s,
