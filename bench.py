@@ -110,6 +110,8 @@ def parse():
     ap.add_argument("--prefetch", action="store_true",
                     help="--sharded: instead of chunks, double-buffer whole fmap2s across pairs "
                          "(pair k+1's broadcast during pair k; eager)")
+    ap.add_argument("--no-sharded-leg", action="store_true",
+                    help="N > 1 dsec: skip the row-sharded 1280x960 leg reported beside the replica value")
     return ap.parse_args()
 
 
@@ -389,8 +391,45 @@ def build_roofline(algo, fl, bb, t_ms, traffic_b):
             "note": BUILD_NOTE[algo]}
 
 
+def spawn_ranks(n):
+    """`--gpus N` without a launcher: start N ranks of this script as child processes (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, rendezvous on 127.0.0.1), before
+    this process touches the GPU, and exit with the first failing rank's status.  Rank 0 prints
+    the one JSON line.  Equivalent to `python -m torch.distributed.run --nproc-per-node N`."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for i in range(n):
+        env = dict(os.environ, RANK=str(i), LOCAL_RANK=str(i), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in procs:  # a rank failed: the others would wait at a collective forever
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc if rc >= 0 else 128 - rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -410,19 +449,34 @@ def main():
 
     if args.workload == "e2e":
         run_e2e(args, world, rank, dev)
-        if world > 1:
-            dist.destroy_process_group()
-        return
+    else:
+        res = run_corr(args, args.workload, args.sharded, world, rank, dev)
+        if world > 1 and not args.sharded and args.workload == "dsec" and not args.no_sharded_leg:
+            # the north_star's scaling case beside the replica value: ONE 1280x960 pair row-sharded
+            # over the N ranks (chunked RCCL broadcast of fmap2, graph-captured), strong scaling
+            try:
+                leg = run_corr(args, "hires1280", True, world, rank, dev, primary=False)
+            except Exception as exc:  # noqa: BLE001 — the replica line above stands; say why the leg is missing
+                leg = {"error": f"{type(exc).__name__}: {exc}"}
+            if rank == 0:
+                res["sharded_hires1280"] = leg
+        if rank == 0:
+            print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
 
+
+def run_corr(args, wl_name, sharded, world, rank, dev, primary=True):
+    """One CorrBlock workload: returns the result dict on rank 0 (None elsewhere).  primary=False
+    (the sharded leg of an N > 1 run): no alternative builds, no CPU baseline."""
     from eraft_amd import CorrBlock, _lib
-    from eraft_amd.corr import _alloc_pyramid
+    from eraft_amd.corr import _alloc_grad_pyramid, _alloc_pyramid
 
     _lib.load()
-    wl = WORKLOADS[args.workload]
+    wl = WORKLOADS[wl_name]
     B, D, H, W, L, r, iters = wl
     K = (2 * r + 1) ** 2
-    train = args.workload in TRAIN_WORKLOADS
-    sharded = args.sharded
+    train = wl_name in TRAIN_WORKLOADS
     if sharded and train:
         raise SystemExit("--sharded times the forward path (build + lookups)")
     # sharded: every rank draws the same pair (same seed); rank 0's fmap2 is what the broadcast
@@ -481,7 +535,7 @@ def main():
     if train:
         # backward of the 12 lookups + pyramid + product (eraft.py:128 detaches coords)
         gouts = [torch.randn(B, L * K, H, W, device=dev, generator=g) for _ in range(iters)]
-        gpyr = _alloc_pyramid(B, H, W, L, f1, zero=True)
+        gpyr = _alloc_grad_pyramid(B, H, W, L, f1, zero=True)
         gbuf = gpyr[0]._base  # the one allocation behind every level view
         f1g = f1.clone().requires_grad_(True)
         f2g = f2.clone().requires_grad_(True)
@@ -525,12 +579,14 @@ def main():
             from eraft_amd.sharded import Fmap2DoubleBuffer, RowShardedCorrBlock
         if prefetch:
             dbuf = Fmap2DoubleBuffer(tuple(f2.shape), dev)
-            pipe["pending"] = dbuf.prefetch(f2 if rank == 0 else None)  # prologue: pair 0's fmap2
+            with torch.no_grad():  # the double buffer is inference-only
+                pipe["pending"] = dbuf.prefetch(f2 if rank == 0 else None)  # prologue: pair 0's fmap2
 
         def pair():
             if prefetch:
                 cur = pipe["pending"]
-                pipe["pending"] = dbuf.prefetch(f2 if rank == 0 else None)
+                with torch.no_grad():
+                    pipe["pending"] = dbuf.prefetch(f2 if rank == 0 else None)
                 blk = RowShardedCorrBlock(f1, cur, num_levels=L, radius=r, fmap1_is_slab=True)
                 for c in coords:
                     blk(c)
@@ -549,6 +605,7 @@ def main():
         # capture poisons the stream), so only an RCCL sharded pair is captured
         host_coll = sharded and world > 1 and dist.get_backend() != "nccl"
         launch = "eager" if args.eager or prefetch or host_coll else "hipgraph"
+        capture_error = None
         step = pair
         if train:
             step = autograd_step
@@ -563,6 +620,7 @@ def main():
                     step = g_step.replay
             except Exception as exc:  # noqa: BLE001 — report and stay eager
                 print(f"train: graph capture of the autograd step failed ({exc}); eager", file=sys.stderr)
+                capture_error = f"{type(exc).__name__}: {exc}"
                 launch = "eager"
                 step = autograd_step
         elif launch == "hipgraph":
@@ -577,6 +635,7 @@ def main():
                 if not sharded:
                     raise
                 print(f"sharded: graph capture failed ({exc}); eager", file=sys.stderr)
+                capture_error = f"{type(exc).__name__}: {exc}"
                 launch = "eager"
                 step = pair
 
@@ -602,7 +661,7 @@ def main():
         # (CorrBlock ctor: pyramid + workspace allocation, then 12 __call__s), reported beside
         # `value` — same K steps after W warmups, HIP graphs unless --eager
         alt_values = {}
-        if not train and not sharded:
+        if primary and not train and not sharded:
             def timed(fn):
                 st = fn
                 if launch == "hipgraph":
@@ -635,8 +694,8 @@ def main():
             pack_ms = mfma_ms = None
             build_ms = build_call_ms
         look_ms = graph_time_ms(run_lookups, stream) / iters
-        fp32_ms = graph_time_ms(build_fp32, stream, rep=4) if algo != _lib.BUILD_FP32 else None
-        x3_ms = graph_time_ms(build_f16x3, stream, rep=4) if algo == _lib.BUILD_BF16X6 else None
+        fp32_ms = graph_time_ms(build_fp32, stream, rep=4) if primary and algo != _lib.BUILD_FP32 else None
+        x3_ms = graph_time_ms(build_f16x3, stream, rep=4) if primary and algo == _lib.BUILD_BF16X6 else None
         bwd_ms = graph_time_ms(run_bwd_kernels, stream, rep=4) if train else None
         bwd_staged_ms = graph_time_ms(run_bwd_staged, stream, rep=4) if train else None
         bwd_x3_ms = graph_time_ms(run_bwd_f16x3, stream, rep=4) if train and algo == _lib.BUILD_BF16X6 else None
@@ -678,7 +737,6 @@ def main():
     hbm_gbs = (bb + iters * lb) / (build_ms + iters * look_ms) / 1e6
 
     if rank == 0:
-        wl_name = args.workload
         res = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -757,14 +815,15 @@ def main():
                             "chunk's pyramid rows are built (corr_build_region) as soon as it has arrived") +
                            "; per-rank broadcast_ms is the whole broadcast timed alone",
                 "backend": os.environ.get("ERAFT_AMD_DIST_BACKEND", "nccl")}
-        if world == 1 and not args.no_cpu_baseline and wl_name not in CPU_SKIP:
+        if capture_error is not None:
+            res["capture_error"] = capture_error
+        if primary and world == 1 and not args.no_cpu_baseline and wl_name not in CPU_SKIP:
             cb = cpu_baseline(wl, args.cpu_seconds, train)
             res["cpu_baseline"] = cb
             res["speedup_vs_cpu"] = round(value / cb["value"], 1)
             res["cpu_baseline_1thread"] = cpu_baseline(wl, args.cpu_seconds * 0.75, train, threads=1)
-        print(json.dumps(res))
-    if world > 1:
-        dist.destroy_process_group()
+        return res
+    return None
 
 
 if __name__ == "__main__":

@@ -65,6 +65,16 @@ static int check_levels(const char *fn, P *const *src, int levels, const char *n
     return CORR_OK;
 }
 
+// Value pyramids (tiled, corr_common.h): 16-B tile rows, so 16-B aligned level bases.
+template <class P>
+static int check_pyramid(const char *fn, P *const *src, int levels, const char *name, P **dst) {
+    int rc = check_levels(fn, src, levels, name, dst);
+    if (rc) return rc;
+    for (int l = 0; l < levels; ++l)
+        if ((uintptr_t)src[l] % 16) return fail(CORR_EINVAL, "%s: %s[%d] is not 16-byte aligned", fn, name, l);
+    return CORR_OK;
+}
+
 static int check_radius(const char *fn, int radius) {
     if (radius < 0 || radius > CORR_MAX_RADIUS)
         return fail(CORR_EINVAL, "%s: radius must be in [0, %d] (got %d)", fn, CORR_MAX_RADIUS, radius);
@@ -77,9 +87,40 @@ using namespace corr;
 
 extern "C" {
 
-int corr_version(void) { return 104; }
+int corr_version(void) { return 200; }
 
 const char *corr_last_error(void) { return g_err; }
+
+size_t corr_map_floats(int Hl, int Wl) {
+    if (Hl < 1 || Wl < 1) return 0;
+    return map_floats(Hl, Wl);
+}
+
+int corr_pyramid_export(const float *const *pyr, int BN, int H, int W, int levels, float *const *out, void *stream) {
+    static const char *fn = "corr_pyramid_export";
+    g_err[0] = 0;
+    int rc = check_dims(fn, 1, 1, H, W, levels);
+    if (rc) return rc;
+    if (BN < 1) return fail(CORR_EINVAL, "%s: BN must be >= 1", fn);
+    ConstLevelPtrs src{};
+    LevelPtrs dst{};
+    if ((rc = check_pyramid(fn, pyr, levels, "pyr", src.p)) || (rc = check_levels(fn, out, levels, "out", dst.p)))
+        return rc;
+    return hip_status(launch_pyramid_export(src, BN, H, W, levels, dst, (hipStream_t)stream), fn);
+}
+
+int corr_pyramid_import(const float *const *src, int BN, int H, int W, int levels, float *const *pyr, void *stream) {
+    static const char *fn = "corr_pyramid_import";
+    g_err[0] = 0;
+    int rc = check_dims(fn, 1, 1, H, W, levels);
+    if (rc) return rc;
+    if (BN < 1) return fail(CORR_EINVAL, "%s: BN must be >= 1", fn);
+    ConstLevelPtrs s{};
+    LevelPtrs dst{};
+    if ((rc = check_levels(fn, src, levels, "src", s.p)) || (rc = check_pyramid(fn, pyr, levels, "pyr", dst.p)))
+        return rc;
+    return hip_status(launch_pyramid_import(s, BN, H, W, levels, dst, (hipStream_t)stream), fn);
+}
 
 int corr_build_rows(const float *fmap1_rows, int NQ, const float *fmap2, int B, int D, int H,
                     int W, int levels, float *const *pyr, void *stream) {
@@ -90,7 +131,7 @@ int corr_build_rows(const float *fmap1_rows, int NQ, const float *fmap2, int B, 
     if (D < 1) return fail(CORR_EINVAL, "%s: D must be >= 1 (got %d)", fn, D);
     if ((rc = check_ptr(fn, fmap1_rows, "fmap1")) || (rc = check_ptr(fn, fmap2, "fmap2"))) return rc;
     LevelPtrs lp{};
-    if ((rc = check_levels(fn, pyr, levels, "pyr", lp.p))) return rc;
+    if ((rc = check_pyramid(fn, pyr, levels, "pyr", lp.p))) return rc;
     return hip_status(launch_build(fmap1_rows, NQ, fmap2, B, D, H, W, levels, lp, (hipStream_t)stream), fn);
 }
 
@@ -126,7 +167,7 @@ int corr_build_ex(int algo, const float *fmap1_rows, int NQ, const float *fmap2,
     if (workspace_bytes < need || !workspace)
         return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
     LevelPtrs lp{};
-    if ((rc = check_levels(fn, pyr, levels, "pyr", lp.p))) return rc;
+    if ((rc = check_pyramid(fn, pyr, levels, "pyr", lp.p))) return rc;
     const int part = phase == CORR_BUILD_ONLY_PACK ? 1 : phase == CORR_BUILD_ONLY_MFMA ? 2 : 0;
     if (bf)
         return hip_status(
@@ -155,7 +196,7 @@ int corr_build_region(int algo, const float *fmap1_rows, int NQ, const float *fm
     if (workspace_bytes < need || !workspace)
         return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
     LevelPtrs lp{};
-    if ((rc = check_levels(fn, pyr, levels, "pyr", lp.p))) return rc;
+    if ((rc = check_pyramid(fn, pyr, levels, "pyr", lp.p))) return rc;
     return hip_status(launch_build_bf16_region(fmap1_rows, NQ, fmap2_rows, y0, y1, B, D, H, W, levels, lp, workspace,
                                                (flags & CORR_REGION_PACK_QUERIES) != 0, (hipStream_t)stream),
                       fn);
@@ -174,7 +215,7 @@ int corr_lookup_rows(const float *const *pyr, const float *coords_rows, int B, i
     if (rc || (rc = check_radius(fn, radius))) return rc;
     if ((rc = check_ptr(fn, coords_rows, "coords")) || (rc = check_ptr(fn, out_rows, "out"))) return rc;
     ConstLevelPtrs lp{};
-    if ((rc = check_levels(fn, pyr, levels, "pyr", lp.p))) return rc;
+    if ((rc = check_pyramid(fn, pyr, levels, "pyr", lp.p))) return rc;
     return hip_status(launch_lookup(lp, coords_rows, B, NQ, H, W, levels, radius, out_rows, (hipStream_t)stream),
                       fn);
 }
@@ -359,12 +400,8 @@ int corr_lookup_conv(const float *const *pyr, const float *coords, int B, int H,
     if (rc) return rc;
     if (radius != 4 || levels > 4)
         return fail(CORR_EUNSUPPORTED, "%s: built for radius 4 and <= 4 levels (got %d, %d)", fn, radius, levels);
-    if (!pyr) return fail(CORR_EINVAL, "%s: pyr is null", fn);
     ConstLevelPtrs lp{};
-    for (int l = 0; l < levels; ++l) {
-        if ((rc = check_ptr(fn, pyr[l], "pyr[l]"))) return rc;
-        lp.p[l] = pyr[l];
-    }
+    if ((rc = check_pyramid(fn, pyr, levels, "pyr", lp.p))) return rc;
     if ((rc = check_ptr(fn, coords, "coords")) || (rc = check_ptr(fn, packed_weight, "packed_weight")) ||
         (rc = check_ptr(fn, bias, "bias")) || (rc = check_ptr(fn, out, "out")))
         return rc;
@@ -388,12 +425,8 @@ int corr_lookup_conv_bwd(const float *const *pyr, const float *coords, int B, in
     if (rc) return rc;
     if (radius != 4 || levels > 4)
         return fail(CORR_EUNSUPPORTED, "%s: built for radius 4 and <= 4 levels (got %d, %d)", fn, radius, levels);
-    if (!pyr) return fail(CORR_EINVAL, "%s: pyr is null", fn);
     ConstLevelPtrs lp{};
-    for (int l = 0; l < levels; ++l) {
-        if ((rc = check_ptr(fn, pyr[l], "pyr[l]"))) return rc;
-        lp.p[l] = pyr[l];
-    }
+    if ((rc = check_pyramid(fn, pyr, levels, "pyr", lp.p))) return rc;
     if ((rc = check_ptr(fn, coords, "coords")) || (rc = check_ptr(fn, packed_weight, "packed_weight")) ||
         (rc = check_ptr(fn, grad_out, "grad_out")))
         return rc;

@@ -62,18 +62,23 @@ struct BuildParams {
 
 
 
-// Epilogue: scale, level 0, in-register pyramid.
+// Epilogue: scale, level 0, in-register pyramid, into the tiled pyramid (corr_common.h).
 // acc[qt][tt][r]: query qw + qt*32 + l32, target (y, x) of the wave's 8x8 sub-patch at
 // (py*8, xw) with y = tt*4 + (r >> 2), x = 4h + (r & 3)   (32x32 C/D map).
-// VEC1 (W % 8 == 0, 16-B aligned levels): the two lane halves (h = 0, 1: the same query, target
-// columns 0-3 / 4-7) swap half of their level-1 rows, so a lane writes 2 level-1 rows of 4
-// columns as two 16-B stores (instead of 8 element stores), and one 8-B level-2 pair.
-template <int QT, bool VEC, bool VEC1>
+// Level 0 leaves as 16-B tile rows (columns X0 .. X0 + 3); for level 1 the two lane halves (h = 0,
+// 1: the same query, target columns 0-3 / 4-7) swap half of their rows, so a lane writes 2 level-1
+// tile rows of 4 columns; level 2 as one 8-B pair, level 3 one cell.  A store runs whenever its
+// tile row lies in the padded map (cells past W_l / H_l are padding: the zero-padded target
+// operands make them finite, nothing reads them).
+template <int QT>
 __device__ __forceinline__ void store_pyramid(const BuildParams &p, f32x16 (&acc)[QT][2], const int b,
                                               const int qw, const int xw, const int py, const int h,
                                               const int l32) {
-    const int N = p.N, NQ = p.NQ, W = p.W, H = p.H;
+    const int NQ = p.NQ, W = p.W, H = p.H;
     const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
+    const int TW0 = map_tiles(W), TW1 = map_tiles(W1), TW2 = map_tiles(W2), TW3 = map_tiles(W3);
+    const int R0 = 4 * map_tiles(H), R1 = 4 * map_tiles(H1), R2 = 4 * map_tiles(H2), R3 = 4 * map_tiles(H3);
+    const size_t M0 = map_floats(H, W), M1 = map_floats(H1, W1), M2 = map_floats(H2, W2), M3 = map_floats(H3, W3);
     const int X0 = xw + 4 * h, Y0 = py * 8;
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
@@ -89,23 +94,12 @@ __device__ __forceinline__ void store_pyramid(const BuildParams &p, f32x16 (&acc
                 v[tt * 4 + (r >> 2)][r & 3] = p.exact_mul ? x * p.inv_s : x / p.s;
             }
         // level 0
-        if (qok) {
-            float *o = p.lvl[0] + qrow * N;
+        if (qok && X0 < W) {
+            float *o = p.lvl[0] + qrow * M0;
 #pragma unroll
-            for (int y = 0; y < 8; ++y) {
-                const int Y = Y0 + y;
-                if (Y < H) {
-                    if (VEC) {
-                        if (X0 < W)
-                            *reinterpret_cast<float4 *>(o + (size_t)Y * W + X0) =
-                                make_float4(v[y][0], v[y][1], v[y][2], v[y][3]);
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if (X0 + e < W) o[(size_t)Y * W + X0 + e] = v[y][e];
-                    }
-                }
-            }
+            for (int y = 0; y < 8; ++y)
+                if (Y0 + y < R0)
+                    *reinterpret_cast<float4 *>(o + map_row4(Y0 + y, X0 >> 2, TW0)) = make_float4(v[y][0], v[y][1], v[y][2], v[y][3]);
         }
         if (p.nlev < 2) continue;
         // level 1: 4 rows x 2 cols per lane
@@ -116,7 +110,7 @@ __device__ __forceinline__ void store_pyramid(const BuildParams &p, f32x16 (&acc
             for (int x = 0; x < 2; ++x)
                 l1[y][x] = pool4(v[2 * y][2 * x], v[2 * y][2 * x + 1], v[2 * y + 1][2 * x],
                                  v[2 * y + 1][2 * x + 1]);
-        if (VEC1) {
+        {
             // h = 0 keeps rows 0-1 and receives columns 2-3 of them; h = 1 keeps rows 2-3 and
             // receives columns 0-1 of them
             float r[2][4];
@@ -130,24 +124,16 @@ __device__ __forceinline__ void store_pyramid(const BuildParams &p, f32x16 (&acc
                     r[y][2 * h + x] = mine;
                     r[y][2 * (1 - h) + x] = got;
                 }
-            if (qok && xw < W) {
-                float *o = p.lvl[1] + qrow * (size_t)(H1 * W1) + (xw >> 1);
+            const int X1 = xw >> 1;  // a multiple of 4
+            if (qok && X1 < W1) {
+                float *o = p.lvl[1] + qrow * M1;
 #pragma unroll
                 for (int y = 0; y < 2; ++y) {
                     const int Y = py * 4 + 2 * h + y;
-                    if (Y < H1)
-                        *reinterpret_cast<float4 *>(o + (size_t)Y * W1) = make_float4(r[y][0], r[y][1], r[y][2], r[y][3]);
+                    if (Y < R1)
+                        *reinterpret_cast<float4 *>(o + map_row4(Y, X1 >> 2, TW1)) = make_float4(r[y][0], r[y][1], r[y][2], r[y][3]);
                 }
             }
-        } else if (qok) {
-            float *o = p.lvl[1] + qrow * (size_t)(H1 * W1);
-#pragma unroll
-            for (int y = 0; y < 4; ++y)
-#pragma unroll
-                for (int x = 0; x < 2; ++x) {
-                    const int Y = py * 4 + y, X = (X0 >> 1) + x;
-                    if (Y < H1 && X < W1) o[Y * W1 + X] = l1[y][x];
-                }
         }
         if (p.nlev < 3) continue;
         // level 2: 2 rows x 1 col per lane
@@ -157,26 +143,18 @@ __device__ __forceinline__ void store_pyramid(const BuildParams &p, f32x16 (&acc
         // the partner half's level-2 pair (x = 1 - h): for the 8-B level-2 stores and level 3
         const float o0 = __shfl_xor(l2[0], 32);
         const float o1 = __shfl_xor(l2[1], 32);
-        if (VEC1) {  // h = 0 writes row 0 (x = 0, 1), h = 1 row 1
-            const int Y = py * 2 + h;
-            if (qok && xw < W && Y < H2)
-                *reinterpret_cast<float2 *>(p.lvl[2] + qrow * (size_t)(H2 * W2) + (size_t)Y * W2 + (xw >> 2)) =
+        {  // h = 0 writes row 0 (x = 0, 1), h = 1 row 1; xw / 4 is even, so the pair is 8-B aligned
+            const int Y = py * 2 + h, X2 = xw >> 2;
+            if (qok && X2 < 4 * TW2 && Y < R2)
+                *reinterpret_cast<float2 *>(p.lvl[2] + qrow * M2 + map_cell(Y, X2, TW2)) =
                     h ? make_float2(o1, l2[1]) : make_float2(l2[0], o0);
-        } else if (qok) {
-            float *o = p.lvl[2] + qrow * (size_t)(H2 * W2);
-            const int X = X0 >> 2;
-#pragma unroll
-            for (int y = 0; y < 2; ++y) {
-                const int Y = py * 2 + y;
-                if (Y < H2 && X < W2) o[Y * W2 + X] = l2[y];
-            }
         }
         if (p.nlev < 4) continue;
         // level 3: the 2x2 level-2 block is split across lane halves h = 0 (x = 0), 1 (x = 1)
         if (h == 0 && qok) {
             const float l3 = pool4(l2[0], o0, l2[1], o1);
             const int Y = py, X = X0 >> 3;
-            if (Y < H3 && X < W3) p.lvl[3][qrow * (size_t)(H3 * W3) + Y * W3 + X] = l3;
+            if (Y < R3 && X < 4 * TW3) p.lvl[3][qrow * M3 + map_cell(Y, X, TW3)] = l3;
         }
     }
 }
@@ -320,7 +298,7 @@ __device__ __forceinline__ void build_tile(const BuildParams &p, float *smem, co
         for (int i = 0; i < QT; ++i) x += acc[i][0][0] + acc[i][1][15];
         if (x == 1234.5f) p.lvl[0][tid] = x;
     } else {
-        store_pyramid<QT, (VM >= 1), (VM == 2)>(p, acc, b, q0 + wq * 32 * QT, px * PW + wt * 8, py, h, l32);
+        store_pyramid<QT>(p, acc, b, q0 + wq * 32 * QT, px * PW + wt * 8, py, h, l32);
     }
 }
 
@@ -339,20 +317,26 @@ __global__ __launch_bounds__(Cfg::NT, Cfg::OCC) void corr_build_kernel(BuildPara
 
 namespace {
 
-// Levels beyond the fused four: plain 2x2 average pool of level l-1 into level l.
+// Levels beyond the fused four: plain 2x2 average pool of level l-1 into level l, both tiled
+// (one thread per cell of level l, padding cells included: they pool padding).
 __global__ __launch_bounds__(256) void pool2x2_kernel(const float *__restrict__ in,
                                                       float *__restrict__ out, long BN, int H,
                                                       int W) {
     const int Ho = H >> 1, Wo = W >> 1;
-    const size_t total = (size_t)BN * Ho * Wo;
+    const int TWi = map_tiles(W), TWo = map_tiles(Wo);
+    const size_t Mi = map_floats(H, W), Mo = map_floats(Ho, Wo);
+    const size_t total = (size_t)BN * Mo;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (size_t)gridDim.x * blockDim.x) {
-        const size_t q = i / ((size_t)Ho * Wo);
-        const int rem = (int)(i - q * Ho * Wo);
-        const int y = rem / Wo, x = rem - y * Wo;
-        const float *I = in + q * H * W;
-        out[i] = pool4(I[(2 * y) * W + 2 * x], I[(2 * y) * W + 2 * x + 1], I[(2 * y + 1) * W + 2 * x],
-                       I[(2 * y + 1) * W + 2 * x + 1]);
+        const size_t q = i / Mo;
+        const int rem = (int)(i - q * Mo);
+        const int t = rem >> 4, c = rem & 15;
+        const int ty = t / TWo, tx = t - ty * TWo;
+        const int y = 4 * ty + (c >> 2), x = 4 * tx + (c & 3);
+        if (y >= Ho || x >= Wo) continue;  // padding of level l: never read
+        const float *I = in + q * Mi;
+        out[i] = pool4(I[map_cell(2 * y, 2 * x, TWi)], I[map_cell(2 * y, 2 * x + 1, TWi)],
+                       I[map_cell(2 * y + 1, 2 * x, TWi)], I[map_cell(2 * y + 1, 2 * x + 1, TWi)]);
     }
 }
 
@@ -363,7 +347,7 @@ hipError_t launch_pool_levels(const LevelPtrs &pyr, int l_from, int levels, long
                               hipStream_t s) {
     for (int l = l_from; l < levels; ++l) {
         const int Hi = H >> (l - 1), Wi = W >> (l - 1);
-        const size_t total = (size_t)BN * (Hi >> 1) * (Wi >> 1);
+        const size_t total = (size_t)BN * map_floats(Hi >> 1, Wi >> 1);
         const int grid = (int)std::min<size_t>((total + 255) / 256, 4096);
         hipLaunchKernelGGL(pool2x2_kernel, dim3(grid), dim3(256), 0, s, pyr.p[l - 1], pyr.p[l], BN,
                            Hi, Wi);
@@ -402,9 +386,8 @@ hipError_t launch_build_cfg(const float *f1, int NQ, const float *f2, int B, int
                      ((uintptr_t)f1 % 16 == 0) && ((uintptr_t)f2 % 16 == 0);
     const long tiles = (long)p.nq * p.npx * p.npy * B;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
-    // 16-B level-1 / 8-B level-2 stores: whole 8-column sub-patches and aligned level bases
-    const bool vec1 = vec1_ok && vec && W % 8 == 0 && (p.nlev < 2 || (uintptr_t)pyr.p[1] % 16 == 0) &&
-                      (p.nlev < 3 || (uintptr_t)pyr.p[2] % 8 == 0);
+    (void)vec1_ok;  // the tiled pyramid's stores are always 16-B tile rows: VM 2 == VM 1
+    const bool vec1 = false;
     static std::atomic<unsigned long long> lds_done[3];
     auto go = [&](auto vm_tag) {
         constexpr int VM = decltype(vm_tag)::value;

@@ -140,8 +140,6 @@ struct Args {
     int NQp, NQB, NQG, Hp, CB, npatch;  // npatch: patches of the target region
     int py0;                            // first patch row of the target region
     int exact;         // 1/sqrt(D) is a power of two (x * 1/s == x / s); else x * RN(1/s), within ~1 ulp
-    int mode0, mode1;  // store width of levels 0 / 1: 2 = 16 B, 1 = 8 B, 0 = elements
-    int cons;          // levels 1 and 2 as 16-B stores (W/2, W/4 multiples of 4, 16-B aligned bases)
     float inv_s, s;
     int order;  // tile order: 0, 1 = patch_tile's; 2 = XCD blocks (xcd_block_tile)
     int nqh, npq;  // order 2: query-group and patch splits of a batch item into XCD blocks
@@ -204,8 +202,7 @@ __device__ __forceinline__ Tile xcd_block_tile(const Args &p, int t) {
 // inline asm (the compiler then adds no wait of its own on them), bit 1 = s_setprio 1 over the
 // K loop (the epilogue of a neighbouring workgroup yields issue slots to MFMA-phase waves), bit 2 =
 // no half-patch body (padding rows computed and discarded: one kernel body).
-// FAST: every level stored as 16-B runs (levels == 4, W % 4 == 0 with 16-B aligned levels and
-// W/2, W/4 multiples of 4: mode0 == 2 and cons), no store-mode branches in the epilogue.
+// FAST: levels == 4 (no level-count branches in the epilogue).
 template <int SS, int NR, bool ACC2, int VF = 0, bool FAST = false>
 __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
     constexpr int QS = ACC2 ? 3 : 4, QD = QS - 1;
@@ -393,9 +390,14 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
     }
 
     // ---- epilogue: 1/sqrt(D), level 0 from registers, levels 1-3 in registers ----
-    const int H = p.H, W = p.W, N = p.N, NQ = p.NQ, nlev = FAST ? 4 : p.nlev;
+    // Every level leaves as 16-B tile rows of the tiled pyramid (corr_common.h) except level 3 (one
+    // cell per lane); a store runs whenever its tile row lies in the padded map (cells past W_l /
+    // H_l are padding: the zero-padded target records make them finite, nothing reads them).
+    const int H = p.H, W = p.W, NQ = p.NQ, nlev = FAST ? 4 : p.nlev;
     const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
-    const int N1 = H1 * W1, N2 = H2 * W2, N3 = H3 * W3;
+    const int TW0 = map_tiles(W), TW1 = map_tiles(W1), TW2 = map_tiles(W2), TW3 = map_tiles(W3);
+    const int R0 = 4 * map_tiles(H), R1 = 4 * map_tiles(H1), R2 = 4 * map_tiles(H2), R3 = 4 * map_tiles(H3);
+    const size_t M0 = map_floats(H, W), M1 = map_floats(H1, W1), M2 = map_floats(H2, W2), M3 = map_floats(H3, W3);
     const int X0 = x0 + 4 * grp;
     float l2s[2][2];  // both blocks' level-2 values: their stores are merged below
 #pragma unroll
@@ -408,18 +410,12 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
         for (int r = 0; r < kPatchRows; ++r)
 #pragma unroll
             for (int g = 0; g < 4; ++g) v[r][g] = (ACC2 ? acc[i][r][g] + acs[i][r][g] : acc[i][r][g]) * p.inv_s;
-        if (qok && nlev > 0) {
-            float *row0 = p.lvl[0] + qrow * N;
-            if constexpr (FAST) {
-                float *rp = row0 + (size_t)y0 * W + X0;
+        if (qok && nlev > 0 && X0 < W) {
+            float *m0 = p.lvl[0] + qrow * M0;
 #pragma unroll
-                for (int r = 0; r < kPatchRows; ++r)
-                    if (y0 + r < H && X0 < W) *reinterpret_cast<float4 *>(rp + r * W) = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
-            } else {
-#pragma unroll
-                for (int r = 0; r < kPatchRows; ++r)
-                    if (y0 + r < H) store4(row0 + (size_t)(y0 + r) * W, X0, W, v[r], p.mode0);
-            }
+            for (int r = 0; r < kPatchRows; ++r)
+                if (y0 + r < R0)
+                    *reinterpret_cast<float4 *>(m0 + map_row4(y0 + r, X0 >> 2, TW0)) = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
         }
         float l1[4][2];
 #pragma unroll
@@ -431,8 +427,8 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
 #pragma unroll
         for (int r = 0; r < 2; ++r) l2[r] = pool4(l1[2 * r][0], l1[2 * r][1], l1[2 * r + 1][0], l1[2 * r + 1][1]);
         l2s[i][0] = l2[0], l2s[i][1] = l2[1];
-        if (FAST || p.cons) {
-            // Level 1 as 16-B stores: lanes grp 2m and 2m + 1 hold level-1 columns x0/2 + 4m + {0,1}
+        {
+            // Level 1 as 16-B tile rows: lanes grp 2m and 2m + 1 hold level-1 columns x0/2 + 4m + {0,1}
             // and {2,3} of the patch's 4 rows; they swap one row's pair (lanes 16 apart) so that the
             // even lane stores rows 0, 2 and the odd lane rows 1, 3, 4 columns each.
             const bool odd = grp & 1;
@@ -443,29 +439,16 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
                 const float g0 = __shfl_xor(odd ? l1[ra][0] : l1[rb][0], 16);
                 const float g1 = __shfl_xor(odd ? l1[ra][1] : l1[rb][1], 16);
                 const float4 o = odd ? make_float4(g0, g1, l1[rb][0], l1[rb][1]) : make_float4(l1[ra][0], l1[ra][1], g0, g1);
-                if (qok && nlev > 1 && (y0 >> 1) + r < H1 && X1 < W1)
-                    *reinterpret_cast<float4 *>(p.lvl[1] + qrow * N1 + (size_t)((y0 >> 1) + r) * W1 + X1) = o;
-            }
-        } else {
-            if (qok && nlev > 1) {
-                float *row1 = p.lvl[1] + qrow * N1;
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if ((y0 >> 1) + r < H1) store2(row1 + (size_t)((y0 >> 1) + r) * W1, X0 >> 1, W1, l1[r][0], l1[r][1], p.mode1);
-            }
-            if (qok && nlev > 2) {
-                float *row2 = p.lvl[2] + qrow * N2;
-#pragma unroll
-                for (int r = 0; r < 2; ++r)
-                    if ((y0 >> 2) + r < H2 && (X0 >> 2) < W2) row2[((y0 >> 2) + r) * W2 + (X0 >> 2)] = l2[r];
+                if (qok && nlev > 1 && (y0 >> 1) + r < R1 && X1 < W1)
+                    *reinterpret_cast<float4 *>(p.lvl[1] + qrow * M1 + map_row4((y0 >> 1) + r, X1 >> 2, TW1)) = o;
             }
         }
     }
     // Levels 2 and 3 of BOTH query blocks in one store instruction each (an xor exchange has one
     // receiver per sender, so every sender sends what its receiver's block needs).
-    if (FAST || p.cons) {
+    {
         // Level 2: lanes grp 0..3 hold columns x0/4 + grp of 2 rows per block; lane g gathers row
-        // g & 1 of block g >> 1 (exchanges with lanes 16, 32, 48 apart), 16 B per lane.
+        // g & 1 of block g >> 1 (exchanges with lanes 16, 32, 48 apart): one 16-B tile row per lane.
         const int bl = grp >> 1, rw = grp & 1;
         auto sel = [&](int k) { return k == 0 ? l2s[0][0] : k == 1 ? l2s[0][1] : k == 2 ? l2s[1][0] : l2s[1][1]; };
         const float t0 = sel(grp);
@@ -474,8 +457,8 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
         auto pick = [&](int k) { return k == 0 ? t0 : k == 1 ? t1 : k == 2 ? t2 : t3; };
         const float4 o = make_float4(pick(grp), pick(grp ^ 1), pick(grp ^ 2), pick(grp ^ 3));
         const int q = (qb0 + bl) * 16 + ci;
-        if (q < NQ && nlev > 2 && (y0 >> 2) + rw < H2 && (x0 >> 2) < W2)
-            *reinterpret_cast<float4 *>(p.lvl[2] + ((size_t)b * NQ + q) * N2 + (size_t)((y0 >> 2) + rw) * W2 + (x0 >> 2)) = o;
+        if (q < NQ && nlev > 2 && (y0 >> 2) + rw < R2 && (x0 >> 2) < W2)
+            *reinterpret_cast<float4 *>(p.lvl[2] + ((size_t)b * NQ + q) * M2 + map_row4((y0 >> 2) + rw, x0 >> 4, TW2)) = o;
     }
     {
         // Level 3: the 2x2 window of level-2 values (a row pair in one lane, the column pair in the
@@ -485,7 +468,7 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
         const float l3 = bl == 0 ? pool4(l2s[0][0], y0v, l2s[0][1], y1v) : pool4(y0v, l2s[1][0], y1v, l2s[1][1]);
         const int q = (qb0 + bl) * 16 + ci;
         const int Y3 = y0 >> 3, X3 = X0 >> 3;
-        if (q < NQ && nlev > 3 && Y3 < H3 && X3 < W3) p.lvl[3][((size_t)b * NQ + q) * N3 + Y3 * W3 + X3] = l3;
+        if (q < NQ && nlev > 3 && Y3 < R3 && X3 < 4 * TW3) p.lvl[3][((size_t)b * NQ + q) * M3 + map_cell(Y3, X3, TW3)] = l3;
     }
 }
 
@@ -516,7 +499,7 @@ inline Ws workspace_of(void *ws, int B, const Geom &g) {
 
 template <int SS, bool ACC2 = true, int VF = 0>
 hipError_t launch_kernel(dim3 grid, const Args &p, hipStream_t s) {
-    const bool fast = p.nlev == 4 && p.mode0 == 2 && p.cons;
+    const bool fast = p.nlev == 4;
     static std::atomic<unsigned long long> lds_done[2];
     const void *fn = fast ? (const void *)corr_build_bf16_kernel<SS, ACC2, VF, true>
                           : (const void *)corr_build_bf16_kernel<SS, ACC2, VF, false>;
@@ -578,9 +561,6 @@ hipError_t launch_mfma(int NQ, int B, int D, int H, int W, int levels, const Lev
     p.s = std::sqrt((float)D);
     p.inv_s = 1.0f / p.s;
     p.exact = is_pow2(p.s);
-    p.mode0 = p.nlev > 0 ? level_store_mode(W, pyr.p[0]) : 0;
-    p.mode1 = p.nlev > 1 ? level_store_mode(W >> 1, pyr.p[1]) : 0;
-    p.cons = p.mode1 == 2 && (p.nlev <= 2 || level_store_mode(W >> 2, pyr.p[2]) == 2);
     // XCD blocks: split each batch item into 8 / B blocks (2 x 4 for one item), so the 8 XCDs
     // get disjoint operand sets; B >= 8: one or more whole batch items per XCD
     p.order = order;

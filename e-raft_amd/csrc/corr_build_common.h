@@ -48,8 +48,8 @@ inline bool is_pow2(float s) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Shared by the two split builds (corr_build_split.hip, corr_build_bf16.hip): tile order,
-// LDS-DMA pieces and the pyramid's run stores.
+// Shared by the two split builds (corr_build_split.hip, corr_build_bf16.hip): tile order and
+// LDS-DMA pieces.
 // ---------------------------------------------------------------------------------------
 constexpr int kGroupQ = 8;  // query groups per L2 tile group
 
@@ -102,38 +102,6 @@ __device__ __forceinline__ void dma16(const void *g, uint32_t lds) {
 // One LDS-DMA dword per lane: g -> LDS at lds + 4 * lane.
 __device__ __forceinline__ void dma4(const void *g, uint32_t lds) {
     asm volatile("global_load_lds_dword %0, off" ::"v"(g), "{m0}"(lds) : "memory");
-}
-
-// A run of 4 at column X (a multiple of 4) of a row of width Wl; mode per level (uniform):
-// 2 = one 16-B store, 1 = two 8-B stores, 0 = elements.
-__device__ __forceinline__ void store4(float *row, int X, int Wl, const float (&v)[4], int mode) {
-    if (mode == 2) {
-        if (X < Wl) *reinterpret_cast<float4 *>(row + X) = make_float4(v[0], v[1], v[2], v[3]);
-    } else if (mode == 1) {
-        if (X < Wl) *reinterpret_cast<float2 *>(row + X) = make_float2(v[0], v[1]);
-        if (X + 2 < Wl) *reinterpret_cast<float2 *>(row + X + 2) = make_float2(v[2], v[3]);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (X + k < Wl) row[X + k] = v[k];
-    }
-}
-
-// A run of 2 at an even column X.
-__device__ __forceinline__ void store2(float *row, int X, int Wl, float a, float b, int mode) {
-    if (mode >= 1) {
-        if (X < Wl) *reinterpret_cast<float2 *>(row + X) = make_float2(a, b);
-    } else {
-        if (X < Wl) row[X] = a;
-        if (X + 1 < Wl) row[X + 1] = b;
-    }
-}
-
-// Store width of one level's runs (columns X = 4k or 2k; row offsets are multiples of Wl).
-inline int level_store_mode(int Wl, const float *base) {
-    if (Wl % 4 == 0 && (uintptr_t)base % 16 == 0) return 2;
-    if (Wl % 2 == 0 && (uintptr_t)base % 8 == 0) return 1;
-    return 0;
 }
 
 // ---------------------------------------------------------------------------------------

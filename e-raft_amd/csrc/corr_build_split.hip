@@ -176,8 +176,6 @@ struct BuildArgs {
     int NQp, NQB, NQG, Hp, CB, Wp, npatch;
     int eshift;      // log2(1/sqrt(D)) when that is exact (folded into the exponent), else 0
     int exact;       // 1/sqrt(D) is a power of two
-    int mode0, mode1;  // store width of levels 0 / 1: 2 = 16 B, 1 = 8 B, 0 = elements
-    int cons;          // levels 1 and 2 as 16-B stores (W/2, W/4 multiples of 4, 16-B aligned bases)
     float inv_s;     // 1/sqrt(D) otherwise (multiplied: within tolerance, not bitwise)
     int order;       // tile order: 0 = query group fastest (groups of kGroupQ), 1 = patch column fastest
 };
@@ -356,9 +354,13 @@ __device__ __forceinline__ void build_tile(const BuildArgs &p, const Tile tl) {
         const int4 e4 = reinterpret_cast<const int4 *>(lds_et)[r * 4 + grp];
         et[r][0] = e4.x, et[r][1] = e4.y, et[r][2] = e4.z, et[r][3] = e4.w;
     }
-    const int H = p.H, W = p.W, N = p.N, NQ = p.NQ, nlev = p.nlev;
+    // Tiled pyramid (corr_common.h): levels 0-2 as 16-B tile rows, level 3 one cell per lane; a
+    // store runs whenever its tile row lies in the padded map (corr_build_bf16.hip's epilogue).
+    const int H = p.H, W = p.W, NQ = p.NQ, nlev = p.nlev;
     const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
-    const int N1 = H1 * W1, N2 = H2 * W2, N3 = H3 * W3;
+    const int TW0 = map_tiles(W), TW1 = map_tiles(W1), TW2 = map_tiles(W2), TW3 = map_tiles(W3);
+    const int R0 = 4 * map_tiles(H), R1 = 4 * map_tiles(H1), R2 = 4 * map_tiles(H2), R3 = 4 * map_tiles(H3);
+    const size_t M0 = map_floats(H, W), M1 = map_floats(H1, W1), M2 = map_floats(H2, W2), M3 = map_floats(H3, W3);
     const int X0 = x0 + 4 * grp;
     float l2s[2][2];  // both blocks' level-2 values: their stores are merged below
 #pragma unroll
@@ -375,11 +377,12 @@ __device__ __forceinline__ void build_tile(const BuildArgs &p, const Tile tl) {
                 if (!p.exact) x = x * p.inv_s;
                 v[r][g] = x;
             }
-        if (qok && nlev > 0) {
-            float *row0 = p.lvl[0] + qrow * N;
+        if (qok && nlev > 0 && X0 < W) {
+            float *m0 = p.lvl[0] + qrow * M0;
 #pragma unroll
             for (int r = 0; r < kPatchRows; ++r)
-                if (y0 + r < H) store4(row0 + (size_t)(y0 + r) * W, X0, W, v[r], p.mode0);
+                if (y0 + r < R0)
+                    *reinterpret_cast<float4 *>(m0 + map_row4(y0 + r, X0 >> 2, TW0)) = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
         }
         float l1[4][2];
 #pragma unroll
@@ -391,10 +394,10 @@ __device__ __forceinline__ void build_tile(const BuildArgs &p, const Tile tl) {
 #pragma unroll
         for (int r = 0; r < 2; ++r) l2[r] = pool4(l1[2 * r][0], l1[2 * r][1], l1[2 * r + 1][0], l1[2 * r + 1][1]);
         l2s[i][0] = l2[0], l2s[i][1] = l2[1];
-        if (p.cons) {
-            // Levels 1 and 2 as 16-B stores.  Level 1: lanes grp 2m and 2m + 1 hold level-1 columns
-            // x0/2 + 4m + {0,1} and {2,3} of the patch's 4 rows; they swap one row's pair (lanes 16
-            // apart) so that the even lane stores rows 0, 2 and the odd lane rows 1, 3, 4 columns each.
+        {
+            // Level 1 as 16-B tile rows: lanes grp 2m and 2m + 1 hold level-1 columns x0/2 + 4m + {0,1}
+            // and {2,3} of the patch's 4 rows; they swap one row's pair (lanes 16 apart) so that the
+            // even lane stores rows 0, 2 and the odd lane rows 1, 3, 4 columns each.
             const bool odd = grp & 1;
             const int X1 = (x0 >> 1) + 4 * (grp >> 1);
 #pragma unroll
@@ -403,29 +406,16 @@ __device__ __forceinline__ void build_tile(const BuildArgs &p, const Tile tl) {
                 const float g0 = __shfl_xor(odd ? l1[ra][0] : l1[rb][0], 16);
                 const float g1 = __shfl_xor(odd ? l1[ra][1] : l1[rb][1], 16);
                 const float4 o = odd ? make_float4(g0, g1, l1[rb][0], l1[rb][1]) : make_float4(l1[ra][0], l1[ra][1], g0, g1);
-                if (qok && nlev > 1 && (y0 >> 1) + r < H1 && X1 < W1)
-                    *reinterpret_cast<float4 *>(p.lvl[1] + qrow * N1 + (size_t)((y0 >> 1) + r) * W1 + X1) = o;
-            }
-        } else {
-            if (qok && nlev > 1) {
-                float *row1 = p.lvl[1] + qrow * N1;
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    if ((y0 >> 1) + r < H1) store2(row1 + (size_t)((y0 >> 1) + r) * W1, X0 >> 1, W1, l1[r][0], l1[r][1], p.mode1);
-            }
-            if (qok && nlev > 2) {
-                float *row2 = p.lvl[2] + qrow * N2;
-#pragma unroll
-                for (int r = 0; r < 2; ++r)
-                    if ((y0 >> 2) + r < H2 && (X0 >> 2) < W2) row2[((y0 >> 2) + r) * W2 + (X0 >> 2)] = l2[r];
+                if (qok && nlev > 1 && (y0 >> 1) + r < R1 && X1 < W1)
+                    *reinterpret_cast<float4 *>(p.lvl[1] + qrow * M1 + map_row4((y0 >> 1) + r, X1 >> 2, TW1)) = o;
             }
         }
     }
     // Levels 2 and 3 of BOTH query blocks in one store instruction each.  An xor exchange has one
     // receiver per sender, so every sender sends what its receiver's block needs.
-    if (p.cons) {
+    {
         // Level 2: lanes grp 0..3 hold columns x0/4 + grp of 2 rows per block; lane g gathers row
-        // g & 1 of block g >> 1 (exchanges with lanes 16, 32, 48 apart), 16 B per lane.
+        // g & 1 of block g >> 1 (exchanges with lanes 16, 32, 48 apart), one 16-B tile row per lane.
         const int bl = grp >> 1, rw = grp & 1;
         // value k = 2 * block + row of this lane, by selects (a dynamic register index goes to scratch)
         auto sel = [&](int k) { return k == 0 ? l2s[0][0] : k == 1 ? l2s[0][1] : k == 2 ? l2s[1][0] : l2s[1][1]; };
@@ -435,8 +425,8 @@ __device__ __forceinline__ void build_tile(const BuildArgs &p, const Tile tl) {
         auto pick = [&](int k) { return k == 0 ? t0 : k == 1 ? t1 : k == 2 ? t2 : t3; };
         const float4 o = make_float4(pick(grp), pick(grp ^ 1), pick(grp ^ 2), pick(grp ^ 3));
         const int q = (qb0 + bl) * 16 + ci;
-        if (q < NQ && nlev > 2 && (y0 >> 2) + rw < H2 && (x0 >> 2) < W2)
-            *reinterpret_cast<float4 *>(p.lvl[2] + ((size_t)b * NQ + q) * N2 + (size_t)((y0 >> 2) + rw) * W2 + (x0 >> 2)) = o;
+        if (q < NQ && nlev > 2 && (y0 >> 2) + rw < R2 && (x0 >> 2) < W2)
+            *reinterpret_cast<float4 *>(p.lvl[2] + ((size_t)b * NQ + q) * M2 + map_row4((y0 >> 2) + rw, x0 >> 4, TW2)) = o;
     }
     {
         // Level 3: the 2x2 window of level-2 values (a row pair in one lane, the column pair in the
@@ -446,7 +436,7 @@ __device__ __forceinline__ void build_tile(const BuildArgs &p, const Tile tl) {
         const float l3 = bl == 0 ? pool4(l2s[0][0], y0v, l2s[0][1], y1v) : pool4(y0v, l2s[1][0], y1v, l2s[1][1]);
         const int q = (qb0 + bl) * 16 + ci;
         const int Y3 = y0 >> 3, X3 = X0 >> 3;
-        if (q < NQ && nlev > 3 && Y3 < H3 && X3 < W3) p.lvl[3][((size_t)b * NQ + q) * N3 + Y3 * W3 + X3] = l3;
+        if (q < NQ && nlev > 3 && Y3 < R3 && X3 < 4 * TW3) p.lvl[3][((size_t)b * NQ + q) * M3 + map_cell(Y3, X3, TW3)] = l3;
     }
 }
 
@@ -532,8 +522,8 @@ hipError_t launch_build_kernel(dim3 grid, const BuildArgs &p, hipStream_t s) {
 }
 
 // The MFMA part (operands already packed in ws).  levels == 0: the MFMAs and epilogue
-// arithmetic without stores (measurement).  cons = false: levels 1-2 as element stores (the
-// previous epilogue, kept for the A/B; same bits).
+// arithmetic without stores (measurement).  cons: unused (the tiled pyramid's stores are always
+// 16-B tile rows; kept for tools/kbench_build.hip's call signature).
 // order: the build's tile order (BuildArgs::order): 1 = a patch row's patches consecutive for
 // one query group (the default: 1280x960 1006 -> 948 us, DSEC / train / MVSEC 1-4 % faster,
 // profiles/r03b_kbench_build_order.txt); tools/kbench_build.hip passes 0 for the A/B.
@@ -557,9 +547,7 @@ hipError_t launch_split_mfma(int NQ, int B, int D, int H, int W, int levels, con
         std::frexp(p.inv_s, &e);
         p.eshift = e - 1;  // 1/s = 2^(e-1)
     }
-    p.mode0 = p.nlev > 0 ? level_store_mode(W, pyr.p[0]) : 0;
-    p.mode1 = p.nlev > 1 ? level_store_mode(W >> 1, pyr.p[1]) : 0;
-    p.cons = cons && p.mode1 == 2 && (p.nlev <= 2 || level_store_mode(W >> 2, pyr.p[2]) == 2);
+    (void)cons;
     p.order = order;
     const long tiles = (long)B * p.npatch * g.NQG;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;

@@ -1049,15 +1049,17 @@ struct PendingReduce {
     float sD = 1.f;
 };
 
+// CU count of the current device, looked up once per device (a process may drive parts with
+// different counts: the tail-reduce plan depends on it).
 inline int device_cus() {
-    static std::atomic<int> n{0};
-    int v = n.load(std::memory_order_relaxed);
+    static std::atomic<int> n[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    std::atomic<int> &slot = n[dev & 63];
+    int v = slot.load(std::memory_order_relaxed);
     if (v == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
-            v = 256;
-        n.store(v, std::memory_order_relaxed);
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        slot.store(v, std::memory_order_relaxed);
     }
     return v;
 }

@@ -19,6 +19,29 @@ struct ConstLevelPtrs {
     const float *p[CORR_MAX_LEVELS];
 };
 
+// ---------------------------------------------------------------------------------------
+// Pyramid layout (the build's output, the lookups' input).  Every query's level-l map
+// (H_l x W_l cells, corr.py:21-27) is stored as 4x4-cell tiles of 64 B, tiles row-major over
+// the map, cells row-major inside a tile:
+//     cell (y, x) of a map at ((y >> 2) * TW + (x >> 2)) * 16 + (y & 3) * 4 + (x & 3),
+//     TW = ceil(W_l / 4), a map = ceil(H_l / 4) * TW * 16 floats (a multiple of 64 B).
+// A query's maps are contiguous (level by level, query after query), so a row slab of queries
+// is a contiguous range, as before.  The cells past W_l / H_l in the last tile column / row are
+// padding: the builds may write anything there and nothing reads them (the lookups zero
+// out-of-map cells themselves).  A (2r+2)^2 window then spans whole 64-B tiles (one 16-B tile
+// row per lane and window row in the gather), where row-major maps gave one 40-B segment per
+// window row in a different line (profiles/r05f_kbench_lookup_tiled.txt).  The reference
+// layout [B*N, 1, H_l, W_l] is materialised on demand (corr_pyramid_export).
+__host__ __device__ inline int map_tiles(int n) { return (n + 3) >> 2; }
+__host__ __device__ inline size_t map_floats(int Hl, int Wl) { return (size_t)map_tiles(Hl) * map_tiles(Wl) * 16; }
+__host__ __device__ inline unsigned map_cell(int y, int x, int TW) {
+    return (unsigned)((((y >> 2) * TW + (x >> 2)) << 4) + ((y & 3) << 2) + (x & 3));
+}
+// Offset of the 16-B tile row holding cells (y, 4t .. 4t + 3).
+__host__ __device__ inline unsigned map_row4(int y, int t, int TW) {
+    return (unsigned)((((y >> 2) * TW + t) << 4) + ((y & 3) << 2));
+}
+
 // Set the thread-local error and return `code`.
 int fail(int code, const char *fmt, ...);
 // Map a HIP status to CORR_OK / CORR_EHIP (recording the message).
@@ -97,6 +120,11 @@ hipError_t launch_voxel_grid_tbilinear(const double *events, int M, int C, int H
 hipError_t launch_voxel_grid(const float *x, const float *y, const float *t, const float *p, int M, int C, int H,
                              int W, int normalize, float *out, void *ws, hipStream_t s);
 hipError_t launch_forward_splat(const float *flow, int B, int H, int W, float *out, void *ws, hipStream_t s);
+// Tiled pyramid <-> the reference's row-major [BN][H_l][W_l] (corr_lookup.hip).
+hipError_t launch_pyramid_export(const ConstLevelPtrs &pyr, long BN, int H, int W, int levels, const LevelPtrs &out,
+                                 hipStream_t s);
+hipError_t launch_pyramid_import(const ConstLevelPtrs &src, long BN, int H, int W, int levels, const LevelPtrs &pyr,
+                                 hipStream_t s);
 size_t build_bwd_workspace(int B, int D, int NQ, int H, int W);
 hipError_t launch_build_bwd(const float *grad_c, const float *f1, int NQ, const float *f2, int B,
                             int D, int H, int W, float *df1, float *df2, float *ws, hipStream_t s);

@@ -6,18 +6,19 @@
 // permute().contiguous() (corr.py:49-50) become ONE launch that writes the NCHW output
 // directly.
 //
-// Work layout: a workgroup owns 64 consecutive query pixels of one batch item at one pyramid
-// level, with S = 2r+1 waves — wave i owns window column i (the x-tap; corr.py:37-43: the
-// slow window index moves x).
+// Work layout: a workgroup owns QB (32; 16 on small maps) consecutive query pixels of one batch
+// item at one pyramid level; thread (q, i) is query q's window column i (the x-tap;
+// corr.py:37-43: the slow window index moves x).
 //   1. thread (q, i): tap i of query q on both axes, rounded exactly as the reference does
 //      (x/2^l + (i - r) -> 2X/(W_l-1) - 1 -> ((x'+1)/2)(W_l-1); one fp32 rounding per op),
 //      its floor and the two 1-D weights; y-taps -> LDS, the thread keeps its x-tap;
 //   2. every query's (S+2)^2 neighbourhood (anchored at the floor of its tap 0, zero outside
-//      the map) is gathered from HBM into LDS — all of a thread's loads issued before any
-//      LDS store, so the gather costs one memory round trip;
+//      the map) is gathered from the TILED map (corr_common.h) into LDS, one 16-B tile row per
+//      lane — all of a thread's loads issued before any LDS store, so the gather costs one
+//      memory round trip;
 //   3. thread (q, i) produces the S outputs (i, j = 0..S-1): 4 corner reads from LDS, fmaf in
 //      the order nw, ne, sw, se (bit-identical to ATen's CPU grid_sampler_2d), stores to
-//      out[b][l*K + i*S + j][n] — 64 consecutive n per wave, fully coalesced.
+//      out[b][l*K + i*S + j][n] — consecutive n per wave, fully coalesced.
 // Tap floors are monotone in the tap index, so one check of the first and last tap proves
 // that every corner lies inside the neighbourhood.  A workgroup where that fails for some
 // query (only possible for |coordinates| near 2^20) takes a uniform slow path that reads such
@@ -48,8 +49,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int kQB = 64;  // queries per workgroup (one per lane)
 
 // Sentinel anchor for NaN / huge coordinates: every window cell is outside the map.
 constexpr int kFarAnchor = -(1 << 28);
@@ -91,126 +90,121 @@ __device__ __forceinline__ bool window_covers(float fx0, float fxl, float fy0, f
     return (fxl - fx0) <= (float)S && (fyl - fy0) <= (float)S;
 }
 
-// Gather each query's neighbourhood into LDS: cell (ry, rx) of query qq = map (ay+ry, ax+rx),
-// zero outside the map or for queries past N.
-template <int S, int NT>
-__device__ __forceinline__ void gather_window(float *win, const int *ax, const int *ay,
-                                              const float *P, size_t qbase, size_t mapsz, int n0,
-                                              int N, int Wl, int Hl, int tid) {
-    constexpr int WIN = S + 2, WS = WIN * WIN, WSTR = WS | 1;
-    constexpr int PER = (kQB * WS + NT - 1) / NT;
-    float vals[PER];
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-        const int g = tid + NT * u;
-        const int qq = g / WS;
-        const int e = g - qq * WS;
-        const int ry = e / WIN, rx = e - ry * WIN;
-        float v = 0.0f;
-        if (g < kQB * WS && n0 + qq < N) {
-            const int Y = ay[qq] + ry, X = ax[qq] + rx;
-            if (X >= 0 && X < Wl && Y >= 0 && Y < Hl) v = P[(qbase + qq) * mapsz + (size_t)Y * Wl + X];
-        }
-        vals[u] = v;
-    }
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-        const int g = tid + NT * u;
-        if (g < kQB * WS) {
-            const int qq = g / WS;
-            win[qq * WSTR + (g - qq * WS)] = vals[u];
-        }
-    }
-}
-
-// Forward gather: one wave per query at a time, lane -> fixed neighbourhood cells, so the
-// (row, col) of each lane's cells is computed once and every load's address is
-// anchor + constant (no per-element integer division).
-template <int S, int QB, int NT, bool NOLOAD = false, bool NTLOAD = false>
-__device__ __forceinline__ void gather_window_wave(float *win, const int *ax, const int *ay,
-                                                   const float *P, size_t qbase, size_t mapsz,
-                                                   int n0, int N, int Wl, int Hl, int tid) {
-    constexpr int WIN = S + 2, WS = WIN * WIN, WSTR = WS | 1;
-    constexpr int NW = NT / 64;
-    constexpr int EPL = (WS + 63) / 64;   // cells per lane per query
-    constexpr int QPW = (QB + NW - 1) / NW;  // queries per wave
-    const int lane = tid & 63, w = tid >> 6;
-    int ry[EPL], rx[EPL];
-#pragma unroll
-    for (int v = 0; v < EPL; ++v) {
-        const int e = lane + 64 * v;
-        ry[v] = e / WIN;
-        rx[v] = e - ry[v] * WIN;
-    }
-    // The query a wave handles at step k is wave-uniform.  All of the wave's anchors are read
-    // from LDS at once (lane k holds query k's) and moved to scalar registers with readlane, so
-    // no step waits on LDS; each load is then base(SGPR) + 32-bit offset.
-    static_assert(QPW <= 64, "one lane per query of the wave");
-    const int wu = __builtin_amdgcn_readfirstlane(w);
-    int myX = kFarAnchor, myY = kFarAnchor;
-    {
-        const int qq = wu + NW * lane;
-        if (lane < QPW && qq < QB && n0 + qq < N) {
-            myX = ax[qq];
-            myY = ay[qq];
-        }
-    }
-    float vals[QPW][EPL];
-#pragma unroll
-    for (int k = 0; k < QPW; ++k) {
-        const int qq = wu + NW * k;
-        const int X0 = __builtin_amdgcn_readlane(myX, k);
-        const int Y0 = __builtin_amdgcn_readlane(myY, k);
-        const float *Pq = P + (qbase + qq) * mapsz;
-#pragma unroll
-        for (int v = 0; v < EPL; ++v) {
-            const int X = X0 + rx[v], Y = Y0 + ry[v];
-            const bool ok = (lane + 64 * v < WS) && (unsigned)X < (unsigned)Wl && (unsigned)Y < (unsigned)Hl;
-            if constexpr (NTLOAD) vals[k][v] = (ok && !NOLOAD) ? __builtin_nontemporal_load(&Pq[(unsigned)(Y * Wl + X)]) : 0.0f;
-            else vals[k][v] = (ok && !NOLOAD) ? Pq[(unsigned)(Y * Wl + X)] : 0.0f;
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < QPW; ++k) {
-        const int qq = w + NW * k;
-#pragma unroll
-        for (int v = 0; v < EPL; ++v)
-            if (qq < QB && lane + 64 * v < WS) win[qq * WSTR + lane + 64 * v] = vals[k][v];
-    }
-}
-
 template <int S, int QB>
 struct LookupSmem {
     static constexpr int WIN = S + 2;
-    static constexpr int WSTR = (WIN * WIN) | 1;  // odd stride: conflict-free lane = query reads
-    float win[QB * WSTR];
+    static constexpr int NTC = (WIN + 6) / 4;  // tile columns that hold WIN cells at any offset
+    // Window row of query q: cell cx (column anchor + cx) at win[q * WQ + cy * WW + 3 + cx].  A
+    // gather lane stores its tile row's 4 cells at columns 4 tc - (anchor & 3) + 3 + c, i.e.
+    // without predicates: cells left or right of the window land in the 3 + (4 NTC - WIN) spare
+    // columns of the row.  Odd query stride: lane = query reads are conflict-free.
+    static constexpr int WW = 4 * NTC + 3;
+    static constexpr int WQ = (WIN * WW) | 1;
+    float win[QB * WQ];
     float ty[3][S][QB];
     float fx[2][QB];  // floor of x-tap 0 and S-1
     int ax[QB], ay[QB];
     int flags;
 };
 
+// Forward gather from the tiled maps (corr_common.h): one wave per query at a time, lane =
+// (window row rr, tile column tc): one 16-B load of the tile row holding cells (anchor_y + rr,
+// 4 (anchor_x / 4 + tc) .. + 3), zero outside the map; then four LDS stores realigned to the
+// window (unconditional: out-of-window cells go to the row's spare columns).  All of a thread's
+// loads are issued before any LDS store, so the gather costs one memory round trip.  The
+// query map bases are wave-uniform: qb is moved to a scalar register, so the 64-bit base
+// arithmetic is scalar.  NOLOAD: ablation (tools/kbench_lookup.hip).
+template <int S, int QB, int NT, bool NOLOAD = false>
+__device__ __forceinline__ void gather_window_tiled(LookupSmem<S, QB> &sm, const float *P, size_t qbase,
+                                                    unsigned mapsz, int n0, int N, int Wl, int Hl, int tid) {
+    using SM = LookupSmem<S, QB>;
+    constexpr int WIN = SM::WIN, NTC = SM::NTC, WW = SM::WW, WQ = SM::WQ;
+    constexpr int LPQ = NTC * WIN;           // lanes per query
+    constexpr int EPL = (LPQ + 63) / 64;     // loads per lane and query
+    constexpr int NW = NT / 64;
+    constexpr int QPW = (QB + NW - 1) / NW;  // queries per wave
+    static_assert(QPW <= 64, "one lane per query of the wave");
+    const unsigned TW = (unsigned)map_tiles(Wl);
+    const int lane = tid & 63;
+    int rr[EPL], tc[EPL];
+#pragma unroll
+    for (int v = 0; v < EPL; ++v) {
+        const int e = lane + 64 * v;
+        rr[v] = e / NTC;
+        tc[v] = e - rr[v] * NTC;
+    }
+    // The query a wave handles at step k is wave-uniform: all of the wave's anchors are read from
+    // LDS at once (lane k holds query k's) and moved to scalar registers with readlane.
+    const int wu = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const unsigned qb = __builtin_amdgcn_readfirstlane((unsigned)qbase);
+    int myX = kFarAnchor, myY = kFarAnchor;
+    {
+        const int qq = wu + NW * lane;
+        if (lane < QPW && qq < QB && n0 + qq < N) {
+            myX = sm.ax[qq];
+            myY = sm.ay[qq];
+        }
+    }
+    f32x4 vals[QPW][EPL];
+#pragma unroll
+    for (int k = 0; k < QPW; ++k) {
+        const int qq = wu + NW * k;
+        const int X0 = __builtin_amdgcn_readlane(myX, k);
+        const int Y0 = __builtin_amdgcn_readlane(myY, k);
+        const float *Pq = P + (size_t)(qb + (unsigned)qq) * mapsz;
+#pragma unroll
+        for (int v = 0; v < EPL; ++v) {
+            const unsigned T = (unsigned)((X0 >> 2) + tc[v]), Y = (unsigned)(Y0 + rr[v]);
+            const bool ok = (lane + 64 * v < LPQ) && T < TW && Y < (unsigned)Hl;
+            vals[k][v] = (ok && !NOLOAD) ? *reinterpret_cast<const f32x4 *>(Pq + map_row4((int)Y, (int)T, (int)TW))
+                                         : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    const bool ragged = (Wl & 3) != 0;  // the last tile column holds cells past W_l: zero them
+#pragma unroll
+    for (int k = 0; k < QPW; ++k) {
+        const int qq = wu + NW * k;
+        const int X0 = __builtin_amdgcn_readlane(myX, k);
+        if (qq >= QB) continue;
+#pragma unroll
+        for (int v = 0; v < EPL; ++v) {
+            if (lane + 64 * v < LPQ) {
+                f32x4 x = vals[k][v];
+                if (ragged) {
+                    const int xb = ((X0 >> 2) + tc[v]) * 4;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) x[c] = xb + c < Wl ? x[c] : 0.0f;
+                }
+                float *row = &sm.win[qq * WQ + rr[v] * WW + 4 * tc[v] + 3 - (X0 & 3)];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) row[c] = x[c];
+            }
+        }
+    }
+}
+
 constexpr int lookup_threads(int S, int QB) { return (QB * S + 63) / 64 * 64; }
 
 // ABL: diagnostic ablations for tools/kbench_lookup.hip only (0 in the library): bit 0 = no
 // neighbourhood loads, bit 1 = no output stores, bit 2 = no coords load, bit 3 = plain (L2-cached)
-// output stores instead of the non-temporal ones (lookup_kernel), bit 4 = non-temporal window loads.
+// output stores instead of the non-temporal ones (lookup_kernel).
 // One pyramid level of one block of QB queries (NT threads): the whole lookup of
 // lookup_kernel below.  emit(j, acc) receives output tap (i, j) of this thread's window column
 // i = tid / QB for query q = tid % QB (called only for live queries).  Shared by lookup_kernel
-// (global NCHW stores) and lookup_conv_kernel (LDS tile feeding the fused 1x1 convolution).
-// The lookup of one block with its coords already loaded (cxv, cyv: this thread's query; 0 for
-// threads without one).
+// (global NCHW stores), lookup_conv_kernel (LDS tile feeding the fused 1x1 convolution) and
+// lookup_conv_bwd_dw_kernel.  The lookup of one block with its coords already loaded (cxv, cyv:
+// this thread's query; 0 for threads without one).
 template <int S, int QB, int NT, int ABL, class Emit>
 __device__ __forceinline__ void lookup_block_v(LookupSmem<S, QB> &sm, const float *__restrict__ P, float cxv,
                                                float cyv, int b, int n0, int N, int H, int W, int l, int tid,
                                                Emit emit) {
     constexpr int R = (S - 1) / 2;
     using SM = LookupSmem<S, QB>;
-    constexpr int WIN = SM::WIN, WSTR = SM::WSTR;
+    constexpr int WIN = SM::WIN, WW = SM::WW, WQ = SM::WQ;
     const int Hl = H >> l, Wl = W >> l;
     const float inv_scale = 1.0f / (float)(1 << l);
-    const size_t mapsz = (size_t)Hl * Wl;
+    const unsigned mapsz = (unsigned)map_floats(Hl, Wl);
+    const int TW = map_tiles(Wl);
     const size_t qbase = (size_t)b * N + n0;
 
     const int q = tid % QB;
@@ -247,15 +241,14 @@ __device__ __forceinline__ void lookup_block_v(LookupSmem<S, QB> &sm, const floa
     }
 
     // ---- 2. neighbourhoods -> LDS ----
-    gather_window_wave<S, QB, NT, (ABL & 1) != 0, (ABL & 16) != 0>(sm.win, sm.ax, sm.ay, P, qbase, mapsz, n0, N, Wl, Hl,
-                                                                    tid);
+    gather_window_tiled<S, QB, NT, (ABL & 1) != 0>(sm, P, qbase, mapsz, n0, N, Wl, Hl, tid);
     __syncthreads();
     const int mode = sm.flags;
     if (!act) return;
 
     // ---- 3. outputs (i, 0..S-1) of query q ----
     const int ax = sm.ax[q], ay = sm.ay[q];
-    const float *wq = &sm.win[q * WSTR];
+    const float *wq = &sm.win[q * WQ + 3];
     const float x0 = tx.f, ex = tx.lo, wx = tx.hi;
     if (mode == 0) {
         // regular taps: tap (i, j) has corners at neighbourhood column i, i+1 and rows j, j+1,
@@ -265,8 +258,8 @@ __device__ __forceinline__ void lookup_block_v(LookupSmem<S, QB> &sm, const floa
         float c0[S + 1], c1[S + 1];
 #pragma unroll
         for (int j = 0; j <= S; ++j) {
-            c0[j] = col[j * WIN];
-            c1[j] = col[j * WIN + 1];
+            c0[j] = col[j * WW];
+            c1[j] = col[j * WW + 1];
         }
 #pragma unroll
         for (int j = 0; j < S; ++j) {
@@ -286,11 +279,11 @@ __device__ __forceinline__ void lookup_block_v(LookupSmem<S, QB> &sm, const floa
         for (int j = 0; j < S; ++j) {
             const float y0 = sm.ty[0][j][q], ey = sm.ty[1][j][q], ny = sm.ty[2][j][q];
             const int cy = far ? 0 : (int)y0 - ay;
-            const float *c = col + cy * WIN;
+            const float *c = col + cy * WW;
             float acc = __fmul_rn(c[0], __fmul_rn(ey, ex));
             acc = __builtin_fmaf(c[1], __fmul_rn(ey, wx), acc);
-            acc = __builtin_fmaf(c[WIN], __fmul_rn(ny, ex), acc);
-            acc = __builtin_fmaf(c[WIN + 1], __fmul_rn(ny, wx), acc);
+            acc = __builtin_fmaf(c[WW], __fmul_rn(ny, ex), acc);
+            acc = __builtin_fmaf(c[WW + 1], __fmul_rn(ny, wx), acc);
             if (qok) emit(j, acc);
         }
     } else {
@@ -299,8 +292,8 @@ __device__ __forceinline__ void lookup_block_v(LookupSmem<S, QB> &sm, const floa
             if (!in_map(xf, yf, Wl, Hl)) return 0.0f;
             const int xi = (int)xf, yi = (int)yf;
             const unsigned ux = (unsigned)(xi - ax), uy = (unsigned)(yi - ay);
-            if (ux < (unsigned)WIN && uy < (unsigned)WIN) return wq[uy * WIN + ux];
-            return Pq[(size_t)yi * Wl + xi];
+            if (ux < (unsigned)WIN && uy < (unsigned)WIN) return wq[uy * WW + ux];
+            return Pq[map_cell(yi, xi, TW)];
         };
         const float x1 = __fadd_rn(x0, 1.0f);
         for (int j = 0; j < S; ++j) {
@@ -334,8 +327,8 @@ __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
     __shared__ LookupSmem<S, QB> sm;
     const int N = NQ;  // query pixels per batch item (H*W, or a row slab of it)
     const int nqb = (N + QB - 1) / QB;
-    const int b = blockIdx.x / nqb;
-    const int n0 = (blockIdx.x - b * nqb) * QB;
+    const int b = __builtin_amdgcn_readfirstlane(blockIdx.x / nqb);
+    const int n0 = __builtin_amdgcn_readfirstlane((blockIdx.x - b * nqb) * QB);
     const int l = blockIdx.y;
     const int i = threadIdx.x / QB, n = n0 + threadIdx.x % QB;
     float *o = out + (((size_t)b * L + l) * K + (size_t)i * S) * N + n;
@@ -1879,6 +1872,65 @@ hipError_t launch_lookup_bwd_fold(const float *const *coords, const float *const
         case 7: return launch_fused_s<15>(lk, o, s);
         default: return hipErrorInvalidValue;
     }
+}
+
+// ---------------------------------------------------------------------------------------
+// Tiled pyramid (corr_common.h) <-> the reference's row-major [BN][H_l][W_l]: EXPORT
+// materialises corr_pyramid's view (corr.py:16,24,27,36 read it as [B*N, 1, H_l, W_l]); IMPORT
+// installs a pyramid given in that layout (padding cells zeroed).  One thread per 16-B tile row.
+// ---------------------------------------------------------------------------------------
+namespace {
+template <bool EXPORT>
+__global__ __launch_bounds__(256) void pyramid_layout_kernel(const float *__restrict__ src, float *__restrict__ dst,
+                                                             long BN, int Hl, int Wl) {
+    const int TW = map_tiles(Wl);
+    const long per = (long)map_floats(Hl, Wl) / 4;  // tile rows per map
+    const long total = BN * per;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const long n = i / per;
+        const int rem = (int)(i - n * per);
+        const int t = rem >> 2, Y = 4 * (t / TW) + (rem & 3), X = 4 * (t % TW);
+        const size_t row = ((size_t)n * Hl + Y) * Wl;
+        if (EXPORT) {
+            if (Y >= Hl) continue;
+            const f32x4 v = reinterpret_cast<const f32x4 *>(src)[i];
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (X + c < Wl) dst[row + X + c] = v[c];
+        } else {
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (Y < Hl && X + c < Wl) v[c] = src[row + X + c];
+            reinterpret_cast<f32x4 *>(dst)[i] = v;
+        }
+    }
+}
+
+template <bool EXPORT>
+hipError_t launch_pyramid_layout(const ConstLevelPtrs &src, long BN, int H, int W, int levels, const LevelPtrs &dst,
+                                 hipStream_t s) {
+    for (int l = 0; l < levels; ++l) {
+        const int Hl = H >> l, Wl = W >> l;
+        const long rows = BN * (long)(map_floats(Hl, Wl) / 4);
+        const int grid = (int)std::min<long>((rows + 255) / 256, 8192);
+        hipLaunchKernelGGL((pyramid_layout_kernel<EXPORT>), dim3(grid), dim3(256), 0, s, src.p[l], dst.p[l], BN, Hl,
+                           Wl);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+}  // namespace
+
+hipError_t launch_pyramid_export(const ConstLevelPtrs &pyr, long BN, int H, int W, int levels, const LevelPtrs &out,
+                                 hipStream_t s) {
+    return launch_pyramid_layout<true>(pyr, BN, H, W, levels, out, s);
+}
+
+hipError_t launch_pyramid_import(const ConstLevelPtrs &src, long BN, int H, int W, int levels, const LevelPtrs &pyr,
+                                 hipStream_t s) {
+    return launch_pyramid_layout<false>(src, BN, H, W, levels, pyr, s);
 }
 
 }  // namespace corr

@@ -30,7 +30,9 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
            "corr_voxel_grid", "corr_lookup_conv", "corr_lookup_conv_weights", "corr_lookup_conv_weights_bytes", "corr_voxel_grid_tbilinear_workspace",
            "corr_voxel_grid_tbilinear", "corr_lookup_bwd_multi", "corr_pool_fold", "corr_backward_workspace",
            "corr_backward", "corr_convex_upsample_bwd_workspace", "corr_convex_upsample_bwd", "corr_build_region",
-           "corr_lookup_conv_bwd_workspace", "corr_lookup_conv_bwd")
+           "corr_lookup_conv_bwd_workspace", "corr_lookup_conv_bwd", "corr_map_floats", "corr_pyramid_export",
+           "corr_pyramid_import")
+ABI_VERSION = 200  # include/corr_mi355x.h: the tiled value pyramid
 
 # Build algorithms (include/corr_mi355x.h).  BF16X6 is the default: every fp32 feature split
 # exactly into three bf16 pieces, the six largest piece products on the bf16 MFMA, fp32
@@ -83,6 +85,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
     vp, i, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
     lib.corr_version.argtypes, lib.corr_version.restype = [], i
     lib.corr_last_error.argtypes, lib.corr_last_error.restype = [], ctypes.c_char_p
+    lib.corr_map_floats.argtypes, lib.corr_map_floats.restype = [i, i], sz
+    lib.corr_pyramid_export.argtypes = [vp, i, i, i, i, vp, vp]
+    lib.corr_pyramid_import.argtypes = [vp, i, i, i, i, vp, vp]
     lib.corr_build.argtypes = [vp, vp, i, i, i, i, i, vp, vp]
     lib.corr_lookup.argtypes = [vp, vp, i, i, i, i, i, vp, vp]
     lib.corr_lookup_bwd.argtypes = [vp, vp, i, i, i, i, i, vp, vp]
@@ -133,8 +138,11 @@ def load(path: str | None = None) -> ctypes.CDLL:
               "corr_build_ex", "corr_build_bwd_ex", "corr_forward_splat",
               "corr_convex_upsample", "corr_voxel_grid", "corr_lookup_conv", "corr_lookup_conv_weights",
               "corr_voxel_grid_tbilinear", "corr_lookup_bwd_multi", "corr_pool_fold", "corr_backward_workspace",
-              "corr_backward", "corr_convex_upsample_bwd", "corr_lookup_conv_bwd"):
+              "corr_backward", "corr_convex_upsample_bwd", "corr_lookup_conv_bwd", "corr_pyramid_export",
+              "corr_pyramid_import"):
         getattr(lib, f).restype = i
+    if lib.corr_version() != ABI_VERSION:
+        raise RuntimeError(f"{so} has ABI {lib.corr_version()}, eraft_amd needs {ABI_VERSION}: rebuild it")
     if path is None:
         _lib = lib
     return lib
@@ -176,6 +184,32 @@ def _nq(t):
     return n
 
 
+def pyramid_export(levels, H, W, out=None):
+    """corr_pyramid_export: the tiled levels ([BN, map_floats]) -> the reference's layout, a list
+    of [BN, 1, H_l, W_l] tensors (allocated unless `out` is given)."""
+    BN = levels[0].shape[0]
+    if out is None:
+        out = [torch.empty((BN, 1, H >> l, W >> l), dtype=torch.float32, device=levels[0].device)
+               for l in range(len(levels))]
+    with torch.cuda.device(levels[0].device):
+        _check(load().corr_pyramid_export(_ptrs(levels, "pyr"), BN, H, W, len(levels), _ptrs(out, "out"),
+                                          _stream(levels[0])))
+    return out
+
+
+def pyramid_import(src, levels, H, W):
+    """corr_pyramid_import: reference-layout levels [BN, 1, H_l, W_l] (any contiguous view) ->
+    the tiled `levels` (padding cells zeroed)."""
+    BN = levels[0].shape[0]
+    src = [t.contiguous() for t in src]
+    for l, t in enumerate(src):
+        if t.numel() != BN * (H >> l) * (W >> l):
+            raise ValueError(f"level {l} has {t.numel()} values, expected {BN}x{H >> l}x{W >> l}")
+    with torch.cuda.device(levels[0].device):
+        _check(load().corr_pyramid_import(_ptrs(src, "src"), BN, H, W, len(levels), _ptrs(levels, "pyr"),
+                                          _stream(levels[0])))
+
+
 def build_workspace(fmap1, fmap2, algo=None):
     """A device workspace for corr_build_ex (None when the algorithm needs none).  fmap2: the
     target map or just its shape [B, D, H, W]."""
@@ -190,7 +224,7 @@ def build_workspace(fmap1, fmap2, algo=None):
 
 
 def build(fmap1, fmap2, levels, algo=None, workspace=None):
-    """corr_build_ex into caller-allocated levels [B*NQ, 1, H>>l, W>>l].  fmap1 may be a row
+    """corr_build_ex into caller-allocated tiled levels (corr._alloc_pyramid).  fmap1 may be a row
     slab [B, D, rows, W] of the query map; fmap2 is the full target map [B, D, H, W].
     algo: BUILD_BF16X6 (default, see default_algo), BUILD_F16X3 or BUILD_FP32."""
     algo = default_algo() if algo is None else algo
@@ -209,7 +243,7 @@ REGION_PACK_QUERIES = 1
 
 
 def build_region(fmap1, fmap2_rows, y0, y1, H, levels, workspace, pack_queries, algo=BUILD_BF16X6):
-    """corr_build_region: the pyramid entries of target rows [y0, y1) (levels [B*NQ, 1, H>>l, W>>l])
+    """corr_build_region: the pyramid entries of target rows [y0, y1) (tiled levels, corr._alloc_pyramid)
     from fmap2_rows [B, D, y1 - y0, W]; workspace from build_workspace(fmap1, <full fmap2 shape>)."""
     B, D, rows, W = fmap2_rows.shape
     if rows != y1 - y0:

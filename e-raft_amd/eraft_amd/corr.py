@@ -33,9 +33,31 @@ def level_shapes(H: int, W: int, num_levels: int):
     return [(H >> l, W >> l) for l in range(num_levels)]
 
 
-def _alloc_pyramid(B: int, H: int, W: int, num_levels: int, like: torch.Tensor, zero=False):
-    """One allocation holding every level, viewed as the reference's [B*H*W, 1, H_l, W_l]."""
-    BN = B * H * W
+def map_floats(Hl: int, Wl: int) -> int:
+    """Floats of one query's tiled level map (include/corr_mi355x.h: 4x4-cell tiles of 64 B)."""
+    return ((Hl + 3) // 4) * ((Wl + 3) // 4) * 16
+
+
+def _alloc_pyramid(B: int, H: int, W: int, num_levels: int, like: torch.Tensor, zero=False, NQ=None):
+    """The build's output / the lookups' input: one allocation holding every level in the
+    library's tiled layout, level l viewed [B*NQ, map_floats(H_l, W_l)] (NQ = H*W queries per
+    batch item by default; a row slab's otherwise).  Materialise the reference's
+    [B*N, 1, H_l, W_l] view with _lib.pyramid_export (CorrBlock.corr_pyramid does)."""
+    BN = B * (H * W if NQ is None else NQ)
+    sizes = [BN * map_floats(h, w) for h, w in level_shapes(H, W, num_levels)]
+    offs, tot = [], 0
+    for s in sizes:  # multiples of 16 floats: every level 64-B aligned
+        offs.append(tot)
+        tot += s
+    fn = torch.zeros if zero else torch.empty
+    buf = fn(tot, dtype=torch.float32, device=like.device)
+    return [buf[o:o + s].view(BN, s // BN) for o, s in zip(offs, sizes)]
+
+
+def _alloc_grad_pyramid(B: int, H: int, W: int, num_levels: int, like: torch.Tensor, zero=False, NQ=None):
+    """A gradient pyramid: the reference's row-major layout, level l [B*NQ, 1, H_l, W_l] in one
+    allocation (corr_lookup_bwd / corr_pool_bwd / corr_backward's scratch; level 0 ends as dC)."""
+    BN = B * (H * W if NQ is None else NQ)
     shapes = level_shapes(H, W, num_levels)
     sizes = [BN * h * w for h, w in shapes]
     # keep every level 16-byte aligned (float4 paths)
@@ -88,13 +110,14 @@ def _weight_pack(weight):
 class _State:
     """Per-block state shared by the build and lookup autograd nodes."""
 
-    __slots__ = ("levels", "grad_levels", "H", "W", "radius", "stash", "trains")
+    __slots__ = ("levels", "grad_levels", "H", "W", "radius", "stash", "trains", "direct")
 
     def __init__(self, H, W, radius):
         self.trains = False      # the build is in the autograd graph (gradients reach the fmaps)
-        self.levels = None
+        self.levels = None       # the tiled pyramid (_alloc_pyramid)
         self.grad_levels = None  # per-lookup path: the accumulated gradient pyramid
         self.stash = []          # fused path: (coords, grad_out) of every lookup backward
+        self.direct = None       # gradients that reached corr_pyramid's exported view, per level
         self.H, self.W, self.radius = H, W, radius
 
 
@@ -102,42 +125,44 @@ class _BuildFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, fmap1, fmap2, num_levels, state):
         B, _, H, W = fmap1.shape
-        levels = _alloc_pyramid(B, H, W, num_levels, fmap1)
-        _lib.build(fmap1, fmap2, levels)
-        # the lookups read state.levels, not these outputs: no zero-filled level gradients
+        state.levels = _alloc_pyramid(B, H, W, num_levels, fmap1)
+        _lib.build(fmap1, fmap2, state.levels)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(fmap1, fmap2)
         ctx.state = state
-        # autograd anchor: every lookup depends on it; its value is never read (no fill kernel)
-        token = fmap1.new_empty(())
-        return (*levels, token)
+        ctx.num_levels = num_levels
+        # autograd anchor: every lookup (and corr_pyramid's exported view) depends on it; its value
+        # is never read (no fill kernel)
+        return fmap1.new_empty(())
 
     @staticmethod
-    def backward(ctx, *grads):
+    def backward(ctx, _token_grad):
         fmap1, fmap2 = ctx.saved_tensors
         st = ctx.state
-        direct = grads[:-1]  # grads[-1] (the token's) carries no value
+        L = ctx.num_levels
+        direct = st.direct if st.direct is not None else [None] * L
+        st.direct = None
         stash, st.stash = st.stash, []
         if st.grad_levels is None and not any(g is not None for g in direct):
             if not stash:
                 return None, None, None, None
             # fused: every lookup's backward + the fold + the GEMMs in corr_backward
             B, _, H, W = fmap1.shape
-            gl = _alloc_pyramid(B, H, W, len(direct), fmap1)  # scratch, overwritten
+            gl = _alloc_grad_pyramid(B, H, W, L, fmap1)  # scratch, overwritten
             df1, df2 = _lib.backward([c for c, _ in stash], [g for _, g in stash], st.radius, gl, fmap1, fmap2)
             return df1, df2, None, None
         gl = st.grad_levels
         if stash:  # direct gradients reached corr_pyramid: run the stashed lookups' backward too
             if gl is None:
                 B, _, H, W = fmap1.shape
-                gl = _alloc_pyramid(B, H, W, len(direct), fmap1, zero=True)
+                gl = _alloc_grad_pyramid(B, H, W, L, fmap1, zero=True)
             for c, g in stash:
                 _lib.lookup_bwd(c, g, st.radius, gl)
         if any(g is not None for g in direct):
             # gradients that reached corr_pyramid outside the lookups
             if gl is None:
                 B, _, H, W = fmap1.shape
-                gl = _alloc_pyramid(B, H, W, len(direct), fmap1, zero=True)
+                gl = _alloc_grad_pyramid(B, H, W, L, fmap1, zero=True)
             for acc, g in zip(gl, direct):
                 if g is not None:
                     acc.add_(g)
@@ -147,6 +172,30 @@ class _BuildFn(torch.autograd.Function):
         _lib.pool_bwd(gl, st.H, st.W)
         df1, df2 = _lib.build_bwd(gl[0], fmap1, fmap2)
         return df1, df2, None, None
+
+
+class _PyramidViewFn(torch.autograd.Function):
+    """corr_pyramid under autograd: the tiled pyramid exported to the reference's
+    [B*N, 1, H_l, W_l] levels (corr.py:16,24,27,36); gradients that reach them are kept for the
+    build's backward, which adds them to the lookups' gradient pyramid (as autograd sums a
+    level's gradients in the reference)."""
+
+    @staticmethod
+    def forward(ctx, token, state):
+        ctx.state = state
+        ctx.set_materialize_grads(False)
+        return tuple(_lib.pyramid_export(state.levels, state.H, state.W))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        st = ctx.state
+        if st.direct is None:
+            st.direct = [None] * len(grads)
+        for l, g in enumerate(grads):
+            if g is not None:
+                st.direct[l] = g.contiguous() if st.direct[l] is None else st.direct[l] + g
+        # no gradient for the token: the engine still runs the build's backward after this one
+        return None, None
 
 
 class _LookupFn(torch.autograd.Function):
@@ -169,7 +218,7 @@ class _LookupFn(torch.autograd.Function):
         else:
             if st.grad_levels is None:
                 B, _, H, W = coords.shape
-                st.grad_levels = _alloc_pyramid(B, H, W, len(st.levels), coords, zero=True)
+                st.grad_levels = _alloc_grad_pyramid(B, H, W, len(st.levels), coords, zero=True)
             _lib.lookup_bwd(coords, grad_out.contiguous(), radius, st.grad_levels)
 
     @staticmethod
@@ -204,6 +253,8 @@ class _LookupConvFn(torch.autograd.Function):
         coords, weight, out = ctx.saved_tensors
         st = ctx.state
         g = grad_out.contiguous().float()
+        if g.data_ptr() % 16:  # the kernel's 16-B loads need an aligned base (a view with an odd offset)
+            g = g.clone()
         B, O, H, W = g.shape
         C = len(st.levels) * (2 * ctx.radius + 1) ** 2
         dev = coords.device
@@ -232,22 +283,43 @@ class CorrBlock:
         _, _, H, W = fmap1.shape
         self._state = _State(H, W, radius)
         self._token = None
+        self._view = None  # corr_pyramid's exported levels, made on first access
         if torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad):
-            outs = _BuildFn.apply(fmap1, fmap2, num_levels, self._state)
-            self.corr_pyramid = list(outs[:-1])
-            self._token = outs[-1]
+            self._token = _BuildFn.apply(fmap1, fmap2, num_levels, self._state)
             self._state.trains = True
         else:
             B = fmap1.shape[0]
-            self.corr_pyramid = _alloc_pyramid(B, H, W, num_levels, fmap1)
-            _lib.build(fmap1.detach(), fmap2.detach(), self.corr_pyramid)
-        self._state.levels = [p.detach() for p in self.corr_pyramid]
+            self._state.levels = _alloc_pyramid(B, H, W, num_levels, fmap1)
+            _lib.build(fmap1.detach(), fmap2.detach(), self._state.levels)
+
+    @property
+    def corr_pyramid(self):
+        """The pyramid as the reference holds it (corr.py:16,24,27,36): a list of num_levels
+        tensors [B*H*W, 1, H_l, W_l].  The library keeps it tiled (include/corr_mi355x.h), so the
+        view is materialised (corr_pyramid_export) on first access; with the build in the autograd
+        graph, gradients that reach it flow to both fmaps as in the reference.  Assigning a list
+        of such tensors installs them (corr_pyramid_import) for the following lookups."""
+        if self._view is None:
+            st = self._state
+            if self._token is not None and torch.is_grad_enabled():
+                self._view = list(_PyramidViewFn.apply(self._token, st))
+            else:
+                self._view = _lib.pyramid_export(st.levels, st.H, st.W)
+        return self._view
+
+    @corr_pyramid.setter
+    def corr_pyramid(self, levels):
+        st = self._state
+        if len(levels) != len(st.levels):
+            raise ValueError(f"corr_pyramid needs {len(st.levels)} levels (got {len(levels)})")
+        _lib.pyramid_import([l.detach() for l in levels], st.levels, st.H, st.W)
+        self._view = None
 
     def _check_coords(self, coords):
         if coords.dim() != 4 or coords.shape[1] != 2:
             raise ValueError(f"coords must be [B, 2, H, W] (got {tuple(coords.shape)})")
         B, _, H, W = coords.shape
-        if B * H * W != self.corr_pyramid[0].shape[0] or (H, W) != (self._state.H, self._state.W):
+        if B * H * W != self._state.levels[0].shape[0] or (H, W) != (self._state.H, self._state.W):
             raise ValueError("coords do not match the feature maps this block was built from")
 
     def __call__(self, coords):
@@ -291,6 +363,6 @@ class CorrBlock:
         """model/corr.py:52-60: all-pairs volume [B, H, W, 1, H, W] scaled by 1/sqrt(D)."""
         _validate_fmaps(fmap1, fmap2, 1)
         B, _, H, W = fmap1.shape
-        (lvl,) = _alloc_pyramid(B, H, W, 1, fmap1)
-        _lib.build(fmap1.detach().contiguous(), fmap2.detach().contiguous(), [lvl])
-        return lvl.view(B, H, W, 1, H, W)
+        lvl = _alloc_pyramid(B, H, W, 1, fmap1)
+        _lib.build(fmap1.detach().contiguous(), fmap2.detach().contiguous(), lvl)
+        return _lib.pyramid_export(lvl, H, W)[0].view(B, H, W, 1, H, W)

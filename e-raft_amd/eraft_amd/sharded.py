@@ -32,7 +32,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from .corr import _alloc_pyramid
+from .corr import _alloc_grad_pyramid, _alloc_pyramid
 
 
 def row_partition(H: int, world: int, rank: int):
@@ -79,9 +79,8 @@ class HipRows:
 
     @staticmethod
     def zero_pyramid(B, NQ, H, W, num_levels, like):
-        lv = _alloc_pyramid_rows(B, NQ, H, W, num_levels, like)
-        lv[0]._base.zero_()
-        return lv
+        """A zeroed gradient pyramid of the slab (the reference's row-major layout)."""
+        return _alloc_grad_pyramid(B, H, W, num_levels, like, zero=True, NQ=NQ)
 
     @staticmethod
     def lookup_bwd(coords_rows, grad_rows, radius, grad_levels, H, W):
@@ -102,7 +101,7 @@ class HipRows:
         in one call -> (dfmap1 of the slab, this slab's partial dfmap2)."""
         B, _, rows, W = f1_rows.shape
         H = f2.shape[2]
-        gl = _alloc_pyramid_rows(B, rows * W, H, W, num_levels, f2)  # scratch
+        gl = _alloc_grad_pyramid(B, H, W, num_levels, f2, NQ=rows * W)  # scratch
         return _lib.backward(coords_list, grad_list, radius, gl, f1_rows, f2)
 
 
@@ -136,15 +135,26 @@ def _broadcast_build_chunked(backend, f1_rows, fmap2, num_levels, bounds, src, g
     return levels
 
 
+_CHUNKS_AGREED = {}
+
+
+def _agreed_chunks(group, key, local, device):
+    """The broadcast's chunk count, agreed over the group once per (group, key): the MIN of the
+    ranks' own choices.  Each rank's choice depends on its environment (ERAFT_AMD_BUILD decides
+    whether the region build exists), and ranks that disagreed would issue different numbers of
+    broadcasts and hang.  key holds only values every rank shares (H, levels, the requested
+    count), so every rank hits or misses the cache together."""
+    k = (id(group), key)
+    if k not in _CHUNKS_AGREED:
+        t = torch.tensor([local], dtype=torch.int64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        _CHUNKS_AGREED[k] = int(t.item())
+    return _CHUNKS_AGREED[k]
+
+
 def _alloc_pyramid_rows(B, NQ, H, W, num_levels, like):
-    shapes = [(H >> l, W >> l) for l in range(num_levels)]
-    sizes = [B * NQ * h * w for h, w in shapes]
-    offs, tot = [], 0
-    for s in sizes:
-        offs.append(tot)
-        tot += (s + 3) // 4 * 4
-    buf = torch.empty(tot, dtype=torch.float32, device=like.device)
-    return [buf[o:o + s].view(B * NQ, 1, h, w) for o, s, (h, w) in zip(offs, sizes, shapes)]
+    """The tiled pyramid of a slab of NQ queries per batch item (corr._alloc_pyramid)."""
+    return _alloc_pyramid(B, H, W, num_levels, like, NQ=NQ)
 
 
 class _ShardState:
@@ -252,10 +262,11 @@ class Fmap2DoubleBuffer:
 
     Inference only: the buffers are detached copies that the prefetch two pairs later
     overwrites, so no gradient could reach the caller's fmap2 through them, and a delayed
-    backward would read a later pair's features.  prefetch() raises on the source rank when
-    handed an fmap2 that requires grad with autograd enabled (after its broadcast completed, so
-    the other ranks are not left inside it), and RowShardedCorrBlock raises on every rank when
-    handed a PendingFmap2 while its fmap1 requires grad; train with the blocking broadcast
+    backward would read a later pair's features.  prefetch() therefore runs only with autograd
+    disabled (torch.no_grad(), as E-RAFT's eval runs, test.py:84) and raises on EVERY rank
+    otherwise — before any collective, on a condition every rank of an SPMD job shares, so no
+    rank is left inside a broadcast — and RowShardedCorrBlock raises on every rank when handed a
+    PendingFmap2 while its fmap1 requires grad; train with the blocking broadcast
     (RowShardedCorrBlock(fmap1, fmap2))."""
 
     def __init__(self, shape, device, group=None, src=0, dtype=torch.float32):
@@ -265,20 +276,19 @@ class Fmap2DoubleBuffer:
         self.k = 0
 
     def prefetch(self, fmap2=None):
+        if torch.is_grad_enabled():
+            # the grad mode is the same on every rank, so all ranks refuse together (whereas only
+            # the source rank could see its fmap2's requires_grad)
+            raise RuntimeError("Fmap2DoubleBuffer is inference-only (its buffers carry no gradient "
+                               "back to fmap2): call prefetch under torch.no_grad(), or train with "
+                               "RowShardedCorrBlock(fmap1, fmap2)")
         buf = self.bufs[self.k % 2]
         self.k += 1
         if self.rank == self.src:
             if fmap2 is None:
                 raise ValueError(f"rank {self.src} is the broadcast source: pass its fmap2")
             buf.copy_(fmap2.detach())
-        pending = RowShardedCorrBlock.prefetch(buf, src=self.src, group=self.group)
-        if self.rank == self.src and torch.is_grad_enabled() and fmap2.requires_grad:
-            # refuse only after the broadcast is issued and done, so the other ranks' matching
-            # broadcast completes and no rank is left inside a collective
-            pending.wait()
-            raise RuntimeError("Fmap2DoubleBuffer is inference-only (its buffers carry no gradient "
-                               "back to fmap2); train with RowShardedCorrBlock(fmap1, fmap2)")
-        return pending
+        return RowShardedCorrBlock.prefetch(buf, src=self.src, group=self.group)
 
 
 class RowShardedCorrBlock:
@@ -325,9 +335,14 @@ class RowShardedCorrBlock:
         self.h0, self.h1 = row_partition(H, self.world, self.rank)
         self.backend = backend
         region = hasattr(backend, "build_region") and backend.region_supported(num_levels)
+        asked = chunks
         if chunks == 0:
             chunks = 4 if region and H >= 32 else 1
-        bounds = chunk_bounds(H, chunks) if region and chunks > 1 else None
+        if not region:
+            chunks = 1
+        if broadcast and self.world > 1:
+            chunks = _agreed_chunks(group, (H, num_levels, asked), chunks, fmap2.device)
+        bounds = chunk_bounds(H, chunks) if chunks > 1 else None
         chunked = broadcast and self.world > 1 and bounds is not None and len(bounds) > 1
         if broadcast and self.world > 1 and not chunked:
             with torch.no_grad():

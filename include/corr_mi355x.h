@@ -10,9 +10,19 @@
  *
  * Layouts (fp32, C-contiguous), N = H*W, K = (2*radius+1)^2:
  *   fmap1, fmap2          [B][D][H][W]                       (corr.py:53-56)
- *   pyramid level l       [B*N][H>>l][W>>l]                  (corr.py:21-27, floor halving)
+ *   pyramid level l       B*N query maps of H_l x W_l cells, H_l = H>>l, W_l = W>>l
+ *                         (corr.py:21-27, floor halving), each map TILED: 4x4-cell tiles of 64 B,
+ *                         tiles row-major, cells row-major inside a tile:
+ *                           cell (y, x) at ((y/4) * ceil(W_l/4) + x/4) * 16 + (y%4) * 4 + x%4,
+ *                         corr_map_floats(H_l, W_l) = ceil(H_l/4) * ceil(W_l/4) * 16 floats per
+ *                         map, maps consecutive (query q's map at q * corr_map_floats).  Cells
+ *                         past W_l / H_l are padding (the builds may write them; never read).
+ *                         Level pointers 16-byte aligned.  The reference's [B*N][H_l][W_l]
+ *                         (corr.py's corr_pyramid) is corr_pyramid_export's output.
  *   coords                [B][2][H][W], ch0 = x, ch1 = y     (utils.py:24-27, corr.py:31)
  *   lookup output         [B][levels*K][H][W]                (corr.py:46-50)
+ *   gradient pyramids     [B*N][H>>l][W>>l] row-major (corr_lookup_bwd, corr_pool_bwd,
+ *                         corr_backward's scratch: the reference's layout; level 0 = dC [B*N][N])
  *
  * Return value: CORR_OK (0) or a negative CORR_E* code; corr_last_error() then returns a
  * thread-local message.  The reference performs no validation (torch raises inside
@@ -45,19 +55,35 @@ extern "C" {
  *   103: CORR_BUILD_BF16X6, corr_build_region, corr_lookup_conv_bwd (the packed weight buffer
  *        grew: size it with corr_lookup_conv_weights_bytes()).
  *   104: corr_build_bwd_ex / corr_backward accept CORR_BUILD_BF16X6 (backward GEMMs no narrower
- *        than fp32); E-RAFT's default backward for the BF16X6 build. */
+ *        than fp32); E-RAFT's default backward for the BF16X6 build.
+ *   200: the value pyramid (the builds' output, the lookups' input) is TILED (see Layouts;
+ *        16-B aligned levels, corr_map_floats per map); corr_map_floats, corr_pyramid_export,
+ *        corr_pyramid_import.  Gradient pyramids keep the reference layout. */
 int corr_version(void);
 
 /* Thread-local description of the last error on this thread ("" if none). */
 const char *corr_last_error(void);
 
+/* Floats of one query's tiled level map of H_l x W_l cells (ceil(H_l/4) * ceil(W_l/4) * 16). */
+size_t corr_map_floats(int Hl, int Wl);
+
+/*
+ * The tiled pyramid <-> the reference's layout.  corr_pyramid_export writes every level as
+ * [BN][H>>l][W>>l] row-major (the reference's corr_pyramid[l] viewed [B*N, 1, H_l, W_l],
+ * corr.py:16,24,27,36); corr_pyramid_import tiles such levels into a pyramid (padding cells
+ * zeroed), so a pyramid computed elsewhere can be looked up.  BN = B * NQ query maps; `pyr`,
+ * `src`, `out` are host arrays of `levels` device pointers; the tiled side 16-B aligned.
+ */
+int corr_pyramid_export(const float *const *pyr, int BN, int H, int W, int levels, float *const *out, void *stream);
+int corr_pyramid_import(const float *const *src, int BN, int H, int W, int levels, float *const *pyr, void *stream);
+
 /*
  * All-pairs correlation + average-pool pyramid.  Replaces CorrBlock.__init__
  * (model/corr.py:13-27) together with CorrBlock.corr (model/corr.py:52-60):
- *   pyr[0][b*N + n][y][x] = sum_d fmap1[b][d][n] * fmap2[b][d][y*W + x] / sqrt(float(D))
- *   pyr[l][q][y][x]       = avg_pool2d(pyr[l-1], 2, stride 2)[q][y][x]   (floor)
- * `pyr` is a HOST array of `levels` device pointers.  levels == 1 gives CorrBlock.corr's
- * [B,H,W,1,H,W] volume.  fp32 in / fp32 MFMA accumulate / fp32 out (CORR_BUILD_FP32;
+ *   pyr[0][b*N + n](y, x) = sum_d fmap1[b][d][n] * fmap2[b][d][y*W + x] / sqrt(float(D))
+ *   pyr[l][q](y, x)       = avg_pool2d(pyr[l-1], 2, stride 2)[q](y, x)   (floor)
+ * (cell (y, x) of query q's tiled map, see Layouts.)  `pyr` is a HOST array of `levels` device
+ * pointers.  levels == 1 gives CorrBlock.corr's [B,H,W,1,H,W] volume (export it for that view).  fp32 in / fp32 MFMA accumulate / fp32 out (CORR_BUILD_FP32;
  * corr_build_ex selects the faster CORR_BUILD_BF16X6, no less accurate, or CORR_BUILD_F16X3).
  */
 int corr_build(const float *fmap1, const float *fmap2, int B, int D, int H, int W, int levels,
@@ -166,7 +192,7 @@ int corr_build_bwd(const float *grad_c, const float *fmap1, const float *fmap2, 
  * reference has no multi-GPU CorrBlock).  The queries are NQ consecutive
  * pixels of fmap1 — a block of whole rows, NQ = rows*W — while the targets are all H*W
  * pixels of fmap2:
- *   fmap1_rows [B][D][NQ]; pyramid level l [B*NQ][H>>l][W>>l];
+ *   fmap1_rows [B][D][NQ]; pyramid level l: B*NQ tiled maps of (H>>l) x (W>>l) cells;
  *   coords_rows [B][2][NQ]; out_rows [B][levels*K][NQ]; grad_c [B*NQ][H*W].
  * Every query's arithmetic is identical to the full-size call, so a row partition
  * reproduces the unsharded results bit for bit.  corr_build_bwd_rows writes this slab's

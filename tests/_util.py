@@ -38,3 +38,33 @@ def bit_equal(a, b):
     if not np.array_equal(na, nb):
         return False
     return np.array_equal(a.view(np.uint32)[~na], b.view(np.uint32)[~nb])
+
+
+def tiled_levels(B, H, W, L, device, fill=None, NQ=None):
+    """Separate tiled level tensors [B*NQ, map_floats(H_l, W_l)] (the library's value pyramid,
+    include/corr_mi355x.h), optionally filled with `fill`."""
+    import torch
+    from eraft_amd.corr import map_floats
+    BN = B * (H * W if NQ is None else NQ)
+    out = []
+    for l in range(L):
+        t = torch.empty(BN, map_floats(H >> l, W >> l), dtype=torch.float32, device=device)
+        if fill is not None:
+            t.fill_(fill)
+        out.append(t)
+    return out
+
+
+def export_levels(levels, H, W):
+    """The tiled levels in the reference's layout, as numpy [BN, 1, H_l, W_l] arrays."""
+    from eraft_amd import _lib
+    return [p.cpu().numpy() for p in _lib.pyramid_export(levels, H, W)]
+
+
+def build_level0(t1, t2, algo, ws=None):
+    """Level 0 of one build (corr_build_ex), row-major numpy [B*N, H*W]."""
+    from eraft_amd import _lib
+    B, _, H, W = t2.shape
+    lv = tiled_levels(B, H, W, 1, t1.device, NQ=t1.shape[2] * t1.shape[3])
+    _lib.build(t1, t2, lv, algo, ws)
+    return export_levels(lv, H, W)[0].reshape(-1, H * W)

@@ -35,7 +35,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 
 def test_version_and_workspace(lib):
-    assert lib.corr_version() == 104
+    assert lib.corr_version() == 200
     # DSEC: 256 x 4800 slabs; at least one slab, deterministic plan
     ws = lib.corr_build_bwd_workspace(1, 256, 60, 80)
     assert ws >= 256 * 4800 * 4 and ws % (256 * 4800 * 4) == 0
@@ -184,3 +184,27 @@ def test_lookup_conv_bwd_validation(lib):
     assert rc == -1 and "workspace" in lib.corr_last_error().decode()
     rc = lib.corr_lookup_conv_bwd(pyr, 16, 8, 36, 48, 4, 4, 16, 16, 1, 16, None, None, None, None, 0, None)
     assert rc == 0
+
+
+def test_tiled_map_size_and_layout_validation(lib):
+    """The value pyramid is tiled (include/corr_mi355x.h): ceil(H_l/4) * ceil(W_l/4) 4x4 tiles
+    per query map, the Python allocator agrees, and level pointers that are not 16-B aligned are
+    refused by the build, the lookup and the export / import before any HIP call."""
+    from eraft_amd.corr import map_floats
+    for h, w in ((60, 80), (7, 10), (15, 20), (1, 2), (17, 23), (160, 240), (4, 5)):
+        assert lib.corr_map_floats(h, w) == map_floats(h, w) == ((h + 3) // 4) * ((w + 3) // 4) * 16
+    assert lib.corr_map_floats(0, 5) == 0
+    bad = (ctypes.c_void_p * 4)(256, 264, 256, 256)  # level 1 only 8-B aligned
+    rc = lib.corr_build(256, 256, 1, 32, 60, 80, 4, bad, None)
+    assert rc == -1 and "16-byte aligned" in lib.corr_last_error().decode()
+    rc = lib.corr_lookup(bad, 256, 1, 60, 80, 4, 4, 256, None)
+    assert rc == -1 and "16-byte aligned" in lib.corr_last_error().decode()
+    ok = (ctypes.c_void_p * 4)(256, 256, 256, 256)
+    rc = lib.corr_pyramid_export(bad, 4800, 60, 80, 4, ok, None)
+    assert rc == -1 and "16-byte aligned" in lib.corr_last_error().decode()
+    rc = lib.corr_pyramid_import(ok, 4800, 60, 80, 4, bad, None)
+    assert rc == -1 and "16-byte aligned" in lib.corr_last_error().decode()
+    rc = lib.corr_pyramid_export(ok, 0, 60, 80, 4, ok, None)
+    assert rc == -1 and "BN" in lib.corr_last_error().decode()
+    rc = lib.corr_pyramid_import(ok, 4800, 4, 80, 4, ok, None)
+    assert rc == -1 and "too small" in lib.corr_last_error().decode()

@@ -114,7 +114,7 @@ def test_config4_train_b8_d256_forward_backward():
 
 
 def test_config5_1920x1280_rows_lookup_and_shards():
-    from eraft_amd import CorrBlock
+    from eraft_amd import CorrBlock, _lib
     from eraft_amd.sharded import HipRows, row_partition
     B, D, H, W, L, r = 1, 256, 160, 240, 4, 4
     N = H * W
@@ -135,7 +135,7 @@ def test_config5_1920x1280_rows_lookup_and_shards():
         lv = HipRows.build(t1[:, :, h0:h1].contiguous(), t2, L)
         mine = [int(q) for q in sel if h0 * W <= q < h1 * W]
         if mine:
-            loc = _rows(lv, [q - h0 * W for q in mine])
+            loc = _rows(_lib.pyramid_export(lv, H, W), [q - h0 * W for q in mine])
             full = _rows(cb.corr_pyramid, mine)
             for l in range(L):
                 assert bit_equal(loc[l], full[l]), (g, l)

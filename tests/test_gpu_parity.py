@@ -9,7 +9,7 @@ import pytest
 import torch
 
 import prng
-from _util import REL_TOL, bit_equal, golden_names, load, norm_rel
+from _util import REL_TOL, bit_equal, build_level0, export_levels, golden_names, load, norm_rel, tiled_levels
 from oracle import oracle
 
 pytestmark = pytest.mark.gpu
@@ -103,17 +103,17 @@ def test_split_build_phases_compose(shape, algo):
     t1 = torch.from_numpy(prng.gauss(21, (B, D, H, W))).to(DEV)
     t2 = torch.from_numpy(prng.gauss(22, (B, D, H, W))).to(DEV)
     L = min(4, int(np.log2(min(H, W))) + 1)
-    shapes = [(B * H * W, 1, H >> l, W >> l) for l in range(L)]
-    full = [torch.empty(s, device=DEV) for s in shapes]
-    split = [torch.full(s, float("nan"), device=DEV) for s in shapes]
+    full = tiled_levels(B, H, W, L, DEV)
+    split = tiled_levels(B, H, W, L, DEV, fill=float("nan"))
     ws = _lib.build_workspace(t1, t2, A)
     _lib.build(t1, t2, full, A, ws)
     ws.zero_()
     _lib.build(t1, t2, split, A | _lib.BUILD_ONLY_PACK, ws)
     _lib.build(t1, t2, split, A | _lib.BUILD_ONLY_MFMA, ws)
     torch.cuda.synchronize()
+    ef, es = export_levels(full, H, W), export_levels(split, H, W)
     for l in range(L):
-        assert bit_equal(full[l].cpu().numpy(), split[l].cpu().numpy()), l
+        assert bit_equal(ef[l], es[l]), l
 
 
 @pytest.mark.parametrize("shape,regions", [
@@ -133,17 +133,17 @@ def test_build_region_matches_full(shape, regions):
     t1 = torch.from_numpy(prng.gauss(61, (B, D, H, W))).to(DEV)
     t2 = torch.from_numpy(prng.gauss(62, (B, D, H, W))).to(DEV)
     L = min(4, int(np.log2(min(H, W))) + 1)
-    shapes = [(B * H * W, 1, H >> l, W >> l) for l in range(L)]
-    full = [torch.empty(s, device=DEV) for s in shapes]
-    reg = [torch.full(s, float("nan"), device=DEV) for s in shapes]
+    full = tiled_levels(B, H, W, L, DEV)
+    reg = tiled_levels(B, H, W, L, DEV, fill=float("nan"))
     _lib.build(t1, t2, full, _lib.BUILD_BF16X6)
     ws = _lib.build_workspace(t1, t2, _lib.BUILD_BF16X6)
     ws.fill_(0x5A)
     for k, (y0, y1) in enumerate(regions):
         _lib.build_region(t1, t2[:, :, y0:y1].contiguous(), y0, y1, H, reg, ws, k == 0)
     torch.cuda.synchronize()
+    ef, er = export_levels(full, H, W), export_levels(reg, H, W)
     for l in range(L):
-        assert bit_equal(full[l].cpu().numpy(), reg[l].cpu().numpy()), l
+        assert bit_equal(ef[l], er[l]), l
 
 
 @pytest.mark.parametrize("name", BUILD_CASES)
@@ -152,9 +152,9 @@ def test_lookup_bitexact_on_reference_pyramid(name):
     L, r = int(g["meta"][5]), int(g["meta"][6])
     _, _, t1, t2 = _fmaps(g["meta"])
     cb = _cb()(t1, t2, num_levels=L, radius=r)
-    # feed the kernel the reference's own pyramid: output must match bit for bit
-    for l in range(L):
-        cb.corr_pyramid[l].copy_(torch.from_numpy(g[f"pyr{l}"]))
+    # feed the kernel the reference's own pyramid (installed through corr_pyramid_import): output
+    # must match bit for bit
+    cb.corr_pyramid = [torch.from_numpy(g[f"pyr{l}"]).to(DEV) for l in range(L)]
     keys = [k[len("coords"):] for k in g if k.startswith("coords")]
     for k in keys:
         out = cb(torch.from_numpy(g["coords" + k]).to(DEV)).cpu().numpy()
@@ -269,9 +269,7 @@ def test_build_f16x3_dynamic_range(case):
     ref = oracle.corr_rows(f1, f2).reshape(B * H * W, H * W)
     outs = {}
     for algo in (_lib.BUILD_F16X3, _lib.BUILD_FP32):
-        lvl = torch.empty(B * H * W, 1, H, W, device=DEV)
-        _lib.build(t1, t2, [lvl], algo)
-        outs[algo] = lvl.cpu().numpy().reshape(B * H * W, H * W)
+        outs[algo] = build_level0(t1, t2, algo)
     for algo, o in outs.items():
         assert np.isfinite(o).all() == np.isfinite(ref).all()
         scale = np.abs(ref).max(axis=1)
@@ -332,9 +330,7 @@ def test_build_bf16x6_error_bound(case):
     B, D, H, W = f1.shape
     S = (D + 31) // 32
     t1, t2 = torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV)
-    lvl = torch.empty(B * H * W, 1, H, W, device=DEV)
-    _lib.build(t1, t2, [lvl], _lib.BUILD_BF16X6)
-    o = lvl.cpu().numpy().reshape(B * H * W, H * W)[rows].astype(np.float64)
+    o = build_level0(t1, t2, _lib.BUILD_BF16X6)[rows].astype(np.float64)
     ref = _fp64_rows(f1, f2, rows)
     a = np.abs(f1[0].reshape(D, H * W).astype(np.float64)[:, rows])
     b = np.abs(f2[0].reshape(D, H * W).astype(np.float64))
@@ -364,9 +360,7 @@ def test_build_bf16x6_not_narrower_than_fp32(case):
     ref = _fp64_rows(f1, f2, rows)
     err = {}
     for algo in (_lib.BUILD_BF16X6, _lib.BUILD_FP32):
-        lvl = torch.empty(B * H * W, 1, H, W, device=DEV)
-        _lib.build(t1, t2, [lvl], algo)
-        o = lvl.cpu().numpy().reshape(B * H * W, H * W)[rows].astype(np.float64)
+        o = build_level0(t1, t2, algo)[rows].astype(np.float64)
         assert np.isfinite(o).all()
         err[algo] = np.abs(o - ref).max(axis=1)
     scale = np.abs(ref).max(axis=1)
@@ -465,8 +459,8 @@ def test_bf16x6_pack_is_exact_split():
     t1, t2 = torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV)
     ws = _lib.build_workspace(t1, t2, _lib.BUILD_BF16X6)
     ws.fill_(0xAB)
-    lvl = torch.empty(B * H * W, 1, H, W, device=DEV)
-    _lib.build(t1, t2, [lvl], _lib.BUILD_BF16X6 | _lib.BUILD_ONLY_PACK, ws)
+    lvl = tiled_levels(B, H, W, 1, DEV)
+    _lib.build(t1, t2, lvl, _lib.BUILD_BF16X6 | _lib.BUILD_ONLY_PACK, ws)
     w = ws.cpu().numpy()
     N, S = H * W, (D + 31) // 32
     NQp = (N + 127) // 128 * 128
@@ -517,7 +511,7 @@ def test_lookup_bwd_bitexact_vs_oracle(B, D, H, W, L, r, kind):
     cold-start first iteration; tap floors jitter -> general range gather), and a few
     coordinates near 2^20 (taps outside the neighbourhood -> sequential scatter path)."""
     from eraft_amd import _lib
-    from eraft_amd.corr import _alloc_pyramid
+    from eraft_amd.corr import _alloc_grad_pyramid
     K = (2 * r + 1) ** 2
     c = prng.lookup_coords(5, B, H, W, 3.0)
     if kind == "grid":
@@ -532,7 +526,7 @@ def test_lookup_bwd_bitexact_vs_oracle(B, D, H, W, L, r, kind):
     ref = oracle.lookup_bwd(c, go, [np.zeros((B * H * W, 1, h, w), np.float32)
                                     for h, w in oracle.level_shapes(H, W, L)], r)
     like = torch.empty(1, device=DEV)
-    gl = _alloc_pyramid(B, H, W, L, like, zero=True)
+    gl = _alloc_grad_pyramid(B, H, W, L, like, zero=True)
     _lib.lookup_bwd(torch.from_numpy(c).to(DEV), torch.from_numpy(go).to(DEV), r, gl)
     for l in range(L):
         assert bit_equal(gl[l].cpu().numpy(), ref[l]), l
@@ -565,13 +559,13 @@ def test_lookup_bwd_multi_and_fold_bitexact(T, B, H, W, L, r):
     """corr_lookup_bwd_multi (all lookups in one launch, chunks of 32, overwriting the pyramid)
     == zero + corr_lookup_bwd per lookup, bit for bit; corr_pool_fold's level 0 == corr_pool_bwd's."""
     from eraft_amd import _lib
-    from eraft_amd.corr import _alloc_pyramid
+    from eraft_amd.corr import _alloc_grad_pyramid
     like = torch.empty(1, device=DEV)
     cs, gs = _bwd_case(T, B, H, W, L, r, 700)
-    ref = _alloc_pyramid(B, H, W, L, like, zero=True)
+    ref = _alloc_grad_pyramid(B, H, W, L, like, zero=True)
     for c, g in zip(cs, gs):
         _lib.lookup_bwd(c, g, r, ref)
-    got = _alloc_pyramid(B, H, W, L, like)
+    got = _alloc_grad_pyramid(B, H, W, L, like)
     for p in got:
         p.fill_(float("nan"))  # the multi-lookup kernel must overwrite every cell
     if T:
@@ -596,16 +590,16 @@ def test_corr_backward_matches_staged_path(algo, B, D, H, W, L, r, T):
     8 (18x24, 36x48), 4 (60x80), 1 (120x160) queries, and the multi-lookup + fold fallback
     (33 lookups > one launch's table; 5 levels)."""
     from eraft_amd import _lib
-    from eraft_amd.corr import _alloc_pyramid
+    from eraft_amd.corr import _alloc_grad_pyramid
     f1 = torch.from_numpy(prng.gauss(61, (B, D, H, W))).to(DEV)
     f2 = torch.from_numpy(prng.gauss(62, (B, D, H, W))).to(DEV)
     cs, gs = _bwd_case(T, B, H, W, L, r, 800)
-    ref = _alloc_pyramid(B, H, W, L, f1, zero=True)
+    ref = _alloc_grad_pyramid(B, H, W, L, f1, zero=True)
     for c, g in zip(cs, gs):
         _lib.lookup_bwd(c, g, r, ref)
     _lib.pool_bwd(ref, H, W)
     r1, r2 = _lib.build_bwd(ref[0].reshape(B * H * W, H * W), f1, f2, _lib._ALGOS[algo])
-    got = _alloc_pyramid(B, H, W, L, f1)
+    got = _alloc_grad_pyramid(B, H, W, L, f1)
     g1, g2 = _lib.backward(cs, gs, r, got, f1, f2, _lib._ALGOS[algo])
     assert bit_equal(got[0].cpu().numpy(), ref[0].cpu().numpy())
     assert bit_equal(g1.cpu().numpy(), r1.cpu().numpy())

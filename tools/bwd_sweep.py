@@ -8,7 +8,7 @@ import torch
 
 sys.path.insert(0, "e-raft_amd")
 from eraft_amd import _lib  # noqa: E402
-from eraft_amd.corr import _alloc_pyramid  # noqa: E402
+from eraft_amd.corr import _alloc_grad_pyramid  # noqa: E402
 
 B, D, H, W, L, r = 8, 256, 36, 48, 4, 4
 K = (2 * r + 1) ** 2
@@ -24,7 +24,7 @@ algo = _lib._ALGOS[sys.argv[2]] if len(sys.argv) > 2 else None
 coords = [(base + (0 if kind == "int" else 2.0 * torch.randn(B, 2, H, W, device=dev, generator=g))).contiguous()
           for _ in range(12)]
 gouts = [torch.randn(B, L * K, H, W, device=dev, generator=g) for _ in range(12)]
-gpyr = _alloc_pyramid(B, H, W, L, f1)
+gpyr = _alloc_grad_pyramid(B, H, W, L, f1)
 for T in (1, 2, 4, 12):
     for _ in range(5):
         _lib.backward(coords[:T], gouts[:T], r, gpyr, f1, f2, algo)

@@ -87,8 +87,8 @@ int main(int argc, char **argv) {
         size_t off[4], cnt[4], tot = 0;
         for (int l = 0; l < 4; ++l) {
             off[l] = tot;
-            cnt[l] = BN * (sh.H >> l) * (sh.W >> l);
-            tot += (cnt[l] + 3) / 4 * 4;
+            cnt[l] = BN * map_floats(sh.H >> l, sh.W >> l);  // the tiled pyramid (corr_common.h)
+            tot += cnt[l];
         }
         const size_t fe = (size_t)sh.B * sh.D * N;
         float *f1, *f2, *ref, *out;
@@ -258,14 +258,18 @@ int main(int argc, char **argv) {
             CK(hipMemcpy(h.data(), out, tot * 4, hipMemcpyDeviceToHost));
             size_t bad = 0;
             for (int l = 1; l < 4; ++l) {
-                const int Hp = sh.H >> (l - 1), Wp = sh.W >> (l - 1), Hl = sh.H >> l, Wl = sh.W >> l;
+                const int Wp = sh.W >> (l - 1), Hl = sh.H >> l, Wl = sh.W >> l;
+                const int TP = map_tiles(Wp), TL = map_tiles(Wl);
+                const size_t MP = map_floats(sh.H >> (l - 1), Wp), ML = map_floats(Hl, Wl);
                 const float *P = h.data() + off[l - 1], *C = h.data() + off[l];
                 for (size_t q = 0; q < BN; ++q)
                     for (int y = 0; y < Hl; ++y)
                         for (int x = 0; x < Wl; ++x) {
-                            const float *a = P + q * Hp * Wp + (2 * y) * Wp + 2 * x;
-                            const float e = pool_host(a[0], a[1], a[Wp], a[Wp + 1]);
-                            const float g = C[q * Hl * Wl + y * Wl + x];
+                            const float *a = P + q * MP;
+                            const float e = pool_host(a[map_cell(2 * y, 2 * x, TP)], a[map_cell(2 * y, 2 * x + 1, TP)],
+                                                      a[map_cell(2 * y + 1, 2 * x, TP)],
+                                                      a[map_cell(2 * y + 1, 2 * x + 1, TP)]);
+                            const float g = C[q * ML + map_cell(y, x, TL)];
                             if (std::memcmp(&e, &g, 4)) ++bad;
                         }
             }

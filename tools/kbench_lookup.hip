@@ -94,7 +94,7 @@ int main(int argc, char **argv) {
         size_t off[4], tot = 0;
         for (int l = 0; l < 4; ++l) {
             off[l] = tot;
-            tot += (BN * (sh.H >> l) * (sh.W >> l) + 3) / 4 * 4;
+            tot += BN * map_floats(sh.H >> l, sh.W >> l);  // the tiled pyramid (corr_common.h)
         }
         float *pyr, *coords, *ref, *out;
         const size_t n_out = (size_t)sh.B * 324 * N;
@@ -122,8 +122,6 @@ int main(int argc, char **argv) {
         vs.push_back({"abl QB32 noload", [=](float *o) { return launch_qb<32, 1>(lp, coords, B, H, W, o); }, {}});
         vs.push_back({"QB16 cached-stores", [=](float *o) { return launch_qb<16, 8>(lp, coords, B, H, W, o); }, {}});
         vs.push_back({"QB32 cached-stores", [=](float *o) { return launch_qb<32, 8>(lp, coords, B, H, W, o); }, {}});
-        vs.push_back({"QB16 nt-loads", [=](float *o) { return launch_qb<16, 16>(lp, coords, B, H, W, o); }, {}});
-        vs.push_back({"QB32 nt-loads", [=](float *o) { return launch_qb<32, 16>(lp, coords, B, H, W, o); }, {}});
         CK(vs[0].launch(ref));
         for (auto &v : vs) {
             CK(hipMemset(out, 0, n_out * 4));
