@@ -76,7 +76,7 @@ __device__ __forceinline__ void store_pyramid(const BuildParams &p, f32x16 (&acc
                                               const int l32) {
     const int NQ = p.NQ, W = p.W, H = p.H;
     const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
-    const int TW0 = map_tiles(W), TW1 = map_tiles(W1), TW2 = map_tiles(W2), TW3 = map_tiles(W3);
+    const int TW0 = map_tcols(W), TW1 = map_tcols(W1), TW2 = map_tcols(W2), TW3 = map_tcols(W3);
     const int R0 = 4 * map_tiles(H), R1 = 4 * map_tiles(H1), R2 = 4 * map_tiles(H2), R3 = 4 * map_tiles(H3);
     const size_t M0 = map_floats(H, W), M1 = map_floats(H1, W1), M2 = map_floats(H2, W2), M3 = map_floats(H3, W3);
     const int X0 = xw + 4 * h, Y0 = py * 8;
@@ -145,7 +145,7 @@ __device__ __forceinline__ void store_pyramid(const BuildParams &p, f32x16 (&acc
         const float o1 = __shfl_xor(l2[1], 32);
         {  // h = 0 writes row 0 (x = 0, 1), h = 1 row 1; xw / 4 is even, so the pair is 8-B aligned
             const int Y = py * 2 + h, X2 = xw >> 2;
-            if (qok && X2 < 4 * TW2 && Y < R2)
+            if (qok && X2 < kTileW * TW2 && Y < R2)
                 *reinterpret_cast<float2 *>(p.lvl[2] + qrow * M2 + map_cell(Y, X2, TW2)) =
                     h ? make_float2(o1, l2[1]) : make_float2(l2[0], o0);
         }
@@ -154,7 +154,7 @@ __device__ __forceinline__ void store_pyramid(const BuildParams &p, f32x16 (&acc
         if (h == 0 && qok) {
             const float l3 = pool4(l2[0], o0, l2[1], o1);
             const int Y = py, X = X0 >> 3;
-            if (Y < R3 && X < 4 * TW3) p.lvl[3][qrow * M3 + map_cell(Y, X, TW3)] = l3;
+            if (Y < R3 && X < kTileW * TW3) p.lvl[3][qrow * M3 + map_cell(Y, X, TW3)] = l3;
         }
     }
 }
@@ -323,16 +323,16 @@ __global__ __launch_bounds__(256) void pool2x2_kernel(const float *__restrict__ 
                                                       float *__restrict__ out, long BN, int H,
                                                       int W) {
     const int Ho = H >> 1, Wo = W >> 1;
-    const int TWi = map_tiles(W), TWo = map_tiles(Wo);
+    const int TWi = map_tcols(W), TWo = map_tcols(Wo);
     const size_t Mi = map_floats(H, W), Mo = map_floats(Ho, Wo);
     const size_t total = (size_t)BN * Mo;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (size_t)gridDim.x * blockDim.x) {
         const size_t q = i / Mo;
         const int rem = (int)(i - q * Mo);
-        const int t = rem >> 4, c = rem & 15;
+        const int t = rem / (4 * kTileW), c = rem % (4 * kTileW);
         const int ty = t / TWo, tx = t - ty * TWo;
-        const int y = 4 * ty + (c >> 2), x = 4 * tx + (c & 3);
+        const int y = 4 * ty + c / kTileW, x = kTileW * tx + c % kTileW;
         if (y >= Ho || x >= Wo) continue;  // padding of level l: never read
         const float *I = in + q * Mi;
         out[i] = pool4(I[map_cell(2 * y, 2 * x, TWi)], I[map_cell(2 * y, 2 * x + 1, TWi)],

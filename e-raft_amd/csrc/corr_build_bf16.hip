@@ -22,7 +22,7 @@
 // 4 consecutive pixels of one query's map: level 0 leaves as 16-B row stores, the 2x2 / 4x4
 // windows of levels 1-2 sit inside one lane, level 3 pairs lanes 16 apart.
 //
-// Workgroup = 4 waves x 32 queries against one 8 x 16 target patch.  The patch's records
+// Workgroup = 4 waves x 32 queries against one 8 x 16 target patch (2 x 4 tiles).  The patch's records
 // (24 KiB per 32-deep K step) stream into a 3-slot LDS ring by LDS-DMA two steps ahead; each
 // wave loads its own queries' records into registers, also two steps ahead.  One barrier per K
 // step.  Two workgroups per CU (72 KiB LDS each).
@@ -33,8 +33,12 @@
 //   bytes [2048, 3072)   lo:  the same positions
 // i.e. exactly the MFMA fragment images of that block: the LDS fill and every fragment read are
 // contiguous 1 KiB (conflict-free ds_read_b128, coalesced loads).
-//   pq [B][S][NQB][3 KiB]     queries: block = 16 consecutive query pixels, NQp = NQB*16
-//   pt [B][S][Hp][CB][3 KiB]  targets: block = (row y, columns 16 cb .. 16 cb + 15)
+//   pq [B][S][NQB][3 KiB]          queries: block = 16 consecutive query pixels, NQp = NQB*16
+//   pt [B][S][Hp/4][4 CB][3 KiB]   targets: block = the 4x4 tile (rows 4 ty .., columns 4 tx ..),
+//                                  pixel ci at (ci / 4, ci % 4) — the pyramid's tile
+//                                  (corr_common.h), so each 16x16 output block of an MFMA is one
+//                                  tile: lane (grp, ci) holds its row grp for query ci, and the
+//                                  four lanes of a query store a whole 64-B tile per instruction
 // Padding pixels and k >= D are zero.
 #include <algorithm>
 #include <atomic>
@@ -110,10 +114,13 @@ __global__ __launch_bounds__(256) void bf16_pack_kernel(PackArgs a) {
         valid = n < a.np[0];
         iblk = blk;
     } else {
-        const int ly = blk / a.CB, x = (blk - ly * a.CB) * 16 + ci;
+        // target block = a 4x4 tile of the map (tile row ty, column tx; 4 CB tiles per row), pixel
+        // ci at (ci / 4, ci % 4): the MFMA's output rows then hold whole tile rows of the pyramid
+        const int TCp = 4 * a.CB, ty = blk / TCp, tx = blk - ty * TCp;
+        const int ly = 4 * ty + (ci >> 2), x = 4 * tx + (ci & 3);
         valid = a.y0 + ly < a.y1 && x < a.W;
         n = ly * a.W + x;
-        iblk = a.y0 * a.CB + blk;
+        iblk = (a.y0 >> 2) * TCp + blk;
     }
     const int NP = a.np[z], k0 = s * kStepK + 8 * grp;
     const float *src = a.f[z] + (size_t)b * a.D * NP + (valid ? n : 0);
@@ -217,15 +224,17 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
     const int S = SS > 0 ? SS : p.S;
     const bool qact = qb0 * 16 < p.NQ;  // wave-uniform
 
-    // LDS-DMA pieces of this wave: pc = w + 4 m (m < 6) -> patch row pc / 3, piece pc % 3, landing
-    // at slot offset pc KiB (row r's pieces at 3 r .. 3 r + 2).
+    // LDS-DMA pieces of this wave: pc = w + 4 m (m < 6) -> patch record rp = pc / 3 (tile row rp / 4,
+    // tile column rp % 4 of the patch), piece pc % 3, landing at slot offset pc KiB (record rp's
+    // pieces at 3 rp .. 3 rp + 2).
+    const int TCp = 4 * p.CB;                          // tiles per row of the target image
     const size_t tstep = (size_t)p.Hp * p.CB * kRecU;  // u32x4 per K step of the target image
-    const u32x4_t *tbase = p.pt + (((size_t)b * S * p.Hp + y0) * p.CB + tl.cb) * kRecU + lane;
+    const u32x4_t *tbase = p.pt + (((size_t)b * S * (p.Hp >> 2) + (y0 >> 2)) * TCp + 4 * tl.cb) * kRecU + lane;
     unsigned toff[kDmaPerWave];
 #pragma unroll
     for (int m = 0; m < kDmaPerWave; ++m) {
-        const int pc = w + 4 * m;
-        toff[m] = (unsigned)((pc / kPieces) * p.CB * kRecU + (pc % kPieces) * 64);
+        const int pc = w + 4 * m, rp = pc / kPieces;
+        toff[m] = (unsigned)(((rp >> 2) * TCp + (rp & 3)) * kRecU + (pc % kPieces) * 64);
     }
     const size_t qstep = (size_t)p.NQB * kRecU;
     const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_void_t *)smem;
@@ -390,85 +399,98 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
     }
 
     // ---- epilogue: 1/sqrt(D), level 0 from registers, levels 1-3 in registers ----
-    // Every level leaves as 16-B tile rows of the tiled pyramid (corr_common.h) except level 3 (one
-    // cell per lane); a store runs whenever its tile row lies in the padded map (cells past W_l /
-    // H_l are padding: the zero-padded target records make them finite, nothing reads them).
+    // MFMA block rp (patch tile (rp / 4, rp % 4)) leaves lane (grp, ci) with row grp of that tile
+    // for query ci.  Writing lane grp = 2 h + k:
+    //   level 0: one 16-B tile row per block; the four lanes of a query fill one 64-B tile per
+    //            store instruction (the pyramid's tile, corr_common.h);
+    //   level 1: row Y = 2 tr + h of the patch's level 1 comes from tile rows 2h, 2h + 1 — lanes
+    //            (h, 0) and (h, 1), 16 apart: each takes level-1 tile k (columns 4k .. 4k + 3) and
+    //            trades the other tile pair's row with its partner; one 16-B store per tr;
+    //   level 2: row Y2 = h from level-1 rows 2h, 2h + 1 — lanes (0, k), (1, k), 32 apart; the
+    //            lanes (h, 0), (h, 1) then meet for the 16-B row, one store per lane over the two
+    //            query blocks; level 3 as level 2 with the pair 32 apart, one cell per lane.
+    // Every pool is ((a + b) + c) + d in avg_pool2d's order (bit-identical).  A store runs whenever
+    // its tile row lies in the padded map (cells past W_l / H_l are padding: the zero-padded target
+    // records make them finite, nothing reads them).
     const int H = p.H, W = p.W, NQ = p.NQ, nlev = FAST ? 4 : p.nlev;
     const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
-    const int TW0 = map_tiles(W), TW1 = map_tiles(W1), TW2 = map_tiles(W2), TW3 = map_tiles(W3);
+    const int TC0 = map_tcols(W), TC1 = map_tcols(W1), TC2 = map_tcols(W2), TC3 = map_tcols(W3);
     const int R0 = 4 * map_tiles(H), R1 = 4 * map_tiles(H1), R2 = 4 * map_tiles(H2), R3 = 4 * map_tiles(H3);
     const size_t M0 = map_floats(H, W), M1 = map_floats(H1, W1), M2 = map_floats(H2, W2), M3 = map_floats(H3, W3);
-    const int X0 = x0 + 4 * grp;
-    float l2s[2][2];  // both blocks' level-2 values: their stores are merged below
+    const int h = grp >> 1, k = grp & 1;
+    float l2s[2][2];  // level 2 of both query blocks: (Y2 = h, X2 = 2k + j)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int q = (qb0 + i) * 16 + ci;
         const bool qok = q < NQ;
         const size_t qrow = (size_t)b * NQ + q;
-        float v[kPatchRows][4];
+        float v[kPatchRows][4];  // v[rp][c]: patch cell (4 (rp >> 2) + grp, 4 (rp & 3) + c)
 #pragma unroll
         for (int r = 0; r < kPatchRows; ++r)
 #pragma unroll
             for (int g = 0; g < 4; ++g) v[r][g] = (ACC2 ? acc[i][r][g] + acs[i][r][g] : acc[i][r][g]) * p.inv_s;
-        if (qok && nlev > 0 && X0 < W) {
+        if (qok && nlev > 0) {
             float *m0 = p.lvl[0] + qrow * M0;
 #pragma unroll
-            for (int r = 0; r < kPatchRows; ++r)
-                if (y0 + r < R0)
-                    *reinterpret_cast<float4 *>(m0 + map_row4(y0 + r, X0 >> 2, TW0)) = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
-        }
-        float l1[4][2];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            l1[r][0] = pool4(v[2 * r][0], v[2 * r][1], v[2 * r + 1][0], v[2 * r + 1][1]);
-            l1[r][1] = pool4(v[2 * r][2], v[2 * r][3], v[2 * r + 1][2], v[2 * r + 1][3]);
-        }
-        float l2[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) l2[r] = pool4(l1[2 * r][0], l1[2 * r][1], l1[2 * r + 1][0], l1[2 * r + 1][1]);
-        l2s[i][0] = l2[0], l2s[i][1] = l2[1];
-        {
-            // Level 1 as 16-B tile rows: lanes grp 2m and 2m + 1 hold level-1 columns x0/2 + 4m + {0,1}
-            // and {2,3} of the patch's 4 rows; they swap one row's pair (lanes 16 apart) so that the
-            // even lane stores rows 0, 2 and the odd lane rows 1, 3, 4 columns each.
-            const bool odd = grp & 1;
-            const int X1 = (x0 >> 1) + 4 * (grp >> 1);
-#pragma unroll
-            for (int rp = 0; rp < 2; ++rp) {
-                const int ra = 2 * rp, rb = ra + 1, r = odd ? rb : ra;
-                const float g0 = __shfl_xor(odd ? l1[ra][0] : l1[rb][0], 16);
-                const float g1 = __shfl_xor(odd ? l1[ra][1] : l1[rb][1], 16);
-                const float4 o = odd ? make_float4(g0, g1, l1[rb][0], l1[rb][1]) : make_float4(l1[ra][0], l1[ra][1], g0, g1);
-                if (qok && nlev > 1 && (y0 >> 1) + r < R1 && X1 < W1)
-                    *reinterpret_cast<float4 *>(p.lvl[1] + qrow * M1 + map_row4((y0 >> 1) + r, X1 >> 2, TW1)) = o;
+            for (int rp = 0; rp < kPatchRows; ++rp) {
+                const int Y = y0 + 4 * (rp >> 2) + grp, T = (x0 >> 2) + (rp & 3);
+                if (Y < R0 && 4 * T < W)
+                    *reinterpret_cast<float4 *>(m0 + map_row4(Y, T, TC0)) = make_float4(v[rp][0], v[rp][1], v[rp][2], v[rp][3]);
             }
         }
+        float l1[2][4];  // l1[tr][m]: level-1 cell (2 tr + h, 4k + m) of the patch
+#pragma unroll
+        for (int tr = 0; tr < 2; ++tr) {
+            float top[2][4], bot[2][4];  // rows 2h, 2h + 1 of tiles 4 tr + 2k + j
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float mine = k ? v[4 * tr + 2 + j][c] : v[4 * tr + j][c];
+                    const float give = k ? v[4 * tr + j][c] : v[4 * tr + 2 + j][c];
+                    const float got = __shfl_xor(give, 16);
+                    top[j][c] = k ? got : mine;
+                    bot[j][c] = k ? mine : got;
+                }
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int j = m >> 1, c = 2 * (m & 1);
+                l1[tr][m] = pool4(top[j][c], top[j][c + 1], bot[j][c], bot[j][c + 1]);
+            }
+            const int Y1 = (y0 >> 1) + 2 * tr + h, T1 = (x0 >> 3) + k;
+            if (qok && nlev > 1 && Y1 < R1 && 4 * T1 < W1)
+                *reinterpret_cast<float4 *>(p.lvl[1] + qrow * M1 + map_row4(Y1, T1, TC1)) =
+                    make_float4(l1[tr][0], l1[tr][1], l1[tr][2], l1[tr][3]);
+        }
+        // level 2 (Y2 = h, X2 = 2k + j): level-1 rows 2h (lane (0, k), tr = h) and 2h + 1 (lane (1, k))
+        float top[4], bot[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const float give = h ? l1[0][m] : l1[1][m];
+            const float got = __shfl_xor(give, 32);
+            top[m] = h ? got : l1[0][m];
+            bot[m] = h ? l1[1][m] : got;
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) l2s[i][j] = pool4(top[2 * j], top[2 * j + 1], bot[2 * j], bot[2 * j + 1]);
     }
-    // Levels 2 and 3 of BOTH query blocks in one store instruction each (an xor exchange has one
-    // receiver per sender, so every sender sends what its receiver's block needs).
     {
-        // Level 2: lanes grp 0..3 hold columns x0/4 + grp of 2 rows per block; lane g gathers row
-        // g & 1 of block g >> 1 (exchanges with lanes 16, 32, 48 apart): one 16-B tile row per lane.
-        const int bl = grp >> 1, rw = grp & 1;
-        auto sel = [&](int k) { return k == 0 ? l2s[0][0] : k == 1 ? l2s[0][1] : k == 2 ? l2s[1][0] : l2s[1][1]; };
-        const float t0 = sel(grp);
-        const float t1 = __shfl_xor(sel(grp ^ 1), 16), t2 = __shfl_xor(sel(grp ^ 2), 32), t3 = __shfl_xor(sel(grp ^ 3), 48);
-        // t_d is column grp ^ d of the wanted row, so component c (column c) is t_(c ^ grp)
-        auto pick = [&](int k) { return k == 0 ? t0 : k == 1 ? t1 : k == 2 ? t2 : t3; };
-        const float4 o = make_float4(pick(grp), pick(grp ^ 1), pick(grp ^ 2), pick(grp ^ 3));
-        const int q = (qb0 + bl) * 16 + ci;
-        if (q < NQ && nlev > 2 && (y0 >> 2) + rw < R2 && (x0 >> 2) < W2)
-            *reinterpret_cast<float4 *>(p.lvl[2] + ((size_t)b * NQ + q) * M2 + map_row4((y0 >> 2) + rw, x0 >> 4, TW2)) = o;
+        // Level 2 rows of BOTH blocks, one 16-B store per lane: lane (h, k) stores row h of block k;
+        // lanes (h, 0), (h, 1) hold columns 0-1 / 2-3 and trade the other block's pair.
+        const float g0 = __shfl_xor(k ? l2s[0][0] : l2s[1][0], 16), g1 = __shfl_xor(k ? l2s[0][1] : l2s[1][1], 16);
+        const float o0 = k ? l2s[1][0] : l2s[0][0], o1 = k ? l2s[1][1] : l2s[0][1];
+        const float4 o = k ? make_float4(g0, g1, o0, o1) : make_float4(o0, o1, g0, g1);
+        const int q = (qb0 + k) * 16 + ci, Y2 = (y0 >> 2) + h;
+        if (q < NQ && nlev > 2 && Y2 < R2 && (x0 >> 2) < W2)
+            *reinterpret_cast<float4 *>(p.lvl[2] + ((size_t)b * NQ + q) * M2 + map_row4(Y2, x0 >> 4, TC2)) = o;
     }
     {
-        // Level 3: the 2x2 window of level-2 values (a row pair in one lane, the column pair in the
-        // lanes 16 apart); even lanes pool block 0, odd lanes block 1, in ((a + b) + c) + d order.
-        const int bl = grp & 1;
-        const float y0v = __shfl_xor(bl ? l2s[0][0] : l2s[1][0], 16), y1v = __shfl_xor(bl ? l2s[0][1] : l2s[1][1], 16);
-        const float l3 = bl == 0 ? pool4(l2s[0][0], y0v, l2s[0][1], y1v) : pool4(y0v, l2s[1][0], y1v, l2s[1][1]);
-        const int q = (qb0 + bl) * 16 + ci;
-        const int Y3 = y0 >> 3, X3 = X0 >> 3;
-        if (q < NQ && nlev > 3 && Y3 < R3 && X3 < 4 * TW3) p.lvl[3][((size_t)b * NQ + q) * M3 + map_cell(Y3, X3, TW3)] = l3;
+        // Level 3, cell X3 = k of block h: level-2 rows 0 (lanes (0, k)) and 1 (lanes (1, k)).
+        const float g0 = __shfl_xor(h ? l2s[0][0] : l2s[1][0], 32), g1 = __shfl_xor(h ? l2s[0][1] : l2s[1][1], 32);
+        const float l3 = h ? pool4(g0, g1, l2s[1][0], l2s[1][1]) : pool4(l2s[0][0], l2s[0][1], g0, g1);
+        const int q = (qb0 + h) * 16 + ci;
+        const int Y3 = y0 >> 3, X3 = (x0 >> 3) + k;
+        if (q < NQ && nlev > 3 && Y3 < R3 && X3 < kTileW * TC3) p.lvl[3][((size_t)b * NQ + q) * M3 + map_cell(Y3, X3, TC3)] = l3;
     }
 }
 

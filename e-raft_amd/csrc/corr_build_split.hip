@@ -358,7 +358,7 @@ __device__ __forceinline__ void build_tile(const BuildArgs &p, const Tile tl) {
     // store runs whenever its tile row lies in the padded map (corr_build_bf16.hip's epilogue).
     const int H = p.H, W = p.W, NQ = p.NQ, nlev = p.nlev;
     const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
-    const int TW0 = map_tiles(W), TW1 = map_tiles(W1), TW2 = map_tiles(W2), TW3 = map_tiles(W3);
+    const int TW0 = map_tcols(W), TW1 = map_tcols(W1), TW2 = map_tcols(W2), TW3 = map_tcols(W3);
     const int R0 = 4 * map_tiles(H), R1 = 4 * map_tiles(H1), R2 = 4 * map_tiles(H2), R3 = 4 * map_tiles(H3);
     const size_t M0 = map_floats(H, W), M1 = map_floats(H1, W1), M2 = map_floats(H2, W2), M3 = map_floats(H3, W3);
     const int X0 = x0 + 4 * grp;
@@ -436,7 +436,7 @@ __device__ __forceinline__ void build_tile(const BuildArgs &p, const Tile tl) {
         const float l3 = bl == 0 ? pool4(l2s[0][0], y0v, l2s[0][1], y1v) : pool4(y0v, l2s[1][0], y1v, l2s[1][1]);
         const int q = (qb0 + bl) * 16 + ci;
         const int Y3 = y0 >> 3, X3 = X0 >> 3;
-        if (q < NQ && nlev > 3 && Y3 < R3 && X3 < 4 * TW3) p.lvl[3][((size_t)b * NQ + q) * M3 + map_cell(Y3, X3, TW3)] = l3;
+        if (q < NQ && nlev > 3 && Y3 < R3 && X3 < kTileW * TW3) p.lvl[3][((size_t)b * NQ + q) * M3 + map_cell(Y3, X3, TW3)] = l3;
     }
 }
 

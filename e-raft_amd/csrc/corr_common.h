@@ -21,26 +21,28 @@ struct ConstLevelPtrs {
 
 // ---------------------------------------------------------------------------------------
 // Pyramid layout (the build's output, the lookups' input).  Every query's level-l map
-// (H_l x W_l cells, corr.py:21-27) is stored as 4x4-cell tiles of 64 B, tiles row-major over
-// the map, cells row-major inside a tile:
-//     cell (y, x) of a map at ((y >> 2) * TW + (x >> 2)) * 16 + (y & 3) * 4 + (x & 3),
-//     TW = ceil(W_l / 4), a map = ceil(H_l / 4) * TW * 16 floats (a multiple of 64 B).
+// (H_l x W_l cells, corr.py:21-27) is stored as tiles of 4 rows x kTileW cells, tiles row-major
+// over the map, cells row-major inside a tile:
+//     cell (y, x) at ((y >> 2) * TC + x / kTileW) * 4 kTileW + (y & 3) * kTileW + x % kTileW,
+//     TC = ceil(W_l / kTileW) tiles per map row, a map = ceil(H_l / 4) * TC * 4 kTileW floats.
 // A query's maps are contiguous (level by level, query after query), so a row slab of queries
 // is a contiguous range, as before.  The cells past W_l / H_l in the last tile column / row are
 // padding: the builds may write anything there and nothing reads them (the lookups zero
-// out-of-map cells themselves).  A (2r+2)^2 window then spans whole 64-B tiles (one 16-B tile
-// row per lane and window row in the gather), where row-major maps gave one 40-B segment per
-// window row in a different line (profiles/r05f_kbench_lookup_tiled.txt).  The reference
-// layout [B*N, 1, H_l, W_l] is materialised on demand (corr_pyramid_export).
-__host__ __device__ inline int map_tiles(int n) { return (n + 3) >> 2; }
-__host__ __device__ inline size_t map_floats(int Hl, int Wl) { return (size_t)map_tiles(Hl) * map_tiles(Wl) * 16; }
-__host__ __device__ inline unsigned map_cell(int y, int x, int TW) {
-    return (unsigned)((((y >> 2) * TW + (x >> 2)) << 4) + ((y & 3) << 2) + (x & 3));
+// out-of-map cells themselves).  A (2r+2)^2 window then spans a few whole tiles (one 16-B
+// tile-row chunk per lane and window row in the gather), where row-major maps gave one 40-B
+// segment per window row in a different line (profiles/r05f_kbench_lookup_tiled.txt).  The
+// reference layout [B*N, 1, H_l, W_l] is materialised on demand (corr_pyramid_export).
+constexpr int kTileW = 4;  // 64-B tiles (profiles/r05i_kbench_*_tw{4,8}.txt: 4 x 8 bands cost the lookups more)
+__host__ __device__ inline int map_tiles(int n) { return (n + 3) >> 2; }  // 4-cell groups (tile rows, 16-B chunks)
+__host__ __device__ inline int map_tcols(int Wl) { return (Wl + kTileW - 1) / kTileW; }
+__host__ __device__ inline size_t map_floats(int Hl, int Wl) {
+    return (size_t)map_tiles(Hl) * map_tcols(Wl) * 4 * kTileW;
 }
-// Offset of the 16-B tile row holding cells (y, 4t .. 4t + 3).
-__host__ __device__ inline unsigned map_row4(int y, int t, int TW) {
-    return (unsigned)((((y >> 2) * TW + t) << 4) + ((y & 3) << 2));
+__host__ __device__ inline unsigned map_cell(int y, int x, int TC) {
+    return (unsigned)((((y >> 2) * TC + x / kTileW) * 4 + (y & 3)) * kTileW + x % kTileW);
 }
+// Offset of the 16-B chunk holding cells (y, 4t .. 4t + 3).
+__host__ __device__ inline unsigned map_row4(int y, int t, int TC) { return map_cell(y, 4 * t, TC); }
 
 // Set the thread-local error and return `code`.
 int fail(int code, const char *fmt, ...);

@@ -124,7 +124,8 @@ __device__ __forceinline__ void gather_window_tiled(LookupSmem<S, QB> &sm, const
     constexpr int NW = NT / 64;
     constexpr int QPW = (QB + NW - 1) / NW;  // queries per wave
     static_assert(QPW <= 64, "one lane per query of the wave");
-    const unsigned TW = (unsigned)map_tiles(Wl);
+    const unsigned TW = (unsigned)map_tiles(Wl);  // 16-B chunks per map row
+    const int TC = map_tcols(Wl);                  // tiles per map row
     const int lane = tid & 63;
     int rr[EPL], tc[EPL];
 #pragma unroll
@@ -156,7 +157,7 @@ __device__ __forceinline__ void gather_window_tiled(LookupSmem<S, QB> &sm, const
         for (int v = 0; v < EPL; ++v) {
             const unsigned T = (unsigned)((X0 >> 2) + tc[v]), Y = (unsigned)(Y0 + rr[v]);
             const bool ok = (lane + 64 * v < LPQ) && T < TW && Y < (unsigned)Hl;
-            vals[k][v] = (ok && !NOLOAD) ? *reinterpret_cast<const f32x4 *>(Pq + map_row4((int)Y, (int)T, (int)TW))
+            vals[k][v] = (ok && !NOLOAD) ? *reinterpret_cast<const f32x4 *>(Pq + map_row4((int)Y, (int)T, TC))
                                          : f32x4{0.f, 0.f, 0.f, 0.f};
         }
     }
@@ -204,7 +205,7 @@ __device__ __forceinline__ void lookup_block_v(LookupSmem<S, QB> &sm, const floa
     const int Hl = H >> l, Wl = W >> l;
     const float inv_scale = 1.0f / (float)(1 << l);
     const unsigned mapsz = (unsigned)map_floats(Hl, Wl);
-    const int TW = map_tiles(Wl);
+    const int TC = map_tcols(Wl);
     const size_t qbase = (size_t)b * N + n0;
 
     const int q = tid % QB;
@@ -293,7 +294,7 @@ __device__ __forceinline__ void lookup_block_v(LookupSmem<S, QB> &sm, const floa
             const int xi = (int)xf, yi = (int)yf;
             const unsigned ux = (unsigned)(xi - ax), uy = (unsigned)(yi - ay);
             if (ux < (unsigned)WIN && uy < (unsigned)WIN) return wq[uy * WW + ux];
-            return Pq[map_cell(yi, xi, TW)];
+            return Pq[map_cell(yi, xi, TC)];
         };
         const float x1 = __fadd_rn(x0, 1.0f);
         for (int j = 0; j < S; ++j) {
@@ -1883,13 +1884,14 @@ namespace {
 template <bool EXPORT>
 __global__ __launch_bounds__(256) void pyramid_layout_kernel(const float *__restrict__ src, float *__restrict__ dst,
                                                              long BN, int Hl, int Wl) {
-    const int TW = map_tiles(Wl);
-    const long per = (long)map_floats(Hl, Wl) / 4;  // tile rows per map
+    const int TC = map_tcols(Wl);
+    const long per = (long)map_floats(Hl, Wl) / 4;  // 16-B chunks per map
     const long total = BN * per;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
         const long n = i / per;
         const int rem = (int)(i - n * per);
-        const int t = rem >> 2, Y = 4 * (t / TW) + (rem & 3), X = 4 * (t % TW);
+        const int t = rem / kTileW, cq = rem % kTileW;  // tile, chunk in the tile (kTileW / 4 per row)
+        const int Y = 4 * (t / TC) + cq / (kTileW / 4), X = kTileW * (t % TC) + 4 * (cq % (kTileW / 4));
         const size_t row = ((size_t)n * Hl + Y) * Wl;
         if (EXPORT) {
             if (Y >= Hl) continue;

@@ -33,9 +33,12 @@ def level_shapes(H: int, W: int, num_levels: int):
     return [(H >> l, W >> l) for l in range(num_levels)]
 
 
+TILE_W = 4  # cells per tile row (include/corr_mi355x.h): tiles of 4 rows x TILE_W cells
+
+
 def map_floats(Hl: int, Wl: int) -> int:
-    """Floats of one query's tiled level map (include/corr_mi355x.h: 4x4-cell tiles of 64 B)."""
-    return ((Hl + 3) // 4) * ((Wl + 3) // 4) * 16
+    """Floats of one query's tiled level map (include/corr_mi355x.h)."""
+    return ((Hl + 3) // 4) * ((Wl + TILE_W - 1) // TILE_W) * 4 * TILE_W
 
 
 def _alloc_pyramid(B: int, H: int, W: int, num_levels: int, like: torch.Tensor, zero=False, NQ=None):

@@ -470,8 +470,10 @@ def test_bf16x6_pack_is_exact_split():
     # record layout: [piece 3][grp 4][ci 16][j 8] bf16; k = 32 s + 8 grp + j
     q = w[:nq].view(np.uint16).reshape(B, S, NQp // 16, 3, 4, 16, 8)
     q = _bf16_to_f32(q).transpose(0, 3, 1, 4, 6, 2, 5).reshape(B, 3, S * 32, NQp)
-    t = w[toff:toff + B * S * Hp * CB * 16 * 192].view(np.uint16).reshape(B, S, Hp, CB, 3, 4, 16, 8)
-    t = _bf16_to_f32(t).transpose(0, 4, 1, 5, 7, 2, 3, 6).reshape(B, 3, S * 32, Hp, CB * 16)
+    # target records are 4x4 tiles (tile row ty, tile column tx of 4 CB per row), pixel ci at
+    # (4 ty + ci // 4, 4 tx + ci % 4)
+    t = w[toff:toff + B * S * Hp * CB * 16 * 192].view(np.uint16).reshape(B, S, Hp // 4, 4 * CB, 3, 4, 4, 4, 8)
+    t = _bf16_to_f32(t).transpose(0, 4, 1, 5, 8, 2, 6, 3, 7).reshape(B, 3, S * 32, Hp, CB * 16)
     for img, x in ((q[..., :N].reshape(B, 3, S * 32, H, W), f1), (t[..., :H, :W], f2)):
         hi, mid, lo = (img[:, c, :D] for c in range(3))
         fin = np.isfinite(x)

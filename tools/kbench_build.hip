@@ -259,7 +259,7 @@ int main(int argc, char **argv) {
             size_t bad = 0;
             for (int l = 1; l < 4; ++l) {
                 const int Wp = sh.W >> (l - 1), Hl = sh.H >> l, Wl = sh.W >> l;
-                const int TP = map_tiles(Wp), TL = map_tiles(Wl);
+                const int TP = map_tcols(Wp), TL = map_tcols(Wl);
                 const size_t MP = map_floats(sh.H >> (l - 1), Wp), ML = map_floats(Hl, Wl);
                 const float *P = h.data() + off[l - 1], *C = h.data() + off[l];
                 for (size_t q = 0; q < BN; ++q)
