@@ -132,11 +132,14 @@ def lookup_bytes(B, H, W, L, r):
     return B * N * (L * (2 * r + 2) ** 2 * 4 + L * (2 * r + 1) ** 2 * 4 + 8)
 
 
-# FETCH_SIZE correction per kernel, calibrated on known byte counts (tools/kbench_fetchcal.hip,
-# profiles/r02ag_fetch_size_calibration.txt): coalesced streams (16-B or 4-B per lane, and the
-# build's LDS-DMA) report half their bytes (x2, as MI355X_MICROARCH.md §HBM states for 16-B
-# streams); the lookup's scattered 44-B window rows are counted at face value in 64-B sectors (x1).
-FETCH_FACTOR = {"lookup_kernel": 1}
+# FETCH_SIZE correction per kernel, calibrated on known byte counts (tools/kbench_fetchcal.hip):
+# coalesced streams (16-B or 4-B per lane, and the build's LDS-DMA) report half their bytes (x2, as
+# MI355X_MICROARCH.md §HBM states for 16-B streams; profiles/r02ag_fetch_size_calibration.txt), and
+# so does the round-5 lookup's tiled window gather (16-B tile-row chunks: half of the 128-B lines
+# it touches, profiles/r05m_fetch_size_calibration.txt).  Only rounds 1-4's row-major gather of
+# scattered 44-B row segments was counted at face value in 64-B sectors (x1); no profile of that
+# layout is read any more (traffic() takes the newest).
+FETCH_FACTOR = {}
 
 
 def traffic(workload, kernel):

@@ -428,7 +428,7 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
 #pragma unroll
         for (int r = 0; r < kPatchRows; ++r)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) v[r][g] = (ACC2 ? acc[i][r][g] + acs[i][r][g] : acc[i][r][g]) * p.inv_s;
+            for (int g = 0; g < 4; ++g) v[r][g] = (ACC2 ? split_sum(acc[i][r][g], acs[i][r][g]) : acc[i][r][g]) * p.inv_s;
         if (qok && nlev > 0) {
             float *m0 = p.lvl[0] + qrow * M0;
 #pragma unroll

@@ -44,6 +44,12 @@ __host__ __device__ inline unsigned map_cell(int y, int x, int TC) {
 // Offset of the 16-B chunk holding cells (y, 4t .. 4t + 3).
 __host__ __device__ inline unsigned map_row4(int y, int t, int TC) { return map_cell(y, 4 * t, TC); }
 
+// Sum of a three-piece split product's two accumulators (hi*hi; the five smaller piece products).
+// An infinite feature splits as (inf, 0, 0), so the small products hold inf * 0 = NaN where fp32
+// gives inf * x = inf; the leading sum already carries fp32's inf / NaN status (inf * 0 and
+// opposite infinities reach it as NaN), so an infinite leading sum is the result.
+__device__ inline float split_sum(float hi, float lo) { return __builtin_isinf(hi) ? hi : hi + lo; }
+
 // Set the thread-local error and return `code`.
 int fail(int code, const char *fmt, ...);
 // Map a HIP status to CORR_OK / CORR_EHIP (recording the message).

@@ -113,8 +113,11 @@ struct LookupSmem {
 // window (unconditional: out-of-window cells go to the row's spare columns).  All of a thread's
 // loads are issued before any LDS store, so the gather costs one memory round trip.  The
 // query map bases are wave-uniform: qb is moved to a scalar register, so the 64-bit base
-// arithmetic is scalar.  NOLOAD: ablation (tools/kbench_lookup.hip).
-template <int S, int QB, int NT, bool NOLOAD = false>
+// arithmetic is scalar.  TIGHT: only the rows / 16-B chunks the query's taps can touch (anchor ..
+// floor(last tap) + 1 on each axis: floors are monotone in the tap index) are loaded — a regular
+// window is 10 x 10 of the 11 x 11 neighbourhood; uncovered and far queries load all of it.  The
+// cells not loaded are written as zeros and never read.  NOLOAD: ablation (tools/kbench_lookup.hip).
+template <int S, int QB, int NT, bool NOLOAD = false, bool TIGHT = false>
 __device__ __forceinline__ void gather_window_tiled(LookupSmem<S, QB> &sm, const float *P, size_t qbase,
                                                     unsigned mapsz, int n0, int N, int Wl, int Hl, int tid) {
     using SM = LookupSmem<S, QB>;
@@ -138,12 +141,16 @@ __device__ __forceinline__ void gather_window_tiled(LookupSmem<S, QB> &sm, const
     // LDS at once (lane k holds query k's) and moved to scalar registers with readlane.
     const int wu = __builtin_amdgcn_readfirstlane(tid >> 6);
     const unsigned qb = __builtin_amdgcn_readfirstlane((unsigned)qbase);
-    int myX = kFarAnchor, myY = kFarAnchor;
+    int myX = kFarAnchor, myY = kFarAnchor, myE = WIN | (WIN << 8);
     {
         const int qq = wu + NW * lane;
         if (lane < QPW && qq < QB && n0 + qq < N) {
             myX = sm.ax[qq];
             myY = sm.ay[qq];
+            if (TIGHT && myX != kFarAnchor && myY != kFarAnchor) {
+                const float fx0 = sm.fx[0][qq], fxl = sm.fx[1][qq], fy0 = sm.ty[0][0][qq], fyl = sm.ty[0][S - 1][qq];
+                if (window_covers<S>(fx0, fxl, fy0, fyl)) myE = ((int)(fxl - fx0) + 2) | (((int)(fyl - fy0) + 2) << 8);
+            }
         }
     }
     f32x4 vals[QPW][EPL];
@@ -153,10 +160,16 @@ __device__ __forceinline__ void gather_window_tiled(LookupSmem<S, QB> &sm, const
         const int X0 = __builtin_amdgcn_readlane(myX, k);
         const int Y0 = __builtin_amdgcn_readlane(myY, k);
         const float *Pq = P + (size_t)(qb + (unsigned)qq) * mapsz;
+        int nx = WIN, ny = WIN;
+        if (TIGHT) {
+            const int E = __builtin_amdgcn_readlane(myE, k);
+            nx = (E & 255) + (X0 & 3), ny = E >> 8;  // chunk columns start at X0 & ~3
+        }
 #pragma unroll
         for (int v = 0; v < EPL; ++v) {
             const unsigned T = (unsigned)((X0 >> 2) + tc[v]), Y = (unsigned)(Y0 + rr[v]);
-            const bool ok = (lane + 64 * v < LPQ) && T < TW && Y < (unsigned)Hl;
+            const bool need = !TIGHT || (rr[v] < ny && 4 * tc[v] < nx);
+            const bool ok = (lane + 64 * v < LPQ) && need && T < TW && Y < (unsigned)Hl;
             vals[k][v] = (ok && !NOLOAD) ? *reinterpret_cast<const f32x4 *>(Pq + map_row4((int)Y, (int)T, TC))
                                          : f32x4{0.f, 0.f, 0.f, 0.f};
         }
@@ -195,7 +208,7 @@ constexpr int lookup_threads(int S, int QB) { return (QB * S + 63) / 64 * 64; }
 // (global NCHW stores), lookup_conv_kernel (LDS tile feeding the fused 1x1 convolution) and
 // lookup_conv_bwd_dw_kernel.  The lookup of one block with its coords already loaded (cxv, cyv:
 // this thread's query; 0 for threads without one).
-template <int S, int QB, int NT, int ABL, class Emit>
+template <int S, int QB, int NT, int ABL, class Emit, bool TIGHT = false>
 __device__ __forceinline__ void lookup_block_v(LookupSmem<S, QB> &sm, const float *__restrict__ P, float cxv,
                                                float cyv, int b, int n0, int N, int H, int W, int l, int tid,
                                                Emit emit) {
@@ -242,7 +255,7 @@ __device__ __forceinline__ void lookup_block_v(LookupSmem<S, QB> &sm, const floa
     }
 
     // ---- 2. neighbourhoods -> LDS ----
-    gather_window_tiled<S, QB, NT, (ABL & 1) != 0>(sm, P, qbase, mapsz, n0, N, Wl, Hl, tid);
+    gather_window_tiled<S, QB, NT, (ABL & 1) != 0, TIGHT>(sm, P, qbase, mapsz, n0, N, Wl, Hl, tid);
     __syncthreads();
     const int mode = sm.flags;
     if (!act) return;
@@ -309,7 +322,7 @@ __device__ __forceinline__ void lookup_block_v(LookupSmem<S, QB> &sm, const floa
     }
 }
 
-template <int S, int QB, int NT, int ABL, class Emit>
+template <int S, int QB, int NT, int ABL, bool TIGHT = false, class Emit>
 __device__ __forceinline__ void lookup_block(LookupSmem<S, QB> &sm, const float *__restrict__ P,
                                              const float *__restrict__ coords, int b, int n0, int N,
                                              int H, int W, int l, int tid, Emit emit) {
@@ -317,10 +330,10 @@ __device__ __forceinline__ void lookup_block(LookupSmem<S, QB> &sm, const float 
     const bool qok = tid / QB < S && n < N;
     const float cxv = (ABL & 4) ? (float)(n % W) : qok ? coords[((size_t)b * 2 + 0) * N + n] : 0.0f;
     const float cyv = (ABL & 4) ? (float)(n / W) : qok ? coords[((size_t)b * 2 + 1) * N + n] : 0.0f;
-    lookup_block_v<S, QB, NT, ABL>(sm, P, cxv, cyv, b, n0, N, H, W, l, tid, emit);
+    lookup_block_v<S, QB, NT, ABL, Emit, TIGHT>(sm, P, cxv, cyv, b, n0, N, H, W, l, tid, emit);
 }
 
-template <int S, int QB, int ABL = 0>
+template <int S, int QB, int ABL = 0, bool TIGHT = false>
 __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
     ConstLevelPtrs pyr, const float *__restrict__ coords, int B, int NQ, int H, int W, int L,
     float *__restrict__ out) {
@@ -333,7 +346,7 @@ __global__ __launch_bounds__(lookup_threads(S, QB)) void lookup_kernel(
     const int l = blockIdx.y;
     const int i = threadIdx.x / QB, n = n0 + threadIdx.x % QB;
     float *o = out + (((size_t)b * L + l) * K + (size_t)i * S) * N + n;
-    lookup_block<S, QB, NT, ABL>(sm, pyr.p[l], coords, b, n0, N, H, W, l, (int)threadIdx.x, [&](int j, float acc) {
+    lookup_block<S, QB, NT, ABL, TIGHT>(sm, pyr.p[l], coords, b, n0, N, H, W, l, (int)threadIdx.x, [&](int j, float acc) {
         // non-temporal: the output streams past L2 (nothing in this kernel re-reads it), so the
         // kernel's end has no dirty lines of it to write back (DSEC 5.8 -> 5.4 us, train 12.2 ->
         // 11.4 us, same bits; profiles/r04q_kbench_lookup_nt.txt)
@@ -478,7 +491,7 @@ __global__ __launch_bounds__(kLcNT) void lookup_conv_kernel(ConstLevelPtrs pyr, 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int o = 32 * w + 16 * t + 4 * (lane >> 4) + r;
-                float v = (acc[t][c][r] + acs[t][c][r]) + bias[o];
+                float v = split_sum(acc[t][c][r], acs[t][c][r]) + bias[o];
                 if (relu && v < 0.0f) v = 0.0f;  // torch.relu: a NaN stays a NaN (fmaxf would drop it)
                 __builtin_nontemporal_store(v, &out[((size_t)b * kLcO + o) * N + n]);  // streams past L2
             }
@@ -1608,6 +1621,23 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const float *__restrict__
     }
 }
 
+template <int S, int QB>
+hipError_t launch_lookup_qb(const ConstLevelPtrs &pyr, const float *coords, int B, int NQ, int H, int W, int L,
+                            float *out, hipStream_t s) {
+    // TIGHT (only the window rows / 16-B chunks the query's taps touch) pays once the grid is
+    // bandwidth-bound, >= 18,000 queries; below that its extents arithmetic sits on the latency
+    // chain (same bits; profiles/r05m_kbench_lookup.txt: 1280x960 16.8 -> 16.1 us, B12 36x48
+    // 15.9 -> 15.5, MVSEC 36x44 B16 18.6 -> 18.5; DSEC 5.6 -> 6.1, train B8 10.4 -> 10.6)
+    const int nqb = (NQ + QB - 1) / QB;
+    if ((long)B * NQ >= 18000)
+        hipLaunchKernelGGL((lookup_kernel<S, QB, 0, true>), dim3(nqb * B, L), dim3(lookup_threads(S, QB)), 0, s,
+                           pyr, coords, B, NQ, H, W, L, out);
+    else
+        hipLaunchKernelGGL((lookup_kernel<S, QB>), dim3(nqb * B, L), dim3(lookup_threads(S, QB)), 0, s, pyr, coords,
+                           B, NQ, H, W, L, out);
+    return hipGetLastError();
+}
+
 template <int S>
 hipError_t launch_lookup_s(const ConstLevelPtrs &pyr, const float *coords, int B, int NQ, int H,
                            int W, int L, float *out, hipStream_t s) {
@@ -1615,19 +1645,10 @@ hipError_t launch_lookup_s(const ConstLevelPtrs &pyr, const float *coords, int B
     // all, where the smaller workgroups pack the CUs better over several rounds (same bits;
     // tools/kbench_lookup with the non-temporal output stores, profiles/r04t_kbench_lookup_qb2.txt:
     // QB 16 / 32 = MVSEC 36x44 B16 19.0 / 19.6 us, B12 36x48 16.1 / 16.1; train B8 12.0 / 11.7,
-    // MVSEC crop 32x32 B16 12.3 / 11.3, DSEC 5.5 / 5.4, 1280x960 22.6 / 22.1)
-    if (S == 9 && H * W <= 2048 && (long)B * NQ >= 20000) {
-        constexpr int QB = 16;
-        const int nqb = (NQ + QB - 1) / QB;
-        hipLaunchKernelGGL((lookup_kernel<S, QB>), dim3(nqb * B, L), dim3(lookup_threads(S, QB)), 0, s,
-                           pyr, coords, B, NQ, H, W, L, out);
-        return hipGetLastError();
-    }
-    constexpr int QB = 32;
-    const int nqb = (NQ + QB - 1) / QB;
-    hipLaunchKernelGGL((lookup_kernel<S, QB>), dim3(nqb * B, L), dim3(lookup_threads(S, QB)), 0, s,
-                       pyr, coords, B, NQ, H, W, L, out);
-    return hipGetLastError();
+    // MVSEC crop 32x32 B16 12.3 / 11.3, DSEC 5.5 / 5.4, 1280x960 22.6 / 22.1; with the tiled
+    // pyramid, profiles/r05m_kbench_lookup.txt: MVSEC 18.6 / 19.2, B12 15.9 / 15.7, train 10.3 / 10.2)
+    if (S == 9 && H * W <= 2048 && (long)B * NQ >= 20000) return launch_lookup_qb<S, 16>(pyr, coords, B, NQ, H, W, L, out, s);
+    return launch_lookup_qb<S, 32>(pyr, coords, B, NQ, H, W, L, out, s);
 }
 
 template <int S>

@@ -239,6 +239,28 @@ def test_gpu_pyramid_and_lookup_vs_oracle(B, D, H, W, L, r, algo, monkeypatch):
     assert bit_equal(cb(torch.from_numpy(c).to(DEV)).cpu().numpy(), oracle.lookup(gpu, c, r))
 
 
+@pytest.mark.parametrize("B,H,W", [(1, 120, 160), (2, 90, 104)])
+def test_lookup_tight_gather_vs_oracle(B, H, W):
+    """>= 18,000 queries: the lookup gathers only the window rows / 16-B chunks its taps touch
+    (corr_lookup.hip launch_lookup_qb, TIGHT).  Bit-exact against the oracle on the exported
+    pyramid for random flows, the integer grid (every tap on a cell: the window's extra row and
+    column unused), the special coordinates (borders, far outside, half pixels) and NaN / inf /
+    huge coordinates sprinkled over the map."""
+    D, L, r = 32, 4, 4
+    f1, f2 = prng.gauss(91, (B, D, H, W)), prng.gauss(92, (B, D, H, W))
+    cb = _cb()(torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV), num_levels=L, radius=r)
+    pyr = [p.cpu().numpy() for p in cb.corr_pyramid]
+    cases = [prng.lookup_coords(93, B, H, W, 6.0), prng.coords_grid(B, H, W), prng.special_coords(B, H, W)]
+    c = prng.lookup_coords(94, B, H, W, 3.0)
+    flat = c.reshape(-1)
+    idx = (prng.uniform(95, (64,)) * flat.size).astype(np.int64)
+    flat[idx] = np.resize(np.array([np.nan, np.inf, -np.inf, 3.0e38, -1e30, 1e6, -0.0, 2.0 ** 20], np.float32), 64)
+    cases.append(c)
+    for c in cases:
+        out = cb(torch.from_numpy(c).to(DEV)).cpu().numpy()
+        assert bit_equal(out, oracle.lookup(pyr, c, r))
+
+
 @pytest.mark.parametrize("case", ["channel_scales", "pixel_scales", "zeros", "tiny", "huge"])
 def test_build_f16x3_dynamic_range(case):
     """The f16 split keeps fp32 accuracy over wide feature ranges: per-channel scales over
@@ -491,6 +513,69 @@ def test_bf16x6_pack_is_exact_split():
         # padding (k >= D, pixels past the map) is zero
         assert (img[:, :, D:] == 0).all()
     assert (q[..., N:] == 0).all() and (t[..., H:, :] == 0).all() and (t[..., W:] == 0).all()
+
+
+@pytest.mark.parametrize("algo_name", ["BUILD_BF16X6", "LOOKUP_CONV"])
+def test_bf16x6_infinite_features_match_fp32(algo_name):
+    """Infinite features through the three-piece split: +-inf splits as (inf, 0, 0), so the small
+    piece products hold inf * 0 = NaN; the result keeps the leading hi*hi sum when that is infinite
+    (corr_common.h split_sum), giving fp32's inf where fp32 gives inf, and NaN exactly where fp32
+    gives NaN (inf * 0 against a zero feature, opposite infinities).  Checked against the
+    fp32-operand build on the full 4-level pyramid: same NaN cells, same infinities with the same
+    signs, finite cells within 1e-5 of the row scale.  LOOKUP_CONV: the fused lookup + 1x1 conv,
+    whose corr operand then holds the infinities, against the plain lookup + an fp64 conv."""
+    from eraft_amd import _lib
+    B, D, H, W, L = 1, 64, 16, 24, 4
+    f1, f2 = prng.gauss(61, (B, D, H, W)), prng.gauss(62, (B, D, H, W))
+    f1[0, 3, 0, 5] = np.inf
+    f1[0, 10, 2, 7] = -np.inf
+    f1[0, 20, 5, 5] = np.inf
+    f1[0, 21, 5, 5] = -np.inf        # pixel (5,5): opposite infinities against any nonzero pair
+    if algo_name == "BUILD_BF16X6":
+        f2[0, 3, 4, 4] = 0.0         # inf * 0 for query (0,5) at target (4,4)
+        f2[0, 10, 1, 1] = np.inf     # -inf * inf for query (2,7) at (1,1)
+        f2[0, 3, 9, 9] = -np.inf     # inf * -inf for query (0,5) at (9,9)
+    else:
+        # one-signed infinite rows for the conv: query (0,5) +inf, (2,7) -inf, (5,5) NaN everywhere
+        for c in (3, 10, 20, 21):
+            f2[0, c] = np.abs(f2[0, c]) + np.float32(0.1)
+    t1, t2 = torch.from_numpy(f1).to(DEV), torch.from_numpy(f2).to(DEV)
+    out = {}
+    for algo in (_lib.BUILD_BF16X6, _lib.BUILD_FP32):
+        lv = tiled_levels(B, H, W, L, DEV)
+        _lib.build(t1, t2, lv, algo)
+        out[algo] = lv
+    if algo_name == "BUILD_BF16X6":
+        pairs = zip(export_levels(out[_lib.BUILD_BF16X6], H, W), export_levels(out[_lib.BUILD_FP32], H, W))
+        got = [(a.reshape(B * H * W, -1), b.reshape(B * H * W, -1)) for a, b in pairs]
+    else:
+        # the fused lookup's corr operand is the bf16x6 pyramid split again: feed it the fp32 build
+        # (same infinities) and compare with the unfused lookup + fp64 conv
+        r = 4
+        C = L * (2 * r + 1) ** 2
+        coords = torch.from_numpy(prng.lookup_coords(63, B, H, W, 3.0)).to(DEV)
+        # positive weights keep the +-inf lookups infinite through the conv (mixed signs: NaN);
+        # the weights' mid / lo pieces are nonzero, so the small products meet inf * lo terms
+        w = torch.from_numpy(np.abs(prng.gauss(64, (256, C), 0.05)) + np.float32(1e-3)).to(DEV)
+        bias = torch.from_numpy(prng.gauss(65, (256,), 0.1)).to(DEV)
+        lk = torch.empty(B, C, H, W, device=DEV)
+        _lib.lookup(out[_lib.BUILD_FP32], coords, r, lk)
+        lk = lk.cpu().numpy().astype(np.float64)
+        assert np.isinf(lk).any()
+        with np.errstate(invalid="ignore"):
+            ref = np.einsum("oc,bchw->bohw", w.cpu().numpy().astype(np.float64), lk)
+        ref = ref + bias.cpu().numpy()[None, :, None, None]
+        fused = torch.empty(B, 256, H, W, device=DEV)
+        _lib.lookup_conv(out[_lib.BUILD_FP32], coords, r, _lib.lookup_conv_weights(w), bias, fused, relu=False)
+        fused = fused.cpu().numpy()
+        got = [(fused.reshape(256, -1).T, ref.astype(np.float32).reshape(256, -1).T)]
+    for a, b in got:
+        assert np.array_equal(np.isnan(a), np.isnan(b))
+        inf = np.isinf(b)
+        assert inf.any() and np.array_equal(np.isinf(a), inf) and np.array_equal(a[inf], b[inf])
+        fin = np.isfinite(b)
+        scale = np.where(fin, np.abs(b), 0).max(axis=1, keepdims=True)
+        assert (np.abs(np.where(fin, a - b, 0)) <= 1e-5 * scale + 1e-30).all()
 
 
 def test_lookup_nan_and_inf_coords():

@@ -72,10 +72,10 @@ struct Variant {
     std::vector<float> us;
 };
 
-template <int QB, int ABL = 0>
+template <int QB, int ABL = 0, bool TIGHT = false>
 static hipError_t launch_qb(const ConstLevelPtrs &pyr, const float *coords, int B, int H, int W, float *out) {
     const int nqb = (H * W + QB - 1) / QB;
-    hipLaunchKernelGGL((lookup_kernel<9, QB, ABL>), dim3(nqb * B, 4), dim3(lookup_threads(9, QB)), 0, 0, pyr,
+    hipLaunchKernelGGL((lookup_kernel<9, QB, ABL, TIGHT>), dim3(nqb * B, 4), dim3(lookup_threads(9, QB)), 0, 0, pyr,
                        coords, B, H * W, H, W, 4, out);
     return hipGetLastError();
 }
@@ -116,6 +116,9 @@ int main(int argc, char **argv) {
         vs.push_back({"prod launch_lookup", [=](float *o) { return launch_lookup(lp, coords, B, H * W, H, W, 4, 4, o, 0); }, {}});
         vs.push_back({"QB16", [=](float *o) { return launch_qb<16>(lp, coords, B, H, W, o); }, {}});
         vs.push_back({"QB32", [=](float *o) { return launch_qb<32>(lp, coords, B, H, W, o); }, {}});
+        vs.push_back({"QB16 tight", [=](float *o) { return launch_qb<16, 0, true>(lp, coords, B, H, W, o); }, {}});
+        vs.push_back({"QB32 tight", [=](float *o) { return launch_qb<32, 0, true>(lp, coords, B, H, W, o); }, {}});
+        vs.push_back({"QB32 tight grid", [=](float *o) { return launch_qb<32, 0, true>(lp, coords_g, B, H, W, o); }, {}});
         vs.push_back({"prod smooth-flow", [=](float *o) { return launch_lookup(lp, coords_s, B, H * W, H, W, 4, 4, o, 0); }, {}});
         vs.push_back({"prod grid (integer)", [=](float *o) { return launch_lookup(lp, coords_g, B, H * W, H, W, 4, 4, o, 0); }, {}});
         vs.push_back({"QB16 smooth-flow", [=](float *o) { return launch_qb<16>(lp, coords_s, B, H, W, o); }, {}});
@@ -123,6 +126,9 @@ int main(int argc, char **argv) {
         vs.push_back({"QB16 cached-stores", [=](float *o) { return launch_qb<16, 8>(lp, coords, B, H, W, o); }, {}});
         vs.push_back({"QB32 cached-stores", [=](float *o) { return launch_qb<32, 8>(lp, coords, B, H, W, o); }, {}});
         CK(vs[0].launch(ref));
+        float *ref_g;  // the integer-grid coords' reference (production launch)
+        CK(hipMalloc(&ref_g, n_out * 4));
+        CK(launch_lookup(lp, coords_g, B, H * W, H, W, 4, 4, ref_g, 0));
         for (auto &v : vs) {
             CK(hipMemset(out, 0, n_out * 4));
             CK(v.launch(out));
@@ -130,11 +136,11 @@ int main(int argc, char **argv) {
             unsigned long long *d, diff = 0;
             CK(hipMalloc(&d, sizeof(*d)));
             CK(hipMemset(d, 0, sizeof(*d)));
-            hipLaunchKernelGGL(count_diff, dim3(2048), dim3(256), 0, 0, ref, out, n_out, d);
+            const bool grid = v.name.find("grid") != std::string::npos;
+            hipLaunchKernelGGL(count_diff, dim3(2048), dim3(256), 0, 0, grid ? ref_g : ref, out, n_out, d);
             CK(hipMemcpy(&diff, d, sizeof(diff), hipMemcpyDeviceToHost));
             CK(hipFree(d));
-            const bool same_inputs = v.name.rfind("abl", 0) != 0 && v.name.find("smooth") == std::string::npos &&
-                                     v.name.find("grid") == std::string::npos;
+            const bool same_inputs = v.name.rfind("abl", 0) != 0 && v.name.find("smooth") == std::string::npos;
             if (diff && same_inputs) printf("!! %s differs in %llu elements\n", v.name.c_str(), diff);
         }
         for (int r = 0; r < rounds; ++r)
@@ -158,6 +164,7 @@ int main(int argc, char **argv) {
         CK(hipFree(coords));
         CK(hipFree(ref));
         CK(hipFree(out));
+        CK(hipFree(ref_g));
     }
     return 0;
 }
