@@ -56,7 +56,8 @@ def default_algo() -> int:
 
 def backward_algo(algo=None) -> int:
     """The backward GEMMs' algorithm for a build algorithm: each build's own arithmetic (bf16x6:
-    the exact three-piece bf16 split GEMMs, no narrower than fp32; f16x3: the two-piece f16 split;
+    the exact three-piece bf16 split GEMMs, smaller worst / mean row error than fp32's; f16x3: the
+    two-piece f16 split;
     fp32: the fp32-operand MFMA GEMMs)."""
     return default_algo() if algo is None else algo
 

@@ -54,8 +54,8 @@ extern "C" {
  *        built against 101 must check this version before calling it.
  *   103: CORR_BUILD_BF16X6, corr_build_region, corr_lookup_conv_bwd (the packed weight buffer
  *        grew: size it with corr_lookup_conv_weights_bytes()).
- *   104: corr_build_bwd_ex / corr_backward accept CORR_BUILD_BF16X6 (backward GEMMs no narrower
- *        than fp32); E-RAFT's default backward for the BF16X6 build.
+ *   104: corr_build_bwd_ex / corr_backward accept CORR_BUILD_BF16X6 (backward GEMMs on the exact
+ *        bf16 split); E-RAFT's default backward for the BF16X6 build.
  *   200: the value pyramid (the builds' output, the lookups' input) is TILED (see Layouts;
  *        16-B aligned levels, corr_map_floats per map); corr_map_floats, corr_pyramid_export,
  *        corr_pyramid_import.  Gradient pyramids keep the reference layout. */
@@ -217,9 +217,9 @@ int corr_build_bwd_rows(const float *grad_c, const float *fmap1_rows, int NQ, co
  * CORR_BUILD_BF16X6 splits every element of F1 / F2 / dC EXACTLY into three bf16 pieces while
  * staging it (no scales, no maxima; the one floor as for the build: |x| < ~2^-110) and runs the
  * six piece products of weight >= 2^-16 per product on the bf16 MFMA into one fp32 accumulator
- * (6 roundings per 16 k, an fp32 fmaf chain 16): no narrower than CORR_BUILD_FP32 (every element
- * within (3 + 6 ceil(K/16) + splits) u sum|ab|; worst and mean row error below the fp32 GEMMs',
- * checked against fp64).  CORR_BUILD_F16X3 packs F1, F2 (per feature row d) and dC (per query
+ * (6 roundings per 16 k, an fp32 fmaf chain 16): every element within (3 + 6 ceil(K/16) + splits)
+ * u sum|ab| (an fp32 dot product: K u sum|ab|), worst and mean row error below the fp32 GEMMs',
+ * checked against fp64 — but with one accumulator not every single row (unlike the build's).  CORR_BUILD_F16X3 packs F1, F2 (per feature row d) and dC (per query
  * row for dfmap1, per target column for dfmap2) as 2^e (hi + lo) f16 pairs and runs three f16
  * MFMAs per product (~2^-22 relative: narrower than fp32).  Split-K partial sums are reduced in
  * split order (deterministic).
