@@ -41,6 +41,7 @@
 
 #include "corr_build_common.h"
 #include "corr_common.h"
+#include "corr_div.h"
 
 namespace corr {
 namespace {
@@ -59,14 +60,16 @@ struct Axis {
     float hi;  // ix - f        : weight of corner f + 1
 };
 
-__device__ __forceinline__ Axis tap_axis(float c, float inv_scale, int t, int r, int size) {
+// rden = recip_rn(size - 1), hoisted by the callers (per level)
+__device__ __forceinline__ Axis tap_axis(float c, float inv_scale, int t, int r, int size, float rden) {
     // corr.py:41  centroid = coords / 2**l   (exact: power-of-two scale)
     // corr.py:43  + delta (integer offsets from linspace(-r, r, 2r+1))
     // utils.py:11 2*x/(W-1) - 1 ; grid_sample unnormalise ((x'+1)/2)*(W-1)
+    // The division is correctly rounded (corr_div.h: the same bits as __fdiv_rn in 3 VALU)
     const float cl = c * inv_scale;
     const float X = cl + (float)(t - r);
     const float den = (float)(size - 1);
-    const float xn = __fsub_rn(__fdiv_rn(2.0f * X, den), 1.0f);
+    const float xn = __fsub_rn(div_rn(2.0f * X, den, rden), 1.0f);
     const float ix = __fmul_rn(__fmul_rn(__fadd_rn(xn, 1.0f), 0.5f), den);
     Axis a;
     a.f = floorf(ix);
@@ -229,8 +232,8 @@ __device__ __forceinline__ void lookup_block_v(LookupSmem<S, QB> &sm, const floa
 
     // ---- 1. taps ----
     if (tid == 0) sm.flags = 0;
-    const Axis tx = tap_axis(cxv, inv_scale, i, R, Wl);
-    const Axis ty = tap_axis(cyv, inv_scale, i, R, Hl);
+    const Axis tx = tap_axis(cxv, inv_scale, i, R, Wl, recip_rn((float)(Wl - 1)));
+    const Axis ty = tap_axis(cyv, inv_scale, i, R, Hl, recip_rn((float)(Hl - 1)));
     if (act) {
         sm.ty[0][i][q] = ty.f;
         sm.ty[1][i][q] = ty.lo;
@@ -933,6 +936,7 @@ __global__ __launch_bounds__(lookup_bwd_threads(S, BQ)) void lookup_bwd_kernel(B
         for (size_t i = tid; i < cells; i += NT) Z[i] = 0.0f;
         __syncthreads();
     }
+    const float rdx = recip_rn((float)(Wl - 1)), rdy = recip_rn((float)(Hl - 1));
     for (int lt = 0; lt < lk.T; ++lt) {
     // constant-index selects (s_cselect): a dynamic index into the by-value table would copy it
     // to scratch
@@ -950,8 +954,8 @@ __global__ __launch_bounds__(lookup_bwd_threads(S, BQ)) void lookup_bwd_kernel(B
     if (t < S) {
         const float cxv = qok ? coords[((size_t)b * 2 + 0) * N + n] : 0.0f;
         const float cyv = qok ? coords[((size_t)b * 2 + 1) * N + n] : 0.0f;
-        a = tap_axis(cxv, inv_scale, t, R, Wl);
-        c = tap_axis(cyv, inv_scale, t, R, Hl);
+        a = tap_axis(cxv, inv_scale, t, R, Wl, rdx);
+        c = tap_axis(cyv, inv_scale, t, R, Hl, rdy);
         const float *g = grad_out + (((size_t)b * L + l) * K + (size_t)t * S) * N + n;
         float v[S];
 #pragma unroll
@@ -1140,6 +1144,17 @@ __global__ __launch_bounds__(lookup_bwd_threads(S, BQ)) void lookup_bwd_kernel(B
 // (branchless: out-of-map cells go to a per-lane dump slot).
 constexpr int kFusedLv = 4;  // level slots (= waves) per workgroup
 
+// median of three (v_med3_i32: clang does not form it from min / max with runtime bounds)
+__device__ __forceinline__ int med3_i32(int x, int lo, int hi) {
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
+    return r;
+}
+
+// A byte address past any workgroup's LDS allocation (<= 160 KiB) even after a map's worth of rows
+// is subtracted: DS reads there return 0, DS writes are dropped.
+constexpr int kLdsOob = 1 << 20;
+
 constexpr int fused_slots(int S) { return S + 2 <= 4 ? 4 : S + 2 <= 8 ? 8 : S + 2 <= 16 ? 16 : 32; }
 
 struct FusedOut {
@@ -1281,6 +1296,7 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     const int lc = act ? l : 0;
     const int Hl = H >> lc, Wl = W >> lc;
     const float inv_scale = 1.0f / (float)(1 << lc);
+    const float rdx = recip_rn((float)(Wl - 1)), rdy = recip_rn((float)(Hl - 1));
     float *st = fsm + o.aux + lc * ST::SIZE;  // this wave's staging
     const int mbase = o.moff[lc] + q * o.qstr[lc];
     const int dump = o.aux + lc * ST::SIZE + ST::DUMP + lane;
@@ -1327,8 +1343,8 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
 #pragma unroll
         for (int u = 0; u < S; ++u) v[u] = pv[u];
         prefetch(min(t + 1, lk.T - 1));
-        const Axis a = tap_axis(cxv, inv_scale, cxl, R, Wl);
-        const Axis c = tap_axis(cyv, inv_scale, cxl, R, Hl);
+        const Axis a = tap_axis(cxv, inv_scale, cxl, R, Wl, rdx);
+        const Axis c = tap_axis(cyv, inv_scale, cxl, R, Hl, rdy);
         // ---- 2. the (query, level) group's form, decided per group ----
         const float fx0 = group_lane<SLOTS, 0>(a.f, lane), fy0 = group_lane<SLOTS, 0>(c.f, lane);
         const bool bad = cx < S && !(a.f - fx0 == (float)cx && c.f - fy0 == (float)cx);
@@ -1395,14 +1411,23 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
                 sv[cy] = acc.x;
                 sv[cy + 1] = acc.y;
             }
-            // byte addresses of the column's cells: one compare, one add and one select per cell
-            const int ayc = cx < C ? ayv : -(1 << 30);
-            const unsigned rb = 4u * (unsigned)rowbase, stride = 4u * (unsigned)Wl, db = 4u * (unsigned)dump;
+            // byte addresses of the column's cells: row ay + cy clamped to [-1, Hl] — rows -1 and Hl
+            // of every map are guard rows (fused_lds_bytes), so the window's cells above / below the
+            // map land in a guard row nothing reads — and a column that is not this lane's to write
+            // starts past the workgroup's LDS allocation, where DS reads return 0 and DS writes are
+            // dropped.  Clamping the ADDRESS of row ay + cy between those of rows -1 and H_l is the
+            // same (addresses grow with the row), so a cell costs one add and one v_med3.
+            const bool mine = colok && cx < C;
+            const int cb = mine ? 4 * (mbase + X) : kLdsOob;
+            const int s4 = 4 * Wl;
+            const int gtop = cb - s4, gbot = cb + Hl * s4;
+            // rows past [-C, H_l] clamp like those bounds (and keep s4 * ay in range)
+            int ra = cb + s4 * (mine ? min(max(ay, -C), Hl) : 0);
             char *const lds = reinterpret_cast<char *>(fsm);
             float old[C];
             unsigned at[C];
 #pragma unroll
-            for (int cy = 0; cy < C; ++cy) at[cy] = (unsigned)(ayc + cy) < (unsigned)Hl ? rb + cy * stride : db;
+            for (int cy = 0; cy < C; ++cy, ra += s4) at[cy] = (unsigned)med3_i32(ra, gtop, gbot);
 #pragma unroll
             for (int cy = 0; cy < C; ++cy) old[cy] = *reinterpret_cast<float *>(lds + at[cy]);  // all reads, then all writes
 #pragma unroll
@@ -1817,16 +1842,20 @@ namespace {
 template <int S>
 size_t fused_lds_bytes(int H, int W, int levels, FusedOut *o) {
     using ST = FusedStage<S>;
-    // query stride = map cells rounded up to 64 / BQ (mod 64): the BQ queries' maps start in
-    // different LDS banks, so a wave's read-modify-writes of neighbouring queries' windows (whose
-    // anchors differ by about one pixel) do not collide
+    // query stride = map cells plus one guard row, rounded up to 64 / BQ (mod 64): the BQ
+    // queries' maps start in different LDS banks, so a wave's read-modify-writes of neighbouring
+    // queries' windows (whose anchors differ by about one pixel) do not collide.  Every map has a
+    // guard row above (row -1) and below (row H_l), which the closed form's clamped rows write
+    // (one row may serve as one map's row H_l and the next map's row -1); a level's region is a
+    // leading guard row and BQ query strides, rounded to 64 floats.
     size_t maps = 0;
     const int stag = 64 / ST::BQ;
     for (int l = 0; l < kFusedLv; ++l) {
-        const int msz = l < levels ? (H >> l) * (W >> l) : 0;
-        const int qs = msz ? (msz + 63) / 64 * 64 + stag : 0;
-        if (o) o->moff[l] = (int)maps, o->msz[l] = msz, o->qstr[l] = qs;
-        maps += (size_t)ST::BQ * qs;
+        const int Hl = H >> l, Wl = W >> l;
+        const int msz = l < levels ? Hl * Wl : 0;
+        const int qs = msz ? ((Hl + 1) * Wl + 63) / 64 * 64 + stag : 0;
+        if (o) o->moff[l] = (int)maps + (msz ? Wl : 0), o->msz[l] = msz, o->qstr[l] = qs;
+        if (msz) maps += ((size_t)Wl + (size_t)ST::BQ * qs + 63) / 64 * 64;
     }
     if (o) o->aux = (int)maps;
     return (maps + (size_t)kFusedLv * ST::SIZE + ST::BQ) * 4;

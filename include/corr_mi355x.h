@@ -101,7 +101,11 @@ int corr_build(const float *fmap1, const float *fmap2, int B, int D, int H, int 
  *                     added once.  The dropped terms are <= 2^-23 of |x_t x_q| and the main
  *                     accumulator rounds D/32 times per dot product (an fp32 fmaf chain: D
  *                     times): no narrower than CORR_BUILD_FP32 (checked per query row against
- *                     an fp64 oracle).  Needs a workspace for the split operands.
+ *                     an fp64 oracle).  +-inf features split as (inf, 0, 0); a result whose
+ *                     hi*hi sum is infinite is that sum, so infinities and NaNs land where the
+ *                     fp32 build puts them (one exception: an infinity against a nonzero feature
+ *                     below bf16's range, |x| < 2^-133, whose hi is 0: NaN where fp32 gives inf).
+ *                     Needs a workspace for the split operands.
  *                     ~2x faster than CORR_BUILD_FP32 on gfx950.
  *   CORR_BUILD_F16X3  each fp32 feature x of pixel n is split as 2^e_n * (hi + lo), f16 hi/lo,
  *                     e_n putting the pixel's largest |x| in [2^14, 2^15); three f16 MFMAs
