@@ -23,6 +23,7 @@ a bounded sample: ``cpu_baseline``.
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import platform
@@ -344,10 +345,17 @@ def cpu_e2e(model, im1, im2, finit, iters, budget_s):
                       f"median {med * 1e3:.0f} ms"}
 
 
-def settle(step, seconds=0.25, cap=5000):
+def settle(step, seconds=0.25, cap=5000, fixed=None):
     """Untimed replays after the W warmup steps until `seconds` have passed: the first ~100 ms of
     replays after a graph capture run 4-5 % slower (clock ramp / first touches of the graph
-    pool), which a 10-step warmup at DSEC (1.5 ms) does not cover (tools/ab_api_vs_direct.py)."""
+    pool), which a 10-step warmup at DSEC (1.5 ms) does not cover (tools/ab_api_vs_direct.py).
+    fixed = n: exactly n replays instead — a step with collectives (the row-sharded pair) must run
+    the same number of times on every rank, which a per-rank clock does not guarantee."""
+    if fixed is not None:
+        for _ in range(fixed):
+            step()
+        torch.cuda.synchronize()
+        return
     t0 = time.perf_counter()
     n = 0
     while n < cap and time.perf_counter() - t0 < seconds:
@@ -449,7 +457,8 @@ def main():
         # nccl = RCCL over xGMI; ERAFT_AMD_DIST_BACKEND=gloo rehearses the multi-rank path with
         # several ranks on ONE GPU (RCCL refuses two ranks per device)
         backend = os.environ.get("ERAFT_AMD_DIST_BACKEND", "nccl")
-        dist.init_process_group(backend, rank=rank, world_size=world,
+        # a mismatched collective fails after 5 minutes instead of holding the node for the default 10
+        dist.init_process_group(backend, rank=rank, world_size=world, timeout=datetime.timedelta(minutes=5),
                                 **({"device_id": dev} if backend == "nccl" else {}))
 
     if args.workload == "e2e":
@@ -643,11 +652,20 @@ def run_corr(args, wl_name, sharded, world, rank, dev, primary=True):
                 capture_error = f"{type(exc).__name__}: {exc}"
                 launch = "eager"
                 step = pair
+            if sharded and world > 1:
+                # every rank must replay the same collectives: one failed capture makes all eager
+                ok = torch.tensor([1 if capture_error is None else 0], device=dev, dtype=torch.int32)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                if int(ok.item()) == 0 and capture_error is None:
+                    capture_error = "another rank's capture failed"
+                    launch = "eager"
+                    step = pair
 
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
-        settle(step)
+        # the sharded pair holds collectives: every rank replays it the same number of times
+        settle(step, fixed=32 if sharded and world > 1 else None)
 
         if world > 1:
             dist.barrier()
