@@ -14,12 +14,11 @@
 //
 // MFMA orientation.  v_mfma_f32_16x16x32_f16 with A = TARGETS (rows) and B = QUERIES (columns):
 // lane l = 16 grp + ci owns query ci of a 16-query block and, in its 4 accumulator registers,
-// targets 4 grp .. 4 grp + 3 of a 16-target block.  A target block is one map row x 16
-// columns, so every lane holds runs of 4 consecutive pixels of one query's map: level 0 leaves
-// the registers as 16-B row stores (a store instruction writes 16 queries x one 64-B run each),
-// and with a wave's 8 blocks = an 8 x 16 target patch, the 2x2, 4x4 windows of levels 1 and 2
-// sit inside one lane (plain adds, the reference's ((a+b)+c)+d order, no shuffles and no LDS
-// staging); level 3 pairs lanes 16 apart (one shuffle per value).
+// targets 4 grp .. 4 grp + 3 of a 16-target block.  A target block is one 4x4 tile of the
+// pyramid (corr_common.h), so lane (grp, ci) holds tile row grp for query ci and the four lanes
+// of a query store the whole 64-B tile in one store instruction; a wave's 8 blocks are an 8 x 16
+// target patch (2 x 4 tiles), whose levels 1-3 pool across lanes 16 / 32 apart in the
+// reference's ((a+b)+c)+d order (shuffles, no LDS staging).
 //
 // Workgroup = 4 waves x 32 queries against ONE 8 x 16 target patch.  The patch's operand
 // records (16 KiB per 32-deep K step) stream into a 3-slot LDS ring by LDS-DMA
@@ -33,7 +32,8 @@
 // i.e. exactly the MFMA fragment image of that block, so the LDS fill and every fragment read
 // are contiguous 1 KiB (conflict-free ds_read_b128, coalesced loads).
 //   pq [B][S][NQB][2 KiB]     queries: block = 16 consecutive query pixels, NQp = NQB*16
-//   pt [B][S][Hp][CB][2 KiB]  targets: block = (row y, columns 16 cb .. 16 cb + 15)
+//   pt [B][S][Hp/4][4 CB][2 KiB]  targets: block = the 4x4 tile (rows 4 ty .., columns 4 tx ..),
+//                                 pixel ci at (ci / 4, ci % 4) — the pyramid's tile (corr_common.h)
 //   eq [B][NQp], et [B][Hp][Wp] int32 exponents.  Padding pixels are zero (exponent 0).
 #include <algorithm>
 #include <atomic>
@@ -110,7 +110,10 @@ __global__ __launch_bounds__(512) void split_pack_wide_kernel(PackArgs a) {
         valid = blk < nblk && n < a.np[0];
         exi = b * a.NQp + n;
     } else {
-        const int y = blk / a.CB, x = (blk - y * a.CB) * 16 + ci;
+        // target block = the 4x4 tile (tile row ty, column tx; 4 CB tiles per row), pixel ci at
+        // (ci / 4, ci % 4): each 16x16 MFMA output block is one pyramid tile (as in the bf16x6 pack)
+        const int TCp = 4 * a.CB, ty = blk / TCp, tx = blk - ty * TCp;
+        const int y = 4 * ty + (ci >> 2), x = 4 * tx + (ci & 3);
         valid = blk < nblk && y < a.H && x < a.W;
         n = y * a.W + x;
         exi = (b * a.Hp + y) * a.Wp + x;
@@ -222,13 +225,16 @@ __device__ __forceinline__ void build_tile(const BuildArgs &p, const Tile tl) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) eqv[i] = p.eq[(size_t)b * p.NQp + (qb0 + i) * 16 + ci] + p.eshift;
 
-    // LDS-DMA pieces of this wave: pc = w + 4 m -> patch row pc >> 1, half pc & 1
+    // LDS-DMA pieces of this wave: pc = w + 4 m -> patch block rp = pc >> 1 (tile row rp / 4, tile
+    // column rp % 4 of the patch), half pc & 1
+    const int TCp = 4 * p.CB;                           // tiles per row of the target image
     const size_t tstep = (size_t)p.Hp * p.CB * kRecU;  // u32x4 per K step of the target image
     const u32x4 *tsrc[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-        const int pc = w + 4 * m;
-        tsrc[m] = p.pt + (((size_t)b * S * p.Hp + y0 + (pc >> 1)) * p.CB + tl.cb) * kRecU + (pc & 1) * 64 + lane;
+        const int pc = w + 4 * m, rp = pc >> 1;
+        tsrc[m] = p.pt + (((size_t)b * S * (p.Hp >> 2) + (y0 >> 2) + (rp >> 2)) * TCp + 4 * tl.cb + (rp & 3)) * kRecU +
+                  (pc & 1) * 64 + lane;
     }
     const size_t qstep = (size_t)p.NQB * kRecU;
     const uint32_t lds_base = (uint32_t)(uintptr_t)(lds_void_t *)smem;
@@ -348,27 +354,28 @@ __device__ __forceinline__ void build_tile(const BuildArgs &p, const Tile tl) {
     }
 
     // ---- epilogue: exponents, 1/sqrt(D), level 0 from registers, levels 1-3 in registers ----
-    int et[kPatchRows][4];
+    // MFMA block r (patch tile (r / 4, r % 4)) leaves lane (grp, ci) with row grp of that tile for
+    // query ci: level 0 as whole 64-B tiles per store instruction, levels 1-3 pooled across lanes
+    // 16 / 32 apart — corr_build_bf16.hip's epilogue, which describes the lane roles.
+    const int h = grp >> 1, k = grp & 1;
+    int et[kPatchRows][4];  // exponents of patch cell (4 (r >> 2) + grp, 4 (r & 3) + g)
 #pragma unroll
     for (int r = 0; r < kPatchRows; ++r) {
-        const int4 e4 = reinterpret_cast<const int4 *>(lds_et)[r * 4 + grp];
+        const int4 e4 = reinterpret_cast<const int4 *>(lds_et)[(4 * (r >> 2) + grp) * 4 + (r & 3)];
         et[r][0] = e4.x, et[r][1] = e4.y, et[r][2] = e4.z, et[r][3] = e4.w;
     }
-    // Tiled pyramid (corr_common.h): levels 0-2 as 16-B tile rows, level 3 one cell per lane; a
-    // store runs whenever its tile row lies in the padded map (corr_build_bf16.hip's epilogue).
     const int H = p.H, W = p.W, NQ = p.NQ, nlev = p.nlev;
     const int H1 = H >> 1, W1 = W >> 1, H2 = H >> 2, W2 = W >> 2, H3 = H >> 3, W3 = W >> 3;
-    const int TW0 = map_tcols(W), TW1 = map_tcols(W1), TW2 = map_tcols(W2), TW3 = map_tcols(W3);
+    const int TC0 = map_tcols(W), TC1 = map_tcols(W1), TC2 = map_tcols(W2), TC3 = map_tcols(W3);
     const int R0 = 4 * map_tiles(H), R1 = 4 * map_tiles(H1), R2 = 4 * map_tiles(H2), R3 = 4 * map_tiles(H3);
     const size_t M0 = map_floats(H, W), M1 = map_floats(H1, W1), M2 = map_floats(H2, W2), M3 = map_floats(H3, W3);
-    const int X0 = x0 + 4 * grp;
-    float l2s[2][2];  // both blocks' level-2 values: their stores are merged below
+    float l2s[2][2];  // level 2 of both query blocks: (Y2 = h, X2 = 2k + j)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int q = (qb0 + i) * 16 + ci;
         const bool qok = q < NQ;
         const size_t qrow = (size_t)b * NQ + q;
-        float v[kPatchRows][4];
+        float v[kPatchRows][4];  // v[r][c]: patch cell (4 (r >> 2) + grp, 4 (r & 3) + c)
 #pragma unroll
         for (int r = 0; r < kPatchRows; ++r)
 #pragma unroll
@@ -377,66 +384,68 @@ __device__ __forceinline__ void build_tile(const BuildArgs &p, const Tile tl) {
                 if (!p.exact) x = x * p.inv_s;
                 v[r][g] = x;
             }
-        if (qok && nlev > 0 && X0 < W) {
+        if (qok && nlev > 0) {
             float *m0 = p.lvl[0] + qrow * M0;
 #pragma unroll
-            for (int r = 0; r < kPatchRows; ++r)
-                if (y0 + r < R0)
-                    *reinterpret_cast<float4 *>(m0 + map_row4(y0 + r, X0 >> 2, TW0)) = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
-        }
-        float l1[4][2];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            l1[r][0] = pool4(v[2 * r][0], v[2 * r][1], v[2 * r + 1][0], v[2 * r + 1][1]);
-            l1[r][1] = pool4(v[2 * r][2], v[2 * r][3], v[2 * r + 1][2], v[2 * r + 1][3]);
-        }
-        float l2[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) l2[r] = pool4(l1[2 * r][0], l1[2 * r][1], l1[2 * r + 1][0], l1[2 * r + 1][1]);
-        l2s[i][0] = l2[0], l2s[i][1] = l2[1];
-        {
-            // Level 1 as 16-B tile rows: lanes grp 2m and 2m + 1 hold level-1 columns x0/2 + 4m + {0,1}
-            // and {2,3} of the patch's 4 rows; they swap one row's pair (lanes 16 apart) so that the
-            // even lane stores rows 0, 2 and the odd lane rows 1, 3, 4 columns each.
-            const bool odd = grp & 1;
-            const int X1 = (x0 >> 1) + 4 * (grp >> 1);
-#pragma unroll
-            for (int rp = 0; rp < 2; ++rp) {
-                const int ra = 2 * rp, rb = ra + 1, r = odd ? rb : ra;
-                const float g0 = __shfl_xor(odd ? l1[ra][0] : l1[rb][0], 16);
-                const float g1 = __shfl_xor(odd ? l1[ra][1] : l1[rb][1], 16);
-                const float4 o = odd ? make_float4(g0, g1, l1[rb][0], l1[rb][1]) : make_float4(l1[ra][0], l1[ra][1], g0, g1);
-                if (qok && nlev > 1 && (y0 >> 1) + r < R1 && X1 < W1)
-                    *reinterpret_cast<float4 *>(p.lvl[1] + qrow * M1 + map_row4((y0 >> 1) + r, X1 >> 2, TW1)) = o;
+            for (int r = 0; r < kPatchRows; ++r) {
+                const int Y = y0 + 4 * (r >> 2) + grp, T = (x0 >> 2) + (r & 3);
+                if (Y < R0 && 4 * T < W)
+                    *reinterpret_cast<float4 *>(m0 + map_row4(Y, T, TC0)) = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
             }
         }
+        float l1[2][4];  // l1[tr][m]: level-1 cell (2 tr + h, 4k + m) of the patch
+#pragma unroll
+        for (int tr = 0; tr < 2; ++tr) {
+            float top[2][4], bot[2][4];  // rows 2h, 2h + 1 of tiles 4 tr + 2k + j
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float mine = k ? v[4 * tr + 2 + j][c] : v[4 * tr + j][c];
+                    const float give = k ? v[4 * tr + j][c] : v[4 * tr + 2 + j][c];
+                    const float got = __shfl_xor(give, 16);
+                    top[j][c] = k ? got : mine;
+                    bot[j][c] = k ? mine : got;
+                }
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int j = m >> 1, c = 2 * (m & 1);
+                l1[tr][m] = pool4(top[j][c], top[j][c + 1], bot[j][c], bot[j][c + 1]);
+            }
+            const int Y1 = (y0 >> 1) + 2 * tr + h, T1 = (x0 >> 3) + k;
+            if (qok && nlev > 1 && Y1 < R1 && 4 * T1 < W1)
+                *reinterpret_cast<float4 *>(p.lvl[1] + qrow * M1 + map_row4(Y1, T1, TC1)) =
+                    make_float4(l1[tr][0], l1[tr][1], l1[tr][2], l1[tr][3]);
+        }
+        // level 2 (Y2 = h, X2 = 2k + j): level-1 rows 2h (lane (0, k), tr = h) and 2h + 1 (lane (1, k))
+        float top[4], bot[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const float give = h ? l1[0][m] : l1[1][m];
+            const float got = __shfl_xor(give, 32);
+            top[m] = h ? got : l1[0][m];
+            bot[m] = h ? l1[1][m] : got;
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) l2s[i][j] = pool4(top[2 * j], top[2 * j + 1], bot[2 * j], bot[2 * j + 1]);
     }
-    // Levels 2 and 3 of BOTH query blocks in one store instruction each.  An xor exchange has one
-    // receiver per sender, so every sender sends what its receiver's block needs.
     {
-        // Level 2: lanes grp 0..3 hold columns x0/4 + grp of 2 rows per block; lane g gathers row
-        // g & 1 of block g >> 1 (exchanges with lanes 16, 32, 48 apart), one 16-B tile row per lane.
-        const int bl = grp >> 1, rw = grp & 1;
-        // value k = 2 * block + row of this lane, by selects (a dynamic register index goes to scratch)
-        auto sel = [&](int k) { return k == 0 ? l2s[0][0] : k == 1 ? l2s[0][1] : k == 2 ? l2s[1][0] : l2s[1][1]; };
-        const float t0 = sel(grp);
-        const float t1 = __shfl_xor(sel(grp ^ 1), 16), t2 = __shfl_xor(sel(grp ^ 2), 32), t3 = __shfl_xor(sel(grp ^ 3), 48);
-        // t_d is column grp ^ d of the wanted row, so component c (column c) is t_(c ^ grp)
-        auto pick = [&](int k) { return k == 0 ? t0 : k == 1 ? t1 : k == 2 ? t2 : t3; };
-        const float4 o = make_float4(pick(grp), pick(grp ^ 1), pick(grp ^ 2), pick(grp ^ 3));
-        const int q = (qb0 + bl) * 16 + ci;
-        if (q < NQ && nlev > 2 && (y0 >> 2) + rw < R2 && (x0 >> 2) < W2)
-            *reinterpret_cast<float4 *>(p.lvl[2] + ((size_t)b * NQ + q) * M2 + map_row4((y0 >> 2) + rw, x0 >> 4, TW2)) = o;
+        // Level 2 rows of BOTH blocks, one 16-B store per lane: lane (h, k) stores row h of block k;
+        // lanes (h, 0), (h, 1) hold columns 0-1 / 2-3 and trade the other block's pair.
+        const float g0 = __shfl_xor(k ? l2s[0][0] : l2s[1][0], 16), g1 = __shfl_xor(k ? l2s[0][1] : l2s[1][1], 16);
+        const float o0 = k ? l2s[1][0] : l2s[0][0], o1 = k ? l2s[1][1] : l2s[0][1];
+        const float4 o = k ? make_float4(g0, g1, o0, o1) : make_float4(o0, o1, g0, g1);
+        const int q = (qb0 + k) * 16 + ci, Y2 = (y0 >> 2) + h;
+        if (q < NQ && nlev > 2 && Y2 < R2 && (x0 >> 2) < W2)
+            *reinterpret_cast<float4 *>(p.lvl[2] + ((size_t)b * NQ + q) * M2 + map_row4(Y2, x0 >> 4, TC2)) = o;
     }
     {
-        // Level 3: the 2x2 window of level-2 values (a row pair in one lane, the column pair in the
-        // lanes 16 apart); even lanes pool block 0, odd lanes block 1, in ((a + b) + c) + d order.
-        const int bl = grp & 1;
-        const float y0v = __shfl_xor(bl ? l2s[0][0] : l2s[1][0], 16), y1v = __shfl_xor(bl ? l2s[0][1] : l2s[1][1], 16);
-        const float l3 = bl == 0 ? pool4(l2s[0][0], y0v, l2s[0][1], y1v) : pool4(y0v, l2s[1][0], y1v, l2s[1][1]);
-        const int q = (qb0 + bl) * 16 + ci;
-        const int Y3 = y0 >> 3, X3 = X0 >> 3;
-        if (q < NQ && nlev > 3 && Y3 < R3 && X3 < kTileW * TW3) p.lvl[3][((size_t)b * NQ + q) * M3 + map_cell(Y3, X3, TW3)] = l3;
+        // Level 3, cell X3 = k of block h: level-2 rows 0 (lanes (0, k)) and 1 (lanes (1, k)).
+        const float g0 = __shfl_xor(h ? l2s[0][0] : l2s[1][0], 32), g1 = __shfl_xor(h ? l2s[0][1] : l2s[1][1], 32);
+        const float l3 = h ? pool4(g0, g1, l2s[1][0], l2s[1][1]) : pool4(l2s[0][0], l2s[0][1], g0, g1);
+        const int q = (qb0 + h) * 16 + ci;
+        const int Y3 = y0 >> 3, X3 = (x0 >> 3) + k;
+        if (q < NQ && nlev > 3 && Y3 < R3 && X3 < kTileW * TC3) p.lvl[3][((size_t)b * NQ + q) * M3 + map_cell(Y3, X3, TC3)] = l3;
     }
 }
 
