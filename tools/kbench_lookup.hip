@@ -123,6 +123,10 @@ int main(int argc, char **argv) {
         vs.push_back({"prod grid (integer)", [=](float *o) { return launch_lookup(lp, coords_g, B, H * W, H, W, 4, 4, o, 0); }, {}});
         vs.push_back({"QB16 smooth-flow", [=](float *o) { return launch_qb<16>(lp, coords_s, B, H, W, o); }, {}});
         vs.push_back({"abl QB32 noload", [=](float *o) { return launch_qb<32, 1>(lp, coords, B, H, W, o); }, {}});
+        vs.push_back({"abl QB32 nostore", [=](float *o) { return launch_qb<32, 2>(lp, coords, B, H, W, o); }, {}});
+        vs.push_back({"abl QB32 nocoords", [=](float *o) { return launch_qb<32, 4>(lp, coords, B, H, W, o); }, {}});
+        vs.push_back({"abl QB32 noload nostore", [=](float *o) { return launch_qb<32, 3>(lp, coords, B, H, W, o); }, {}});
+        vs.push_back({"abl QB32 none (taps only)", [=](float *o) { return launch_qb<32, 7>(lp, coords, B, H, W, o); }, {}});
         vs.push_back({"QB16 cached-stores", [=](float *o) { return launch_qb<16, 8>(lp, coords, B, H, W, o); }, {}});
         vs.push_back({"QB32 cached-stores", [=](float *o) { return launch_qb<32, 8>(lp, coords, B, H, W, o); }, {}});
         CK(vs[0].launch(ref));
