@@ -87,7 +87,7 @@ using namespace corr;
 
 extern "C" {
 
-int corr_version(void) { return 200; }
+int corr_version(void) { return 201; }
 
 const char *corr_last_error(void) { return g_err; }
 
@@ -347,7 +347,7 @@ int corr_pool_fold(float *const *grad_pyr, int B, int NQ, int H, int W, int leve
 
 size_t corr_backward_workspace(int algo, int B, int D, int NQ, int H, int W, int radius) {
     if (B < 1 || D < 1 || NQ < 1 || H < 1 || W < 1 || radius < 0) return 0;
-    return backward_workspace(algo, B, D, NQ, H, W, radius);
+    return backward_workspace(algo & ~CORR_BACKWARD_EXACT_FOLD, B, D, NQ, H, W, radius);
 }
 
 int corr_backward(int algo, const float *const *coords_rows, const float *const *grad_out_rows, int T,
@@ -356,7 +356,8 @@ int corr_backward(int algo, const float *const *coords_rows, const float *const 
                   size_t workspace_bytes, void *stream) {
     static const char *fn = "corr_backward";
     g_err[0] = 0;
-    if (algo != CORR_BUILD_FP32 && algo != CORR_BUILD_F16X3 && algo != CORR_BUILD_BF16X6)
+    const int base = algo & ~CORR_BACKWARD_EXACT_FOLD;
+    if (base != CORR_BUILD_FP32 && base != CORR_BUILD_F16X3 && base != CORR_BUILD_BF16X6)
         return fail(CORR_EUNSUPPORTED, "%s: unknown algorithm %d", fn, algo);
     int rc = check_dims(fn, B, NQ, H, W, levels);
     if (rc || (rc = check_radius(fn, radius))) return rc;
@@ -369,7 +370,7 @@ int corr_backward(int algo, const float *const *coords_rows, const float *const 
     if ((rc = check_ptr(fn, fmap1_rows, "fmap1")) || (rc = check_ptr(fn, fmap2, "fmap2")) ||
         (rc = check_ptr(fn, dfmap1_rows, "dfmap1")) || (rc = check_ptr(fn, dfmap2, "dfmap2")))
         return rc;
-    const size_t need = corr_backward_workspace(algo, B, D, NQ, H, W, radius);
+    const size_t need = corr_backward_workspace(base, B, D, NQ, H, W, radius);
     if (workspace_bytes < need || (need && !workspace))
         return fail(CORR_EINVAL, "%s: workspace of %zu bytes needed, got %zu", fn, need, workspace_bytes);
     LevelPtrs lp{};

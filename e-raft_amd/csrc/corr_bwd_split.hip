@@ -1225,6 +1225,8 @@ hipError_t launch_pool_fold(const LevelPtrs &gpyr, int B, int NQ, int H, int W, 
 hipError_t launch_backward(int algo, const float *const *coords, const float *const *grad_out, int T,
                            const float *f1, int NQ, const float *f2, int B, int D, int H, int W, int levels, int radius,
                            const LevelPtrs &gpyr, float *df1, float *df2, void *ws, hipStream_t s) {
+    const bool exact = (algo & CORR_BACKWARD_EXACT_FOLD) != 0;
+    algo &= ~CORR_BACKWARD_EXACT_FOLD;
     hipError_t e;
     {  // fused: all lookups + the fold in one launch, dC and its row maxima straight out of LDS,
        // the column maxima as per-workgroup partials reduced by colmax_reduce_kernel
@@ -1249,7 +1251,7 @@ hipError_t launch_backward(int algo, const float *const *coords, const float *co
             rm.rows = D;
         }
         e = launch_lookup_bwd_fold(coords, grad_out, T, B, NQ, H, W, levels, radius, gpyr.p[0], rmax, cmax, cpart, s,
-                                   rm);
+                                   rm, exact);
         if (e == hipSuccess) {
             if (algo == CORR_BUILD_BF16X6)
                 return bwd_split_gemms(gpyr.p[0], f1, NQ, f2, B, D, H, W, df1, df2, carve(ws, B, D, NQ, N), s, true,

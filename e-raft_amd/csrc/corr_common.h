@@ -79,9 +79,12 @@ struct FoldRowMax {
     int cols[2];
     int rows;  // 0: none
 };
+// exact: regular windows replay grid_sampler_2d_backward's per-tap products bit for bit (else the
+// separable closed form at radius 4, corr_backward's default).
 hipError_t launch_lookup_bwd_fold(const float *const *coords, const float *const *grad_out, int T, int B, int NQ,
                                   int H, int W, int levels, int radius, float *dc, unsigned *rmax, unsigned *cmax,
-                                  float *cpart, hipStream_t s, const FoldRowMax &rm = FoldRowMax{});
+                                  float *cpart, hipStream_t s, const FoldRowMax &rm = FoldRowMax{},
+                                  bool exact = true);
 size_t backward_workspace(int algo, int B, int D, int NQ, int H, int W, int radius);
 hipError_t launch_pool_fold(const LevelPtrs &gpyr, int B, int NQ, int H, int W, int levels, void *ws, int D,
                             hipStream_t s);

@@ -1272,7 +1272,9 @@ __device__ __forceinline__ void kernarg_lookup(int t, const float *&c, const flo
 // PROBE (measurement builds only, tools/kbench_bwd.hip; the library uses 0): bit 0 = no lookup
 // loop, bit 1 = no fold (no dC / maxima), bit 2 = no LDS zero-init (wrong results, timing only),
 // bit 3 = plain (L2-cached) dC stores instead of the non-temporal ones.
-template <int S, int PROBE = 0>
+// SEP: regular windows by the separable closed form (corr_backward's default); false replays
+// grid_sampler_2d_backward's per-tap products bit for bit (CORR_BACKWARD_EXACT_FOLD).
+template <int S, int PROBE = 0, bool SEP = false>
 __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLookups lk, FusedOut o) {
     using ST = FusedStage<S>;
     constexpr int R = (S - 1) / 2, K = S * S, C = S + 1, WIN = ST::WIN;
@@ -1395,6 +1397,25 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
             auto gcv = [&](int j) { return j >= 0 && j < S ? v[j] : 0.f; };
             const f32x2 WH = f32x2{whi, whi}, WL = f32x2{wlo, wlo};
             float sv[C + 1];
+            if constexpr (SEP) {
+                // separable (the default): the column's two x-taps first, hx[j] = g(cx - 1, j) whi +
+                // g(cx, j) wlo for each y-tap j, then the y-taps, cell cy = hx[cy - 1] yhi[cy - 1] +
+                // hx[cy] ylo[cy] — the same four (tap, corner) terms with the same per-tap weights,
+                // rounded in another order (~1e-7 relative; tests/test_gpu_parity.py), for ~30
+                // instead of ~70 VALU per lane
+                float hx[S];
+#pragma unroll
+                for (int j = 0; j + 1 < S; j += 2) {
+                    const f32x2 h = __builtin_elementwise_fma(f32x2{v[j], v[j + 1]}, WL, f32x2{gpr[j], gpr[j + 1]} * WH);
+                    hx[j] = h.x, hx[j + 1] = h.y;
+                }
+                if constexpr ((S & 1) != 0) hx[S - 1] = __builtin_fmaf(v[S - 1], wlo, gpr[S - 1] * whi);
+#pragma unroll
+                for (int cy = 0; cy < C; ++cy) {
+                    const float up = cy >= 1 ? hx[cy - 1] * yhi_[cy - 1] : 0.f;
+                    sv[cy] = cy < S ? __builtin_fmaf(hx[cy], ylo_[cy], up) : up;
+                }
+            } else
 #pragma unroll
             for (int cy = 0; cy < C; cy += 2) {  // cells cy, cy + 1; se / sw use y-tap cy - 1, ne / nw cy
                 const f32x2 yhi = f32x2{yv(2, cy - 1), yv(2, cy)}, ylo = f32x2{yv(1, cy), yv(1, cy + 1)};
@@ -1861,7 +1882,7 @@ size_t fused_lds_bytes(int H, int W, int levels, FusedOut *o) {
     return (maps + (size_t)kFusedLv * ST::SIZE + ST::BQ) * 4;
 }
 
-template <int S>
+template <int S, bool SEP = false>
 hipError_t launch_fused_s(const BwdLookups &lk, FusedOut o, hipStream_t s) {
     const size_t bytes = fused_lds_bytes<S>(o.H, o.W, o.L, &o);
     // the dynamic-LDS limit is raised once per device to the largest image this path accepts
@@ -1874,7 +1895,7 @@ hipError_t launch_fused_s(const BwdLookups &lk, FusedOut o, hipStream_t s) {
     const int limit = std::min(160 * 1024, dev_max);
     if (bytes > (size_t)limit) return hipErrorNotSupported;
     static std::atomic<unsigned long long> done{0};
-    e = ensure_lds_limit((const void *)lookup_bwd_fold_kernel<S>, limit, done);
+    e = ensure_lds_limit((const void *)lookup_bwd_fold_kernel<S, 0, SEP>, limit, done);
     if (e != hipSuccess) return e;
     const int nqb = (o.NQ + FusedStage<S>::BQ - 1) / FusedStage<S>::BQ;
     o.nfold = nqb * o.B;
@@ -1886,7 +1907,7 @@ hipError_t launch_fused_s(const BwdLookups &lk, FusedOut o, hipStream_t s) {
         o.rm_rows_per_wave = (int)std::max(1L, (rows + cap * kFusedLv - 1) / (cap * kFusedLv));
         extra = (int)((rows + (long)o.rm_rows_per_wave * kFusedLv - 1) / ((long)o.rm_rows_per_wave * kFusedLv));
     }
-    hipLaunchKernelGGL(lookup_bwd_fold_kernel<S>, dim3((unsigned)(o.nfold + extra)), dim3(64 * kFusedLv), bytes, s,
+    hipLaunchKernelGGL((lookup_bwd_fold_kernel<S, 0, SEP>), dim3((unsigned)(o.nfold + extra)), dim3(64 * kFusedLv), bytes, s,
                        lk, o);
     return hipGetLastError();
 }
@@ -1900,7 +1921,7 @@ int lookup_bwd_fold_groups(int NQ, int radius) {
 
 hipError_t launch_lookup_bwd_fold(const float *const *coords, const float *const *grad_out, int T, int B, int NQ,
                                   int H, int W, int levels, int radius, float *dc, unsigned *rmax, unsigned *cmax,
-                                  float *cpart, hipStream_t s, const FoldRowMax &rm) {
+                                  float *cpart, hipStream_t s, const FoldRowMax &rm, bool exact) {
     if (T < 1 || T > kMaxLookups || levels < 1 || levels > kFusedLv) return hipErrorNotSupported;
     BwdLookups lk{};
     lk.T = T;
@@ -1917,7 +1938,8 @@ hipError_t launch_lookup_bwd_fold(const float *const *coords, const float *const
         case 1: return launch_fused_s<3>(lk, o, s);
         case 2: return launch_fused_s<5>(lk, o, s);
         case 3: return launch_fused_s<7>(lk, o, s);
-        case 4: return launch_fused_s<9>(lk, o, s);
+        // the separable closed form is instantiated for E-RAFT's radius only
+        case 4: return exact ? launch_fused_s<9, false>(lk, o, s) : launch_fused_s<9, true>(lk, o, s);
         case 5: return launch_fused_s<11>(lk, o, s);
         case 6: return launch_fused_s<13>(lk, o, s);
         case 7: return launch_fused_s<15>(lk, o, s);

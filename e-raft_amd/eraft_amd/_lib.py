@@ -32,7 +32,7 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
            "corr_backward", "corr_convex_upsample_bwd_workspace", "corr_convex_upsample_bwd", "corr_build_region",
            "corr_lookup_conv_bwd_workspace", "corr_lookup_conv_bwd", "corr_map_floats", "corr_pyramid_export",
            "corr_pyramid_import")
-ABI_VERSION = 200  # include/corr_mi355x.h: the tiled value pyramid
+ABI_VERSION = 201  # include/corr_mi355x.h: the tiled value pyramid; separable fold by default
 
 # Build algorithms (include/corr_mi355x.h).  BF16X6 is the default: every fp32 feature split
 # exactly into three bf16 pieces, the six largest piece products on the bf16 MFMA, fp32
@@ -44,6 +44,7 @@ BUILD_F16X3 = 1
 BUILD_BF16X6 = 2
 BUILD_ONLY_PACK = 0x100  # measurement: OR into BUILD_F16X3 / _BF16X6 to run only the operand pack
 BUILD_ONLY_MFMA = 0x200  # ... or only the MFMA kernel (the workspace holds this pair's pack)
+BACKWARD_EXACT_FOLD = 0x400  # OR into corr_backward's algo: the bit-exact fold (exact_fold())
 _ALGOS = {"fp32": BUILD_FP32, "f16x3": BUILD_F16X3, "bf16x6": BUILD_BF16X6}
 
 
@@ -329,15 +330,26 @@ def pool_fold(grad_levels, B, H, W):
                                      _stream(grad_levels[0])))
 
 
-def backward(coords_list, grad_list, radius, grad_levels, fmap1, fmap2, algo=None):
+def exact_fold() -> bool:
+    """ERAFT_AMD_EXACT_FOLD=1: corr_backward's fused fold replays grid_sampler_2d_backward's
+    per-tap products bit for bit (CORR_BACKWARD_EXACT_FOLD) instead of the separable closed form
+    (dC within ~1e-7 of the staged path, the default)."""
+    return os.environ.get("ERAFT_AMD_EXACT_FOLD", "1") == "1"
+
+
+def backward(coords_list, grad_list, radius, grad_levels, fmap1, fmap2, algo=None, exact=None):
     """corr_backward: (dfmap1, dfmap2) of one build and its lookups (all at once, in order).
     grad_levels: scratch gradient pyramid (overwritten; level 0 ends as dLoss/dcorr).
-    algo: the GEMMs' algorithm (default: backward_algo())."""
+    algo: the GEMMs' algorithm (default: backward_algo()); exact: the bit-exact fold (default:
+    exact_fold())."""
     algo = backward_algo() if algo is None else algo
+    exact = exact_fold() if exact is None else exact
     B, D, H, W = fmap2.shape
     lib = load()
     NQ = _nq(fmap1)
     ws_bytes = lib.corr_backward_workspace(algo, B, D, NQ, H, W, radius)
+    if exact:
+        algo |= BACKWARD_EXACT_FOLD
     if ws_bytes == ctypes.c_size_t(-1).value:
         raise CorrError(CORR_EUNSUPPORTED, f"unknown backward algorithm {algo}")
     df1 = torch.empty_like(fmap1)

@@ -58,7 +58,9 @@ extern "C" {
  *        bf16 split); E-RAFT's default backward for the BF16X6 build.
  *   200: the value pyramid (the builds' output, the lookups' input) is TILED (see Layouts;
  *        16-B aligned levels, corr_map_floats per map); corr_map_floats, corr_pyramid_export,
- *        corr_pyramid_import.  Gradient pyramids keep the reference layout. */
+ *        corr_pyramid_import.  Gradient pyramids keep the reference layout.
+ *   201: corr_backward's fused fold takes the separable closed form by default (dC within ~1e-7
+ *        of the staged path, not bitwise); CORR_BACKWARD_EXACT_FOLD restores the bit-exact replay. */
 int corr_version(void);
 
 /* Thread-local description of the last error on this thread ("" if none). */
@@ -252,9 +254,15 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
  *     every level in 160 KiB: e.g. r = 4 up to 60x80 fmaps), the lookups and the fold run as ONE
  *     kernel whose gradient maps live in LDS and which writes only dC (plus dC's row maxima and
  *     per-workgroup column maxima for the F16X3 packs; BF16X6 needs none); otherwise corr_lookup_bwd_multi +
- *     corr_pool_fold.  Both give the same bits.  Workspace: corr_backward_workspace (radius
- *     sizes the column-maxima partials).
+ *     corr_pool_fold.  At radius 4 the fused kernel sums a regular window's cells separably (the
+ *     column's two x-taps first, then the y-taps: the same four (tap, corner) terms per cell with
+ *     the reference's per-tap weights, rounded in another order — dC within ~1e-7 norm-relative of
+ *     the staged path); algo | CORR_BACKWARD_EXACT_FOLD makes it replay grid_sampler_2d_backward's
+ *     per-tap products instead, bit-identical to corr_lookup_bwd_multi + corr_pool_fold (as every
+ *     other radius and the non-fused path always are).  Workspace: corr_backward_workspace
+ *     (radius sizes the column-maxima partials; the flag does not change it).
  */
+#define CORR_BACKWARD_EXACT_FOLD 0x400
 int corr_lookup_bwd_multi(const float *const *coords_rows, const float *const *grad_out_rows, int T, int B,
                           int NQ, int H, int W, int levels, int radius, float *const *grad_pyr, void *stream);
 int corr_pool_fold(float *const *grad_pyr, int B, int NQ, int H, int W, int levels, void *stream);

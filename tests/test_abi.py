@@ -35,7 +35,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 
 def test_version_and_workspace(lib):
-    assert lib.corr_version() == 200
+    assert lib.corr_version() == 201
     # DSEC: 256 x 4800 slabs; at least one slab, deterministic plan
     ws = lib.corr_build_bwd_workspace(1, 256, 60, 80)
     assert ws >= 256 * 4800 * 4 and ws % (256 * 4800 * 4) == 0
@@ -150,12 +150,17 @@ def test_backward_workspace_and_validation(lib):
     assert lib.corr_backward_workspace(2, B, D, N, H, W, r) == lib.corr_build_bwd_ex_workspace(2, B, D, N, H, W)
     assert lib.corr_backward_workspace(2, B, D, N, H, W, r) < ws
     assert lib.corr_build_bwd_ex_workspace(3, B, D, N, H, W) == ctypes.c_size_t(-1).value
+    # CORR_BACKWARD_EXACT_FOLD (0x400) selects the fold's arithmetic only: same workspace
+    for a in (0, 1, 2):
+        assert lib.corr_backward_workspace(a | 0x400, B, D, N, H, W, r) == lib.corr_backward_workspace(a, B, D, N, H, W, r)
     ptrs = (ctypes.c_void_p * 1)(16)
     gp = (ctypes.c_void_p * 4)(16, 16, 16, 16)
     rc = lib.corr_backward(1, ptrs, ptrs, 1, 16, N, 16, B, D, H, W, 4, r, gp, 16, 16, 16, 4, None)
     assert rc == -1 and "workspace" in lib.corr_last_error().decode()
     rc = lib.corr_backward(1, ptrs, ptrs, 1, None, N, 16, B, D, H, W, 4, r, gp, 16, 16, 16, ws, None)
     assert rc == -1
+    rc = lib.corr_backward(3 | 0x400, ptrs, ptrs, 1, 16, N, 16, B, D, H, W, 4, r, gp, 16, 16, 16, ws, None)
+    assert rc == -2 and "unknown algorithm" in lib.corr_last_error().decode()
 
 
 def test_lookup_conv_validation(lib):

@@ -667,15 +667,19 @@ def test_lookup_bwd_multi_and_fold_bitexact(T, B, H, W, L, r):
     assert bit_equal(got[0].cpu().numpy(), ref[0].cpu().numpy())
 
 
+@pytest.mark.parametrize("exact", [True, False])
 @pytest.mark.parametrize("algo", ["bf16x6", "f16x3", "fp32"])
 @pytest.mark.parametrize("B,D,H,W,L,r,T", [(2, 32, 18, 24, 4, 4, 5), (1, 20, 17, 23, 3, 3, 2), (8, 64, 36, 48, 4, 4, 12),
                                            (1, 16, 12, 16, 4, 4, 33), (1, 16, 60, 80, 4, 4, 3),
                                            (1, 16, 64, 96, 5, 2, 2), (1, 8, 120, 160, 4, 4, 2)])
-def test_corr_backward_matches_staged_path(algo, B, D, H, W, L, r, T):
-    """corr_backward is bit-identical to the staged path (lookup_bwd per lookup, pool_bwd,
-    build_bwd with its own absmax).  Covers the fused LDS-resident kernel at workgroup sizes
-    8 (18x24, 36x48), 4 (60x80), 1 (120x160) queries, and the multi-lookup + fold fallback
-    (33 lookups > one launch's table; 5 levels)."""
+def test_corr_backward_matches_staged_path(algo, B, D, H, W, L, r, T, exact):
+    """corr_backward against the staged path (lookup_bwd per lookup, pool_bwd, build_bwd with its
+    own absmax).  Covers the fused LDS-resident kernel at workgroup sizes 8 (18x24, 36x48), 4
+    (60x80), 1 (120x160) queries, and the multi-lookup + fold fallback (33 lookups > one launch's
+    table; 5 levels).  exact (CORR_BACKWARD_EXACT_FOLD): bit-identical.  Default: the fused fold's
+    separable closed form at r = 4 (the same per-tap weights, another rounding order): dC within
+    1e-6 norm-relative of the staged path (the verdict's bar; seen ~1e-7) and dfmap1 / dfmap2
+    within 1e-6; the other radii and the fallback stay bit-identical."""
     from eraft_amd import _lib
     from eraft_amd.corr import _alloc_grad_pyramid
     f1 = torch.from_numpy(prng.gauss(61, (B, D, H, W))).to(DEV)
@@ -687,10 +691,16 @@ def test_corr_backward_matches_staged_path(algo, B, D, H, W, L, r, T):
     _lib.pool_bwd(ref, H, W)
     r1, r2 = _lib.build_bwd(ref[0].reshape(B * H * W, H * W), f1, f2, _lib._ALGOS[algo])
     got = _alloc_grad_pyramid(B, H, W, L, f1)
-    g1, g2 = _lib.backward(cs, gs, r, got, f1, f2, _lib._ALGOS[algo])
-    assert bit_equal(got[0].cpu().numpy(), ref[0].cpu().numpy())
-    assert bit_equal(g1.cpu().numpy(), r1.cpu().numpy())
-    assert bit_equal(g2.cpu().numpy(), r2.cpu().numpy())
+    g1, g2 = _lib.backward(cs, gs, r, got, f1, f2, _lib._ALGOS[algo], exact=exact)
+    pairs = ((got[0], ref[0]), (g1, r1), (g2, r2))
+    if exact or r != 4 or T > 32 or L > 4:
+        for a, b in pairs:
+            assert bit_equal(a.cpu().numpy(), b.cpu().numpy())
+    else:
+        for k, (a, b) in enumerate(pairs):
+            e = norm_rel(a.cpu().numpy(), b.cpu().numpy())
+            print(f"{'dC dF1 dF2'.split()[k]}: {e:.2e}")
+            assert e <= 1e-6, (k, e)
 
 
 def test_lookup_only_loss_runs_one_backward_call(monkeypatch):
@@ -717,13 +727,38 @@ def test_lookup_only_loss_runs_one_backward_call(monkeypatch):
     assert t1.grad is not None and t2.grad is not None
 
 
+def test_autograd_separable_fold_close_to_per_lookup(monkeypatch):
+    """CorrBlock autograd with the default fused fold (separable closed form) against the
+    per-lookup path (ERAFT_AMD_FUSED_BWD=0, the reference's scatter order): fmap gradients within
+    1e-6 norm-relative at the train shape's width (36x48, 12 lookups, the first on the integer
+    grid as at a cold start)."""
+    B, D, H, W, L, r, T = 2, 64, 36, 48, 4, 4, 12
+    f1n, f2n = prng.gauss(73, (B, D, H, W)), prng.gauss(74, (B, D, H, W))
+    cs, gs = _bwd_case(T, B, H, W, L, r, 910)
+    res = {}
+    monkeypatch.setenv("ERAFT_AMD_EXACT_FOLD", "0")
+    for mode in ("1", "0"):
+        monkeypatch.setenv("ERAFT_AMD_FUSED_BWD", mode)
+        t1 = torch.from_numpy(f1n).to(DEV).requires_grad_(True)
+        t2 = torch.from_numpy(f2n).to(DEV).requires_grad_(True)
+        cb = _cb()(t1, t2, L, r)
+        sum((cb(c) * g).sum() for c, g in zip(cs, gs)).backward()
+        res[mode] = (t1.grad.cpu().numpy(), t2.grad.cpu().numpy())
+    for k, (a, b) in enumerate(zip(res["1"], res["0"])):
+        e = norm_rel(a, b)
+        print(f"dF{k + 1}: {e:.2e}")
+        assert e <= 1e-6, (k, e)
+
+
 def test_autograd_fused_backward_equals_per_lookup(monkeypatch):
-    """CorrBlock autograd: the stash + corr_backward path and ERAFT_AMD_FUSED_BWD=0's per-lookup
-    path give bit-identical fmap gradients, also when a direct pyramid gradient is present."""
+    """CorrBlock autograd: the stash + corr_backward path with the bit-exact fold
+    (ERAFT_AMD_EXACT_FOLD=1) and ERAFT_AMD_FUSED_BWD=0's per-lookup path give bit-identical fmap
+    gradients, also when a direct pyramid gradient is present."""
     B, D, H, W, L, r = 2, 32, 24, 32, 4, 4
     f1n, f2n = prng.gauss(71, (B, D, H, W)), prng.gauss(72, (B, D, H, W))
     cs, gs = _bwd_case(6, B, H, W, L, r, 900)
     res = {}
+    monkeypatch.setenv("ERAFT_AMD_EXACT_FOLD", "1")  # the fused fold's bit-exact replay
     for mode in ("1", "0"):
         for direct in (False, True):
             monkeypatch.setenv("ERAFT_AMD_FUSED_BWD", mode)
