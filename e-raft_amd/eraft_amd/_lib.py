@@ -334,7 +334,7 @@ def exact_fold() -> bool:
     """ERAFT_AMD_EXACT_FOLD=1: corr_backward's fused fold replays grid_sampler_2d_backward's
     per-tap products bit for bit (CORR_BACKWARD_EXACT_FOLD) instead of the separable closed form
     (dC within ~1e-7 of the staged path, the default)."""
-    return os.environ.get("ERAFT_AMD_EXACT_FOLD", "1") == "1"
+    return os.environ.get("ERAFT_AMD_EXACT_FOLD", "0") == "1"
 
 
 def backward(coords_list, grad_list, radius, grad_levels, fmap1, fmap2, algo=None, exact=None):
