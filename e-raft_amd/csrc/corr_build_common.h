@@ -119,9 +119,11 @@ __device__ __forceinline__ unsigned rn_pair(float a, float b, float &ha, float &
 }
 
 // Split a pair of fp32 features into packed bf16 (hi, mid, lo) pairs, x = hi + mid + lo exactly.
-// Guards: an infinite feature keeps hi = x and mid = lo = 0 (its products are x * the other
-// operand, as in fp32); a finite feature whose hi rounds up past the bf16 range (|x| within
-// 2^-9 of FLT_MAX) takes the truncated hi instead.  NaN propagates through hi.
+// Guards: an infinite feature keeps hi = x and mid = lo = 0 (its hi*hi product is x * hi of the
+// other operand; its products with the other operand's zero mid / lo pieces are NaN, which the
+// consumers' split_sum discards when the hi*hi sum is infinite, corr_common.h); a finite feature
+// whose hi rounds up past the bf16 range (|x| within 2^-9 of FLT_MAX) takes the truncated hi
+// instead.  NaN propagates through hi.
 __device__ __forceinline__ void split3(float a, float b, unsigned &hi, unsigned &mid, unsigned &lo) {
     float ha, hb;
     hi = rn_pair(a, b, ha, hb);

@@ -333,8 +333,9 @@ __device__ __forceinline__ void split2(float x0, float x1, int s, bool guard, ha
 // rounds to a finite bf16), mid = bf16_rn(x - hi), lo = x - hi - mid.  Finite x: x - hi is exact
 // (same binade, or |x| <= 2^-126 ... ), and so is the last difference, so x = hi + mid + lo bit for
 // bit — the same pieces as split3 wherever hi does not overflow; past M, hi = the bf16 maximum
-// and the residual carries the rest (split3 truncates there instead).  inf / NaN give non-finite
-// pieces, so every product with them is non-finite, as in fp32.
+// and the residual carries the rest (split3 truncates there instead).  An infinite element
+// splits as (the clamped hi, inf, NaN), so every output it reaches is NaN where an fp32 GEMM
+// gives +-inf (documented with corr_build_bwd_ex; one accumulator cannot tell them apart).
 __device__ __forceinline__ void split3_bwd(float a, float b, unsigned &hi, unsigned &mid, unsigned &lo) {
     constexpr float M = 3.3961775e38f;  // 0x7F7F7FFF
     float ha, hb, ma, mb, da, db;

@@ -461,6 +461,31 @@ def test_build_bwd_bf16x6_not_narrower_than_fp32(case):
         assert rb.max() <= r32.max() and rb.mean() <= r32.mean()
 
 
+def test_build_bwd_bf16x6_inf_gives_nan():
+    """The documented non-finite behaviour of the bf16x6 backward GEMMs (include/corr_mi355x.h,
+    corr_build_bwd_ex): an infinite dC element makes exactly the outputs it reaches NaN (dF1
+    column of its query row, dF2 column of its target), where fp32 gives +-inf; every other output
+    is finite and matches the fp32-operand GEMMs within 1e-6 of the scale."""
+    from eraft_amd import _lib
+    B, D, H, W = 1, 32, 8, 12
+    N = H * W
+    f1, f2 = prng.gauss(181, (B, D, H, W)), prng.gauss(182, (B, D, H, W))
+    gc = prng.gauss(183, (B * N, N))
+    gc[5, 17] = np.inf
+    tg, t1, t2 = (torch.from_numpy(x).to(DEV) for x in (gc, f1, f2))
+    d1, d2 = (g.cpu().numpy().reshape(B, D, N) for g in _lib.build_bwd(tg, t1, t2, _lib.BUILD_BF16X6))
+    e1, e2 = (g.cpu().numpy().reshape(B, D, N) for g in _lib.build_bwd(tg, t1, t2, _lib.BUILD_FP32))
+    nan1 = np.zeros_like(d1, bool)
+    nan1[0, :, 5] = True
+    nan2 = np.zeros_like(d2, bool)
+    nan2[0, :, 17] = True
+    assert np.array_equal(np.isnan(d1), nan1) and np.array_equal(np.isnan(d2), nan2)
+    assert np.isinf(e1[nan1]).all() and np.isinf(e2[nan2]).all()  # fp32: +-inf there
+    for a, b in ((d1, e1), (d2, e2)):
+        ok = np.isfinite(b)
+        assert np.abs(a[ok] - b[ok]).max() <= 1e-6 * np.abs(b[ok]).max()
+
+
 def _bf16_to_f32(u16):
     return (u16.astype(np.uint32) << 16).view(np.float32)
 
