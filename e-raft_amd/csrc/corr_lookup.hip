@@ -1356,9 +1356,24 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         const bool far = ax == kFarAnchor || ay == kFarAnchor;
         const bool unc = qok && !window_covers<S>(fx0, group_lane<SLOTS, S - 1>(a.f, lane), fy0,
                                                   group_lane<SLOTS, S - 1>(c.f, lane));
+        // irregular groups take the range form — or, separable and one DPP row per group, the
+        // general separable form below, unless a tap's floor is more than one cell off its regular
+        // place (only near |coordinates| ~ 2^20) or some upstream gradient of the wave is not
+        // finite (that form multiplies every candidate tap, so a zero weight would turn an
+        // infinite gradient into a NaN the reference does not have)
+        bool rangef = irregular;
+        if constexpr (SEP && SLOTS == 16) {
+            if (__ballot(irregular)) {
+                const bool odd = cx < S && !(fabsf(a.f - fx0 - (float)cx) <= 1.f && fabsf(c.f - fy0 - (float)cx) <= 1.f);
+                bool nonfin = false;
+#pragma unroll
+                for (int u = 0; u < S; ++u) nonfin |= !__builtin_isfinite(v[u]);
+                rangef = irregular && (__ballot(nonfin) != 0 || (__ballot(odd && qok && !far) & gmask) != 0);
+            }
+        }
         // the range form and the sequential scatter read any tap and any tap's gradients from the
         // wave's staging: written only when some group of the wave takes one of those paths
-        if (__ballot(irregular || unc)) {
+        if (__ballot(rangef || unc)) {
             if (cx < S) {
                 tx(0, cx) = a.f, tx(1, cx) = a.lo, tx(2, cx) = a.hi;
                 ty(0, cx) = c.f, ty(1, cx) = c.lo, ty(2, cx) = c.hi;
@@ -1374,6 +1389,30 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         const int ayv = colok ? ay : -(1 << 30);
         const int rowbase = mbase + ay * Wl + X;
         auto cell_at = [&](int cy) { return (unsigned)(ayv + cy) < (unsigned)Hl ? rowbase + cy * Wl : dump; };
+        // adds the column's NC cells sv[cy] (rows ay + cy) to the map.  Byte addresses: row ay + cy
+        // clamped to [-1, Hl] — rows -1 and Hl of every map are guard rows (fused_lds_bytes), so
+        // the window's cells above / below the map land in a guard row nothing reads — and a column
+        // that is not this lane's to write starts past the workgroup's LDS allocation, where DS
+        // reads return 0 and DS writes are dropped.  Clamping the ADDRESS of row ay + cy between
+        // those of rows -1 and H_l is the same (addresses grow with the row), so a cell costs one
+        // add and one v_med3.
+        auto add_column = [&]<int NC>(const float (&sv)[NC]) {
+            const bool mine = colok && cx < NC;
+            const int cb = mine ? 4 * (mbase + X) : kLdsOob;
+            const int s4 = 4 * Wl;
+            const int gtop = cb - s4, gbot = cb + Hl * s4;
+            // rows past [-NC, H_l] clamp like those bounds (and keep s4 * ay in range)
+            int ra = cb + s4 * (mine ? min(max(ay, -NC), Hl) : 0);
+            char *const lds = reinterpret_cast<char *>(fsm);
+            float old[NC];
+            unsigned at[NC];
+#pragma unroll
+            for (int cy = 0; cy < NC; ++cy, ra += s4) at[cy] = (unsigned)med3_i32(ra, gtop, gbot);
+#pragma unroll
+            for (int cy = 0; cy < NC; ++cy) old[cy] = *reinterpret_cast<float *>(lds + at[cy]);  // all reads, then all writes
+#pragma unroll
+            for (int cy = 0; cy < NC; ++cy) *reinterpret_cast<float *>(lds + at[cy]) = old[cy] + sv[cy];
+        };
         if (!irregular) {
             // closed form.  Absent terms (window edges) carry zero weights and gradients: adding
             // +-0 to a sum that started at +0 leaves it unchanged, so every cell sums its 4 terms
@@ -1432,27 +1471,52 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
                 sv[cy] = acc.x;
                 sv[cy + 1] = acc.y;
             }
-            // byte addresses of the column's cells: row ay + cy clamped to [-1, Hl] — rows -1 and Hl
-            // of every map are guard rows (fused_lds_bytes), so the window's cells above / below the
-            // map land in a guard row nothing reads — and a column that is not this lane's to write
-            // starts past the workgroup's LDS allocation, where DS reads return 0 and DS writes are
-            // dropped.  Clamping the ADDRESS of row ay + cy between those of rows -1 and H_l is the
-            // same (addresses grow with the row), so a cell costs one add and one v_med3.
-            const bool mine = colok && cx < C;
-            const int cb = mine ? 4 * (mbase + X) : kLdsOob;
-            const int s4 = 4 * Wl;
-            const int gtop = cb - s4, gbot = cb + Hl * s4;
-            // rows past [-C, H_l] clamp like those bounds (and keep s4 * ay in range)
-            int ra = cb + s4 * (mine ? min(max(ay, -C), Hl) : 0);
-            char *const lds = reinterpret_cast<char *>(fsm);
-            float old[C];
-            unsigned at[C];
+            add_column(reinterpret_cast<const float (&)[C]>(sv));
+        } else if (!rangef) {
+            if constexpr (SEP && SLOTS == 16) {
+                // general separable form (irregular windows: taps of a query whose floors are not all
+                // anchor + t, e.g. the cold-start integer grid, where rounding leaves some taps a hair
+                // below their integer).  Tap t's floor is anchor + t + e_t with e_t in {-1, 0, 1}, so it
+                // reaches cells t - 1 .. t + 2 of the neighbourhood: slot k in {-1, 0, 1, 2} weighs
+                // lo at k = e_t, hi at k = e_t + 1, 0 elsewhere.  Column cx gathers x-taps cx, cx - 1,
+                // cx - 2, cx + 1 (DPP row shifts: the 16-lane group is the DPP row, lanes outside it
+                // read 0), then row cy gathers y-taps cy, cy - 1, cy - 2, cy + 1 (broadcast weights).
+                // Non-reached slots multiply a finite gradient by 0 (rangef excludes non-finite ones).
+                const bool tv = cx < S;
+                auto slots = [&](float e, float lo, float hi, float &wm1, float &w0, float &w1, float &w2) {
+                    const bool m = e == -1.f, z = e == 0.f, p = e == 1.f;  // e = 2: no tap
+                    wm1 = m ? lo : 0.f;
+                    w0 = m ? hi : (z ? lo : 0.f);
+                    w1 = z ? hi : (p ? lo : 0.f);
+                    w2 = p ? hi : 0.f;
+                };
+                float xm1, x0, x1, x2, ym1, y0, y1, y2;
+                slots(tv ? a.f - fx0 - (float)cx : 2.f, a.lo, a.hi, xm1, x0, x1, x2);
+                slots(tv ? c.f - fy0 - (float)cx : 2.f, c.lo, c.hi, ym1, y0, y1, y2);
+                auto shr1 = [](float x) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x111, 0xF, 0xF, true)); };
+                auto shr2 = [](float x) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x112, 0xF, 0xF, true)); };
+                auto shl1 = [](float x) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x101, 0xF, 0xF, true)); };
+                const float wp1 = shr1(x1), wp2 = shr2(x2), wn1 = shl1(xm1);
+                float hx[S];
 #pragma unroll
-            for (int cy = 0; cy < C; ++cy, ra += s4) at[cy] = (unsigned)med3_i32(ra, gtop, gbot);
+                for (int j = 0; j < S; ++j)
+                    hx[j] = __builtin_fmaf(v[j], x0, __builtin_fmaf(shr1(v[j]), wp1, __builtin_fmaf(shr2(v[j]), wp2, shl1(v[j]) * wn1)));
+                float Ym1[S], Y0[S], Y1[S], Y2[S];
+                group_lanes<SLOTS, S>(ym1, lane, Ym1);
+                group_lanes<SLOTS, S>(y0, lane, Y0);
+                group_lanes<SLOTS, S>(y1, lane, Y1);
+                group_lanes<SLOTS, S>(y2, lane, Y2);
+                float sv[WIN];
 #pragma unroll
-            for (int cy = 0; cy < C; ++cy) old[cy] = *reinterpret_cast<float *>(lds + at[cy]);  // all reads, then all writes
-#pragma unroll
-            for (int cy = 0; cy < C; ++cy) *reinterpret_cast<float *>(lds + at[cy]) = old[cy] + sv[cy];
+                for (int cy = 0; cy < WIN; ++cy) {
+                    float acc = cy < S ? hx[cy] * Y0[cy] : 0.f;
+                    if (cy >= 1 && cy - 1 < S) acc = __builtin_fmaf(hx[cy - 1], Y1[cy - 1], acc);
+                    if (cy >= 2 && cy - 2 < S) acc = __builtin_fmaf(hx[cy - 2], Y2[cy - 2], acc);
+                    if (cy + 1 < S) acc = __builtin_fmaf(hx[cy + 1], Ym1[cy + 1], acc);
+                    sv[cy] = acc;
+                }
+                add_column(sv);
+            }
         } else {
             float dy[S];
 #pragma unroll

@@ -728,6 +728,41 @@ def test_corr_backward_matches_staged_path(algo, B, D, H, W, L, r, T, exact):
             assert e <= 1e-6, (k, e)
 
 
+@pytest.mark.parametrize("exact", [True, False])
+def test_corr_backward_infinite_upstream_gradients(exact):
+    """Infinite upstream gradients (on regular, integer-grid and far windows) give dC the staged
+    path's inf / NaN cells exactly — the separable fold's general form for irregular windows
+    multiplies every candidate tap, so a wave holding a non-finite gradient replays its irregular
+    windows by the range form instead — and its finite cells within 1e-6 (bit-identical when
+    exact)."""
+    from eraft_amd import _lib
+    from eraft_amd.corr import _alloc_grad_pyramid
+    B, D, H, W, L, r, T = 2, 16, 18, 24, 4, 4, 3
+    f1 = torch.from_numpy(prng.gauss(63, (B, D, H, W))).to(DEV)
+    f2 = torch.from_numpy(prng.gauss(64, (B, D, H, W))).to(DEV)
+    cs, gs = _bwd_case(T, B, H, W, L, r, 820)
+    K = (2 * r + 1) ** 2
+    for t, g in enumerate(gs):  # +inf at a few (tap, query) points of each lookup, every level
+        for l in range(L):
+            g[0, l * K + (7 * t + 3) % K, 5, 7 + t] = float("inf")
+            g[1, l * K + 40, 11, 3 * t] = float("inf")
+    ref = _alloc_grad_pyramid(B, H, W, L, f1, zero=True)
+    for c, g in zip(cs, gs):
+        _lib.lookup_bwd(c, g, r, ref)
+    _lib.pool_bwd(ref, H, W)
+    got = _alloc_grad_pyramid(B, H, W, L, f1)
+    _lib.backward(cs, gs, r, got, f1, f2, _lib._ALGOS["bf16x6"], exact=exact)
+    a, b = got[0].cpu().numpy(), ref[0].cpu().numpy()
+    assert np.isnan(b).any() and np.isinf(b).any()
+    assert np.array_equal(np.isnan(a), np.isnan(b)) and np.array_equal(np.isposinf(a), np.isposinf(b))
+    assert np.array_equal(np.isneginf(a), np.isneginf(b))
+    fin = np.isfinite(b)
+    if exact:
+        assert bit_equal(a[fin], b[fin])
+    else:
+        assert norm_rel(a[fin], b[fin]) <= 1e-6
+
+
 def test_lookup_only_loss_runs_one_backward_call(monkeypatch):
     """a loss that reaches the pyramid only through lookups makes no zero-filled
     pyramid gradient (materialize_grads off) and no per-lookup kernel: the build's backward is

@@ -106,6 +106,7 @@ int main(int argc, char **argv) {
     vs.push_back({"SEP full T=12", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12); }, {}});
     vs.push_back({"SEP full T=12, lookup 0 on the integer grid", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, true); }, {}});
     vs.push_back({"SEP full T=1", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 1); }, {}});
+    vs.push_back({"SEP full T=1 on the integer grid", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 1, true); }, {}});
     vs.push_back({"full T=12, no maxima, cached dC", [&] { launch(lookup_bwd_fold_kernel<S, 8>, 12, false, 0, &onm); }, {}});
     vs.push_back({"no lookups, no maxima", [&] { launch(lookup_bwd_fold_kernel<S, 1>, 12, false, 0, &onm); }, {}});
     vs.push_back({"no lookups, no maxima, cached dC", [&] { launch(lookup_bwd_fold_kernel<S, 9>, 12, false, 0, &onm); }, {}});
