@@ -1259,19 +1259,33 @@ __device__ __forceinline__ void group_lanes(float x, int lane, float (&out)[N]) 
 // also keeps the compiler from moving LDS accesses across it).
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// The lookup table is the kernel's FIRST argument: read entry t straight from the kernarg
-// segment (one scalar load) — indexing the by-value copy with a runtime t makes the compiler
-// either spill the table to scratch or emit a 32-way branch tree.
-__device__ __forceinline__ void kernarg_lookup(int t, const float *&c, const float *&g) {
-    typedef const BwdLookups __attribute__((address_space(4))) *KPtr;
-    const KPtr kp = (KPtr)__builtin_amdgcn_kernarg_segment_ptr();
-    c = kp->coords[t];
-    g = kp->grad[t];
-}
+// The lookup table (the kernel's FIRST argument) in VGPRs: lane i holds lookup i's two pointers,
+// read once from the kernarg segment by a vector load; lookup t's are then two pairs of
+// v_readlane.  Indexing the by-value copy with a runtime t makes the compiler either spill the
+// table to scratch or emit a 32-way branch tree, and a scalar load per lookup would make every
+// lookup wait for lgkmcnt(0) — i.e. also for the previous lookup's LDS writes — before its loads.
+struct LaneTable {
+    uint32_t c_lo, c_hi, g_lo, g_hi;
+    __device__ __forceinline__ explicit LaneTable(int lane) {
+        typedef const BwdLookups __attribute__((address_space(4))) *KPtr;
+        const KPtr kp = (KPtr)__builtin_amdgcn_kernarg_segment_ptr();
+        const int i = min(lane, kMaxLookups - 1);
+        const uint64_t c = (uint64_t)kp->coords[i], g = (uint64_t)kp->grad[i];
+        c_lo = (uint32_t)c, c_hi = (uint32_t)(c >> 32), g_lo = (uint32_t)g, g_hi = (uint32_t)(g >> 32);
+    }
+    __device__ __forceinline__ void get(int t, const float *&c, const float *&g) const {
+        // (readlane returns int: widen through uint32_t, or a low word >= 2^31 sign-extends)
+        c = reinterpret_cast<const float *>(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(c_hi, t) << 32) |
+                                            (uint64_t)(uint32_t)__builtin_amdgcn_readlane(c_lo, t));
+        g = reinterpret_cast<const float *>(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(g_hi, t) << 32) |
+                                            (uint64_t)(uint32_t)__builtin_amdgcn_readlane(g_lo, t));
+    }
+};
 
 // PROBE (measurement builds only, tools/kbench_bwd.hip; the library uses 0): bit 0 = no lookup
 // loop, bit 1 = no fold (no dC / maxima), bit 2 = no LDS zero-init (wrong results, timing only),
-// bit 3 = plain (L2-cached) dC stores instead of the non-temporal ones.
+// bit 3 = plain (L2-cached) dC stores instead of the non-temporal ones, bit 4 = wait for the
+// lookup's LDS writes at the end of each lookup (round 5's s_waitcnt).
 // SEP: regular windows by the separable closed form (corr_backward's default); false replays
 // grid_sampler_2d_backward's per-tap products bit for bit (CORR_BACKWARD_EXACT_FOLD).
 template <int S, int PROBE = 0, bool SEP = false>
@@ -1317,9 +1331,10 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     const uint32_t coff = loader ? (uint32_t)n * 4u : kOob;
     const uint32_t goff = loader ? (uint32_t)(((lc * K + cx * S) * NQ + n) * 4) : kOob;
     float pcx, pcy, pv[S];
+    const LaneTable table(lane);
     auto prefetch = [&](int t) {
         const float *coords, *grad_out;
-        kernarg_lookup(t, coords, grad_out);
+        table.get(t, coords, grad_out);
         const auto rc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(coords + (size_t)b * 2 * NQ), 0,
                                                           2 * NQ * 4, 0x00020000);
         const auto rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(grad_out + (size_t)b * L * K * NQ), 0,
@@ -1591,7 +1606,11 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
                 if (mine && Y >= 0 && Y < Hl) Mq[Y * Wl + X] = keep[ry] + Mq[Y * Wl + X];
             }
         }
-        wave_lds_sync();  // the next lookup rewrites the staging
+        // the next lookup rewrites the staging: a compiler barrier keeps this lookup's LDS accesses
+        // before the next one's (one wave's DS operations execute in issue order, so no wait is
+        // needed: the map writes drain while the next lookup's taps are computed)
+        if constexpr ((PROBE & 16) != 0) wave_lds_sync();
+        else asm volatile("" ::: "memory");
     }
     __syncthreads();
 

@@ -104,6 +104,7 @@ int main(int argc, char **argv) {
     vs.push_back({"full T=12, no maxima (bf16x6)", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12, false, 0, &onm); }, {}});
     vs.push_back({"SEP full T=12, no maxima (bf16x6)", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, 0, &onm); }, {}});
     vs.push_back({"SEP full T=12", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12); }, {}});
+    vs.push_back({"SEP full T=12, trailing LDS wait", [&] { launch(lookup_bwd_fold_kernel<S, 16, true>, 12); }, {}});
     vs.push_back({"SEP full T=12, lookup 0 on the integer grid", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, true); }, {}});
     vs.push_back({"SEP full T=1", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 1); }, {}});
     vs.push_back({"SEP full T=1 on the integer grid", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 1, true); }, {}});
