@@ -1173,12 +1173,12 @@ struct FusedOut {
 // Row |max| work of the blocks appended to the fold grid (rowmax2_kernel's per-row reduction:
 // a wave walks each of its rows with 16-B loads, one cross-lane reduction per row).  They sit
 // at the end of the grid, so they run in the fold's last, partly empty round of workgroups.
-__device__ __forceinline__ void fold_rowmax_block(const FusedOut &o, int blk) {
+__device__ __forceinline__ void fold_rowmax_block(const FusedOut &o, int blk, int waves) {
     const FoldRowMax &a = o.rm;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int per_op = o.B * a.rows;  // rows of one operand, over the batch
     for (int k = 0; k < o.rm_rows_per_wave; ++k) {
-        const int g = (blk * kFusedLv + wv) * o.rm_rows_per_wave + k;
+        const int g = (blk * waves + wv) * o.rm_rows_per_wave + k;
         if (g >= 2 * per_op) return;  // whole waves
         const int t = g / per_op, br = g - t * per_op;
         const int cols = a.cols[t];
@@ -1208,6 +1208,13 @@ struct FusedStage {
     static constexpr int TX = 0, TY = TX + 3 * S * BQ, GG = TY + 3 * S * BQ, AX = GG + K * BQ, AY = AX + BQ,
                          DUMP = AY + BQ, SIZE = DUMP + 64;
 };
+
+// The separable fold with one DPP row per (query, level) group keeps no per-wave staging in LDS:
+// its irregular windows take the general separable form and its rare windows (corners outside
+// the neighbourhood, taps more than one cell off, non-finite gradients) the sequential scatter,
+// which reads the group's taps and gradients by lane shuffles (ds_bpermute: no LDS allocated).
+template <int S, bool SEP>
+constexpr bool fold_no_staging() { return SEP && FusedStage<S>::SLOTS == 16; }
 
 // Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2).  Renumber them so
 // every XCD gets a contiguous range: neighbouring query groups — which share the 128-B lines of
@@ -1288,21 +1295,25 @@ struct LaneTable {
 // lookup's LDS writes at the end of each lookup (round 5's s_waitcnt).
 // SEP: regular windows by the separable closed form (corr_backward's default); false replays
 // grid_sampler_2d_backward's per-tap products bit for bit (CORR_BACKWARD_EXACT_FOLD).
+// (Several query groups per workgroup — 8 or 16 queries, so that the groups' waves would share
+// L1 fills of the upstream-gradient lines — were measured and dropped: L2 requests unchanged,
+// T = 12 92 -> 101 / 164 us, profiles/r05zi_kbench_bwd_groups_dropped.txt.)
 template <int S, int PROBE = 0, bool SEP = false>
 __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLookups lk, FusedOut o) {
     using ST = FusedStage<S>;
     constexpr int R = (S - 1) / 2, K = S * S, C = S + 1, WIN = ST::WIN;
-    constexpr int SLOTS = ST::SLOTS, BQ = ST::BQ, NT = 64 * kFusedLv;
+    constexpr int SLOTS = ST::SLOTS, BQ = ST::BQ, WQ = BQ, NT = 64 * kFusedLv;
+    constexpr bool NOST = fold_no_staging<S, SEP>();
     extern __shared__ float fsm[];
 
     if ((int)blockIdx.x >= o.nfold) {  // appended row-maxima blocks (uniform per workgroup)
-        fold_rowmax_block(o, (int)blockIdx.x - o.nfold);
+        fold_rowmax_block(o, (int)blockIdx.x - o.nfold, kFusedLv);
         return;
     }
     const int NQ = o.NQ, H = o.H, W = o.W, L = o.L, N = H * W;
-    const int nqb = (NQ + BQ - 1) / BQ;
+    const int nqb = (NQ + WQ - 1) / WQ;
     const int blk = xcd_contiguous(blockIdx.x, o.nfold);
-    const int b = blk / nqb, n0 = (blk - b * nqb) * BQ;
+    const int b = blk / nqb, n0 = (blk - b * nqb) * WQ;
     const int tid = threadIdx.x, lane = tid & 63;
     const int l = tid >> 6;  // wave = level
     const int q = lane / SLOTS, cx = lane - q * SLOTS;
@@ -1319,17 +1330,25 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     auto tx = [&](int c, int t) -> float & { return st[ST::TX + (c * S + t) * BQ + q]; };
     auto ty = [&](int c, int t) -> float & { return st[ST::TY + (c * S + t) * BQ + q]; };
     auto gg = [&](int k) -> float & { return st[ST::GG + k * BQ + q]; };
-    unsigned *RM = reinterpret_cast<unsigned *>(fsm + o.aux + kFusedLv * ST::SIZE);  // [BQ]
+    unsigned *RM = reinterpret_cast<unsigned *>(fsm + o.aux + (NOST ? 0 : kFusedLv * ST::SIZE));  // [WQ]
 
     // the next lookup's coords and upstream gradients are loaded one lookup ahead (registers),
     // by buffer loads over batch item b's slice: every lane loads, and the lanes that own no
     // (tap, query) point past the slice, so the range check returns their zeros (no branch
-    // around the loads, no select at use, 32-bit offsets).
+    // around the loads, no select at use, 32-bit offsets).  The gradients are loaded in the
+    // transposed lane order (lane 4 cx + q holds x-tap cx of query q), so the 4 lanes of a quad
+    // read one 16-B run (the BQ queries' values of one row): one cache access per quad instead
+    // of one per lane — the vector memory pipe (TA / TD ~85 % busy) bounded the lookup loop
+    // (profiles/r05zg_fold_pmc.txt) — and one ds_bpermute per value restores lane order.
     const bool loader = act && cx < S && qok;
     const int cxl = min(cx, S - 1);
     constexpr uint32_t kOob = 0x80000000u;
     const uint32_t coff = loader ? (uint32_t)n * 4u : kOob;
-    const uint32_t goff = loader ? (uint32_t)(((lc * K + cx * S) * NQ + n) * 4) : kOob;
+    constexpr bool kQuadLoads = SLOTS == 16 && BQ == 4;
+    const int lq = kQuadLoads ? (lane & 3) : q, lx = kQuadLoads ? (lane >> 2) : cx;
+    const bool gloader = act && lx < S && n0 + lq < NQ;
+    const uint32_t goff = gloader ? (uint32_t)(((lc * K + lx * S) * NQ + n0 + lq) * 4) : kOob;
+    const int gsrc = kQuadLoads ? 4 * (4 * cx + q) : 0;  // ds_bpermute byte address of this lane's loader
     float pcx, pcy, pv[S];
     const LaneTable table(lane);
     auto prefetch = [&](int t) {
@@ -1347,10 +1366,9 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     };
     if (act) prefetch(0);  // issued before the LDS zeroing, so its latency hides behind it
     if (!(PROBE & 4))
-        // every map of the workgroup, 16 B per store (o.aux is a multiple of 64 floats:
-        // BQ query strides of 64k + 64 / BQ)
+        // every map of the workgroup, 16 B per store (o.aux is a multiple of 4 floats)
         for (int i = 4 * tid; i < o.aux; i += 4 * NT) *reinterpret_cast<float4 *>(fsm + i) = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (tid < BQ) RM[tid] = 0u;
+    if (tid < WQ) RM[tid] = 0u;
     __syncthreads();
 
     for (int t = 0; !(PROBE & 1) && act && t < lk.T; ++t) {  // absent levels (l >= L) only join the fold
@@ -1358,7 +1376,8 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         const float cxv = pcx, cyv = pcy;  // 0 for the lanes without a (tap, query)
         float v[S];
 #pragma unroll
-        for (int u = 0; u < S; ++u) v[u] = pv[u];
+        for (int u = 0; u < S; ++u)
+            v[u] = kQuadLoads ? __int_as_float(__builtin_amdgcn_ds_bpermute(gsrc, __float_as_int(pv[u]))) : pv[u];
         prefetch(min(t + 1, lk.T - 1));
         const Axis a = tap_axis(cxv, inv_scale, cxl, R, Wl, rdx);
         const Axis c = tap_axis(cyv, inv_scale, cxl, R, Hl, rdy);
@@ -1371,24 +1390,26 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         const bool far = ax == kFarAnchor || ay == kFarAnchor;
         const bool unc = qok && !window_covers<S>(fx0, group_lane<SLOTS, S - 1>(a.f, lane), fy0,
                                                   group_lane<SLOTS, S - 1>(c.f, lane));
-        // irregular groups take the range form — or, separable and one DPP row per group, the
-        // general separable form below, unless a tap's floor is more than one cell off its regular
-        // place (only near |coordinates| ~ 2^20) or some upstream gradient of the wave is not
-        // finite (that form multiplies every candidate tap, so a zero weight would turn an
-        // infinite gradient into a NaN the reference does not have)
-        bool rangef = irregular;
-        if constexpr (SEP && SLOTS == 16) {
+        // irregular groups take the range form (exact) — or, without staging (NOST), the general
+        // separable form below, unless a tap's floor is more than one cell off its regular place
+        // (only near |coordinates| ~ 2^20) or some upstream gradient of the wave is not finite
+        // (that form multiplies every candidate tap, so a zero weight would turn an infinite
+        // gradient into a NaN the reference does not have): those groups, like the groups whose
+        // corners leave the neighbourhood, take the sequential scatter (seq)
+        bool rangef = irregular, seq = unc;
+        if constexpr (NOST) {
+            rangef = false;
             if (__ballot(irregular)) {
                 const bool odd = cx < S && !(fabsf(a.f - fx0 - (float)cx) <= 1.f && fabsf(c.f - fy0 - (float)cx) <= 1.f);
                 bool nonfin = false;
 #pragma unroll
                 for (int u = 0; u < S; ++u) nonfin |= !__builtin_isfinite(v[u]);
-                rangef = irregular && (__ballot(nonfin) != 0 || (__ballot(odd && qok && !far) & gmask) != 0);
+                seq = unc || (irregular && qok && !far &&
+                              (__ballot(nonfin) != 0 || (__ballot(odd && qok && !far) & gmask) != 0));
             }
-        }
-        // the range form and the sequential scatter read any tap and any tap's gradients from the
-        // wave's staging: written only when some group of the wave takes one of those paths
-        if (__ballot(rangef || unc)) {
+        } else if (__ballot(rangef || unc)) {
+            // the range form and the sequential scatter read any tap and any tap's gradients from
+            // the wave's staging: written only when some group of the wave takes one of those paths
             if (cx < S) {
                 tx(0, cx) = a.f, tx(1, cx) = a.lo, tx(2, cx) = a.hi;
                 ty(0, cx) = c.f, ty(1, cx) = c.lo, ty(2, cx) = c.hi;
@@ -1398,7 +1419,7 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
             wave_lds_sync();
         }
         const int X = ax + cx;
-        const bool colok = qok && !unc && !far && cx < WIN && X >= 0 && X < Wl;
+        const bool colok = qok && !seq && !far && cx < WIN && X >= 0 && X < Wl;
         // cell (cx, cy) of the window -> its map address, or the lane's dump slot when the cell
         // is outside the map / the column is not this lane's to write
         const int ayv = colok ? ay : -(1 << 30);
@@ -1496,7 +1517,7 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
                 // lo at k = e_t, hi at k = e_t + 1, 0 elsewhere.  Column cx gathers x-taps cx, cx - 1,
                 // cx - 2, cx + 1 (DPP row shifts: the 16-lane group is the DPP row, lanes outside it
                 // read 0), then row cy gathers y-taps cy, cy - 1, cy - 2, cy + 1 (broadcast weights).
-                // Non-reached slots multiply a finite gradient by 0 (rangef excludes non-finite ones).
+                // Non-reached slots multiply a finite gradient by 0 (seq takes the waves with non-finite ones).
                 const bool tv = cx < S;
                 auto slots = [&](float e, float lo, float hi, float &wm1, float &w0, float &w1, float &w2) {
                     const bool m = e == -1.f, z = e == 0.f, p = e == 1.f;  // e = 2: no tap
@@ -1532,7 +1553,7 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
                 }
                 add_column(sv);
             }
-        } else {
+        } else if constexpr (!NOST) {
             float dy[S];
 #pragma unroll
             for (int j = 0; j < S; ++j) dy[j] = ty(0, j) - fy0;
@@ -1563,12 +1584,13 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
                 fsm[at] = fsm[at] + sv;
             }
         }
-        // ---- 2c. groups whose corners leave the neighbourhood: sequential scatter ----
+        // ---- 2c. groups whose corners leave the neighbourhood (and, NOST, the rare irregular
+        // ones): sequential scatter ----
         // The group's in-map window cells are saved to registers and zeroed, so they serve as the
         // zeroed window scratch; afterwards cell = saved + scatter sum (lookup_bwd_kernel's order).
-        if (__ballot(unc)) {
+        if (__ballot(seq)) {
             float *Mq = fsm + mbase;
-            const bool mine = unc && cx < WIN && X >= 0 && X < Wl;
+            const bool mine = seq && cx < WIN && X >= 0 && X < Wl;
             float keep[WIN];
 #pragma unroll
             for (int ry = 0; ry < WIN; ++ry) {
@@ -1580,11 +1602,31 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
                 }
             }
             wave_lds_sync();
-            if (unc && cx == 0) {
-                auto scatter = [&](float xf, float yf, float val) {
-                    if (!in_map(xf, yf, Wl, Hl)) return;
-                    Mq[(int)yf * Wl + (int)xf] += val;  // window cells: the zeroed scratch
-                };
+            auto scatter = [&](float xf, float yf, float val) {
+                if (!in_map(xf, yf, Wl, Hl)) return;
+                Mq[(int)yf * Wl + (int)xf] += val;  // window cells: the zeroed scratch
+            };
+            if constexpr (NOST) {
+                // the group's taps and gradients by lane shuffles (all lanes take part; lane 0 of
+                // each sequential group scatters)
+                const int g0 = lane & ~(SLOTS - 1);
+                for (int ii = 0; ii < S; ++ii) {
+                    const float x0 = __shfl(a.f, g0 + ii, 64), ex = __shfl(a.lo, g0 + ii, 64);
+                    const float wx = __shfl(a.hi, g0 + ii, 64), x1 = __fadd_rn(x0, 1.0f);
+#pragma unroll
+                    for (int j = 0; j < S; ++j) {
+                        const float gv = __shfl(v[j], g0 + ii, 64);
+                        const float y0 = __shfl(c.f, g0 + j, 64), ey = __shfl(c.lo, g0 + j, 64);
+                        const float ny = __shfl(c.hi, g0 + j, 64), y1 = __fadd_rn(y0, 1.0f);
+                        if (seq && cx == 0) {
+                            scatter(x0, y0, __fmul_rn(gv, __fmul_rn(ey, ex)));
+                            scatter(x1, y0, __fmul_rn(gv, __fmul_rn(ey, wx)));
+                            scatter(x0, y1, __fmul_rn(gv, __fmul_rn(ny, ex)));
+                            scatter(x1, y1, __fmul_rn(gv, __fmul_rn(ny, wx)));
+                        }
+                    }
+                }
+            } else if (seq && cx == 0) {
                 for (int ii = 0; ii < S; ++ii) {
                     const float x0 = tx(0, ii), x1 = __fadd_rn(x0, 1.0f);
                     const float ex = tx(1, ii), wx = tx(2, ii);
@@ -1616,9 +1658,9 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
 
     if constexpr ((PROBE & 2) != 0) return;
     // ---- 3. fold into level 0, write dC with its row / column maxima ----
-    float rq[BQ];
+    float rq[WQ];
 #pragma unroll
-    for (int k = 0; k < BQ; ++k) rq[k] = 0.f;
+    for (int k = 0; k < WQ; ++k) rq[k] = 0.f;
     if (W % 4 == 0 && ((uintptr_t)o.dc & 15) == 0 && ((uintptr_t)o.cpart & 15) == 0) {
         // 4 consecutive cells of one row per thread: one 16-B LDS read of level 0, one 8-B read of
         // level 1 (W/2 even, so its 2 cells are 8-B aligned), one value of each coarser level
@@ -1635,7 +1677,7 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
             }
             float cm[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int k = 0; k < BQ; ++k) {
+            for (int k = 0; k < WQ; ++k) {
                 if (n0 + k >= NQ) continue;
                 float lv[kFusedLv][4];
                 const float4 t0 = *reinterpret_cast<const float4 *>(fsm + off[0] + k * o.qstr[0]);
@@ -1695,7 +1737,7 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
                 if (v + 1 < L && yv < 2 * (Hv >> 1) && xv < 2 * (Wv >> 1)) rc |= 1u << v;
             }
 #pragma unroll
-            for (int k = 0; k < BQ; ++k) {
+            for (int k = 0; k < WQ; ++k) {
                 if (n0 + k >= NQ) continue;
                 float up = 0.f;
                 bool have = false;
@@ -1720,14 +1762,14 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         }
     }
 #pragma unroll
-    for (int k = 0; k < BQ; ++k) {
+    for (int k = 0; k < WQ; ++k) {
         float r = rq[k];
 #pragma unroll
         for (int sh = 32; sh >= 1; sh >>= 1) r = fmaxf(r, __shfl_xor(r, sh));
         if (lane == 0 && r > 0.f) atomicMax(&RM[k], __float_as_uint(r));
     }
     __syncthreads();
-    if (o.rmax && tid < BQ && n0 + tid < NQ) o.rmax[(size_t)b * NQ + n0 + tid] = RM[tid];
+    if (o.rmax && tid < WQ && n0 + tid < NQ) o.rmax[(size_t)b * NQ + n0 + tid] = RM[tid];
 }
 
 // avg_pool2d backward, one level: fine[q][y][x] += coarse[q][y/2][x/2] * 0.25 on the pooled
@@ -1943,31 +1985,37 @@ hipError_t launch_pool_bwd(const LevelPtrs &gpyr, long BN, int H, int W, int lev
 // maps at every level + per-wave staging) exceeds 160 KiB, or levels > 4, or T > kMaxLookups —
 // the caller then takes the staged path.
 namespace {
-template <int S>
+template <int S, bool SEP = false>
 size_t fused_lds_bytes(int H, int W, int levels, FusedOut *o) {
     using ST = FusedStage<S>;
-    // query stride = map cells plus one guard row, rounded up to 64 / BQ (mod 64): the BQ
-    // queries' maps start in different LDS banks, so a wave's read-modify-writes of neighbouring
-    // queries' windows (whose anchors differ by about one pixel) do not collide.  Every map has a
-    // guard row above (row -1) and below (row H_l), which the closed form's clamped rows write
-    // (one row may serve as one map's row H_l and the next map's row -1); a level's region is a
-    // leading guard row and BQ query strides, rounded to 64 floats.
+    // query stride = map cells plus one guard row, rounded up to an ODD multiple of 64 / BQ
+    // floats: the BQ queries' maps then start in BQ different LDS banks (q * stride mod 64), so a
+    // wave's read-modify-writes of neighbouring queries' windows (whose anchors differ by about
+    // one pixel) do not collide.  Every map has a guard row above (row -1) and below (row H_l),
+    // which the closed form's clamped rows write (one row may serve as one map's row H_l and the
+    // next map's row -1); a level's region is a leading guard row and BQ query strides, rounded
+    // to 4 floats (16-B zeroing; the fold's 16-B / 8-B reads of levels 0 / 1).  The per-wave
+    // staging follows unless the kernel has none (fold_no_staging).
     size_t maps = 0;
     const int stag = 64 / ST::BQ;
     for (int l = 0; l < kFusedLv; ++l) {
         const int Hl = H >> l, Wl = W >> l;
         const int msz = l < levels ? Hl * Wl : 0;
-        const int qs = msz ? ((Hl + 1) * Wl + 63) / 64 * 64 + stag : 0;
+        int qs = 0;
+        if (msz) {
+            qs = ((Hl + 1) * Wl + stag - 1) / stag * stag;
+            if (ST::BQ > 1 && ((qs / stag) & 1) == 0) qs += stag;
+        }
         if (o) o->moff[l] = (int)maps + (msz ? Wl : 0), o->msz[l] = msz, o->qstr[l] = qs;
-        if (msz) maps += ((size_t)Wl + (size_t)ST::BQ * qs + 63) / 64 * 64;
+        if (msz) maps += ((size_t)Wl + (size_t)ST::BQ * qs + 3) / 4 * 4;
     }
     if (o) o->aux = (int)maps;
-    return (maps + (size_t)kFusedLv * ST::SIZE + ST::BQ) * 4;
+    return (maps + (fold_no_staging<S, SEP>() ? 0 : (size_t)kFusedLv * ST::SIZE) + ST::BQ) * 4;
 }
 
 template <int S, bool SEP = false>
 hipError_t launch_fused_s(const BwdLookups &lk, FusedOut o, hipStream_t s) {
-    const size_t bytes = fused_lds_bytes<S>(o.H, o.W, o.L, &o);
+    const size_t bytes = fused_lds_bytes<S, SEP>(o.H, o.W, o.L, &o);
     // the dynamic-LDS limit is raised once per device to the largest image this path accepts
     // (not to this call's size: a later, larger shape must not run against a smaller limit),
     // capped at what the device offers per workgroup
@@ -1980,18 +2028,19 @@ hipError_t launch_fused_s(const BwdLookups &lk, FusedOut o, hipStream_t s) {
     static std::atomic<unsigned long long> done{0};
     e = ensure_lds_limit((const void *)lookup_bwd_fold_kernel<S, 0, SEP>, limit, done);
     if (e != hipSuccess) return e;
-    const int nqb = (o.NQ + FusedStage<S>::BQ - 1) / FusedStage<S>::BQ;
+    constexpr int WQ = FusedStage<S>::BQ, WAVES = kFusedLv;
+    const int nqb = (o.NQ + WQ - 1) / WQ;
     o.nfold = nqb * o.B;
     // row-maxima blocks: at most half a round of workgroup slots (the fold's tail), >= 1 row per wave
     int extra = 0;
     if (o.rm.rows > 0) {
         const long rows = 2L * o.B * o.rm.rows;
         const long cap = std::max(1L, (long)(256 * std::max<size_t>(1, 160 * 1024 / bytes)) / 2);
-        o.rm_rows_per_wave = (int)std::max(1L, (rows + cap * kFusedLv - 1) / (cap * kFusedLv));
-        extra = (int)((rows + (long)o.rm_rows_per_wave * kFusedLv - 1) / ((long)o.rm_rows_per_wave * kFusedLv));
+        o.rm_rows_per_wave = (int)std::max(1L, (rows + cap * WAVES - 1) / (cap * WAVES));
+        extra = (int)((rows + (long)o.rm_rows_per_wave * WAVES - 1) / ((long)o.rm_rows_per_wave * WAVES));
     }
-    hipLaunchKernelGGL((lookup_bwd_fold_kernel<S, 0, SEP>), dim3((unsigned)(o.nfold + extra)), dim3(64 * kFusedLv), bytes, s,
-                       lk, o);
+    hipLaunchKernelGGL((lookup_bwd_fold_kernel<S, 0, SEP>), dim3((unsigned)(o.nfold + extra)), dim3(64 * WAVES), bytes,
+                       s, lk, o);
     return hipGetLastError();
 }
 }  // namespace

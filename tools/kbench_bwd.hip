@@ -91,6 +91,11 @@ int main(int argc, char **argv) {
     // occupancy sensitivity of the lookup loop)
     FusedOut onm = o;  // the bf16x6 backward's fold: dC only, no maxima
     onm.rmax = nullptr, onm.cpart = nullptr;
+    FusedOut os = o;  // the separable kernel's LDS image (no per-wave staging)
+    const size_t bytes_sep = fused_lds_bytes<S, true>(H, W, L, &os);
+    FusedOut osnm = os;
+    osnm.rmax = nullptr, osnm.cpart = nullptr;
+    printf("separable: LDS %zu B per workgroup\n", bytes_sep);
     auto launch = [&](auto kern, int t_count, bool grid0 = false, size_t lds = 0, const FusedOut *oo = nullptr) {
         BwdLookups l2 = lk;
         l2.T = t_count;
@@ -102,12 +107,13 @@ int main(int argc, char **argv) {
     std::vector<V> vs;
     vs.push_back({"full T=12", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12); }, {}});
     vs.push_back({"full T=12, no maxima (bf16x6)", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12, false, 0, &onm); }, {}});
-    vs.push_back({"SEP full T=12, no maxima (bf16x6)", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, 0, &onm); }, {}});
-    vs.push_back({"SEP full T=12", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12); }, {}});
-    vs.push_back({"SEP full T=12, trailing LDS wait", [&] { launch(lookup_bwd_fold_kernel<S, 16, true>, 12); }, {}});
-    vs.push_back({"SEP full T=12, lookup 0 on the integer grid", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, true); }, {}});
-    vs.push_back({"SEP full T=1", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 1); }, {}});
-    vs.push_back({"SEP full T=1 on the integer grid", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 1, true); }, {}});
+    vs.push_back({"SEP full T=12, no maxima (bf16x6)", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, bytes_sep, &osnm); }, {}});
+    vs.push_back({"SEP full T=12", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, bytes_sep, &os); }, {}});
+    vs.push_back({"SEP full T=12, LDS padded to 3 WG/CU", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, 52 * 1024, &os); }, {}});
+    vs.push_back({"SEP full T=12, trailing LDS wait", [&] { launch(lookup_bwd_fold_kernel<S, 16, true>, 12, false, bytes_sep, &os); }, {}});
+    vs.push_back({"SEP full T=12, lookup 0 on the integer grid", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, true, bytes_sep, &os); }, {}});
+    vs.push_back({"SEP full T=1", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 1, false, bytes_sep, &os); }, {}});
+    vs.push_back({"SEP full T=1 on the integer grid", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 1, true, bytes_sep, &os); }, {}});
     vs.push_back({"full T=12, no maxima, cached dC", [&] { launch(lookup_bwd_fold_kernel<S, 8>, 12, false, 0, &onm); }, {}});
     vs.push_back({"no lookups, no maxima", [&] { launch(lookup_bwd_fold_kernel<S, 1>, 12, false, 0, &onm); }, {}});
     vs.push_back({"no lookups, no maxima, cached dC", [&] { launch(lookup_bwd_fold_kernel<S, 9>, 12, false, 0, &onm); }, {}});
