@@ -302,7 +302,7 @@ def run_e2e(args, world, rank, dev):
         res["cpu_baseline"] = cpu_e2e(model, im1, im2, finit, iters, args.cpu_seconds)
         res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
     if rank == 0:
-        print(json.dumps(res))
+        emit(res)
 
 
 def cpu_e2e(model, im1, im2, finit, iters, budget_s):
@@ -404,6 +404,16 @@ def build_roofline(algo, fl, bb, t_ms, traffic_b):
             "note": BUILD_NOTE[algo]}
 
 
+_JSON_OUT = None  # where the one JSON line goes (the process's stdout, see main)
+
+
+def emit(res):
+    """Print the result line (rank 0) on the original stdout."""
+    out = _JSON_OUT or sys.stdout
+    out.write(json.dumps(res) + "\n")
+    out.flush()
+
+
 def spawn_ranks(n):
     """`--gpus N` without a launcher: start N ranks of this script as child processes (RANK /
     LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, rendezvous on 127.0.0.1), before
@@ -453,6 +463,12 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
+        # stdout carries only the JSON line: native libraries' chatter on fd 1 (gloo prints its
+        # connection lines there) goes to stderr, the line to the saved original stdout
+        global _JSON_OUT
+        sys.stdout.flush()
+        _JSON_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # nccl = RCCL over xGMI; ERAFT_AMD_DIST_BACKEND=gloo rehearses the multi-rank path with
         # several ranks on ONE GPU (RCCL refuses two ranks per device)
@@ -475,7 +491,7 @@ def main():
             if rank == 0:
                 res["sharded_hires1280"] = leg
         if rank == 0:
-            print(json.dumps(res))
+            emit(res)
     if world > 1:
         dist.destroy_process_group()
 

@@ -90,6 +90,7 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (const Shape &sh : shapes) {
+        if (argc > 2 && std::string(argv[2]) != sh.name) continue;  // one shape (PMC passes)
         const size_t N = (size_t)sh.H * sh.W, BN = (size_t)sh.B * N;
         size_t off[4], tot = 0;
         for (int l = 0; l < 4; ++l) {
@@ -130,6 +131,12 @@ int main(int argc, char **argv) {
         vs.push_back({"QB16 cached-stores", [=](float *o) { return launch_qb<16, 8>(lp, coords, B, H, W, o); }, {}});
         vs.push_back({"QB32 cached-stores", [=](float *o) { return launch_qb<32, 8>(lp, coords, B, H, W, o); }, {}});
         CK(vs[0].launch(ref));
+        if (argc > 3) {  // one variant (PMC passes)
+            std::vector<Variant> keep;
+            for (auto &v : vs)
+                if (v.name == argv[3]) keep.push_back(v);
+            vs = keep;
+        }
         float *ref_g;  // the integer-grid coords' reference (production launch)
         CK(hipMalloc(&ref_g, n_out * 4));
         CK(launch_lookup(lp, coords_g, B, H * W, H, W, 4, 4, ref_g, 0));
