@@ -258,10 +258,14 @@ int corr_build_bwd_ex(int algo, const float *grad_c, const float *fmap1_rows, in
  *     every level in 160 KiB: e.g. r = 4 up to 60x80 fmaps), the lookups and the fold run as ONE
  *     kernel whose gradient maps live in LDS and which writes only dC (plus dC's row maxima and
  *     per-workgroup column maxima for the F16X3 packs; BF16X6 needs none); otherwise corr_lookup_bwd_multi +
- *     corr_pool_fold.  At radius 4 the fused kernel sums a regular window's cells separably (the
- *     column's two x-taps first, then the y-taps: the same four (tap, corner) terms per cell with
- *     the reference's per-tap weights, rounded in another order — dC within ~1e-7 norm-relative of
- *     the staged path); algo | CORR_BACKWARD_EXACT_FOLD makes it replay grid_sampler_2d_backward's
+ *     corr_pool_fold.  At radius 4 the fused kernel sums a window's cells separably (the column's
+ *     x-taps first, then the y-taps: the same (tap, corner) terms per cell with the reference's
+ *     per-tap weights, rounded in another order — dC within ~1e-7 norm-relative of the staged
+ *     path; windows whose taps are not all on a regular grid, e.g. the cold-start integer grid,
+ *     by the general form with four slots per tap; a window with a corner outside its
+ *     neighbourhood, or in a wave holding a non-finite upstream gradient, by the reference's
+ *     sequential scatter, so infinities give the staged path's inf / NaN cells);
+ *     algo | CORR_BACKWARD_EXACT_FOLD makes it replay grid_sampler_2d_backward's
  *     per-tap products instead, bit-identical to corr_lookup_bwd_multi + corr_pool_fold (as every
  *     other radius and the non-fused path always are).  Workspace: corr_backward_workspace
  *     (radius sizes the column-maxima partials; the flag does not change it).
