@@ -110,6 +110,9 @@ int main(int argc, char **argv) {
     vs.push_back({"SEP full T=12, no maxima (bf16x6)", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, bytes_sep, &osnm); }, {}});
     vs.push_back({"SEP full T=12", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, bytes_sep, &os); }, {}});
     vs.push_back({"SEP full T=12, LDS padded to 3 WG/CU", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, 52 * 1024, &os); }, {}});
+    // "cold": the upstream gradients evicted from the MALL before each launch (a 512 MB memset in
+    // between, outside the timed region)
+    vs.push_back({"SEP full T=12, cold", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, bytes_sep, &os); }, {}});
     vs.push_back({"SEP full T=12, trailing LDS wait", [&] { launch(lookup_bwd_fold_kernel<S, 16, true>, 12, false, bytes_sep, &os); }, {}});
     vs.push_back({"SEP full T=12, lookup 0 on the integer grid", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, true, bytes_sep, &os); }, {}});
     vs.push_back({"SEP full T=1", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 1, false, bytes_sep, &os); }, {}});
@@ -140,8 +143,26 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e1));
     for (auto &v : vs) v.run();
     CK(hipDeviceSynchronize());
+    void *flush;
+    const size_t flush_bytes = 512ull << 20;
+    CK(hipMalloc(&flush, flush_bytes));
     for (int r = 0; r < rounds; ++r)
         for (auto &v : vs) {
+            if (v.name.find("cold") != std::string::npos) {
+                float tot = 0.f;
+                for (int i = 0; i < PER; ++i) {
+                    CK(hipMemsetAsync(flush, i + r, flush_bytes, 0));
+                    CK(hipEventRecord(e0, 0));
+                    v.run();
+                    CK(hipEventRecord(e1, 0));
+                    CK(hipEventSynchronize(e1));
+                    float ms;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    tot += ms;
+                }
+                v.us.push_back(tot * 1e3f / PER);
+                continue;
+            }
             CK(hipEventRecord(e0, 0));
             for (int i = 0; i < PER; ++i) v.run();
             CK(hipEventRecord(e1, 0));
