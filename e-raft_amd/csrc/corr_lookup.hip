@@ -1137,11 +1137,12 @@ __global__ __launch_bounds__(lookup_bwd_threads(S, BQ)) void lookup_bwd_kernel(B
 // the fold.  Per lookup: lanes cx < S compute tap cx of both axes; the closed form takes the
 // group's other taps by DPP (row_newbcast for the y-taps and the anchors, row_shr for x-tap
 // cx - 1 and its gradients), so a regular lookup touches LDS only for its cells.  Lane cx then
-// produces its column's cells — closed form (regular taps), contiguous hit ranges (irregular),
-// or, when a corner leaves the (S+2)^2 neighbourhood, lookup_bwd_kernel's sequential scatter
-// into a zeroed window scratch (these two read every tap and gradient from the wave's LDS
-// staging, written only when some group of the wave needs it) — and adds them to the map
-// (branchless: out-of-map cells go to a per-lane dump slot).
+// produces its column's cells — closed form (regular taps), contiguous hit ranges (irregular;
+// separable: the general separable form), or, when a corner leaves the (S+2)^2 neighbourhood,
+// lookup_bwd_kernel's sequential scatter into a zeroed window scratch (the exact kernel reads
+// every tap and gradient for these from the wave's LDS staging, written only when some group of
+// the wave needs it; the separable kernel has no staging and shuffles them) — and adds them to
+// the map (out-of-map cells: clamped into guard rows, or a per-lane dump slot).
 constexpr int kFusedLv = 4;  // level slots (= waves) per workgroup
 
 // median of three (v_med3_i32: clang does not form it from min / max with runtime bounds)
