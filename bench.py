@@ -18,7 +18,10 @@ W warmup steps, untimed replays continue for 0.25 s (settle()).  Separately, HIP
 launch stream bracket graphs of the build alone and of the 12 lookups alone, giving the build
 kernels' average durations (-> MFMA roofline) and the per-lookup average (-> HBM roofline).
 Rank 0 at N=1 also times the reference op sequence on the host CPU (oracle/torch_ops.py) on
-a bounded sample: ``cpu_baseline``.
+a bounded sample: ``cpu_baseline``.  At N=1 the DSEC line also carries ``workloads``: the same
+measurement (value, ms_per_step, roofline, roofline_lookup; train: backward_kernels; train and
+mvsec: cpu_baseline) for BASELINE config 4 (train, B8 36x48 forward + backward), config 3
+(mvsec, B16 36x44) and config 5's 1280x960 size (hires1280), each in the same process.
 """
 from __future__ import annotations
 
@@ -92,6 +95,16 @@ WORKLOADS = {
 }
 CPU_SKIP = {"hires1280", "hires1920"}  # a CPU pair takes tens of seconds and >10 GB
 TRAIN_WORKLOADS = {"train"}
+# The default (DSEC) line also measures these BASELINE configs, one `workloads` entry each
+# (config 4 train, config 3 MVSEC B16, config 5's 1280x960 size), so the driver's own run times
+# them; --no-workloads skips them.
+EXTRA_WORKLOADS = ("train", "mvsec", "hires1280")
+ACHIEVABLE_HBM_GBS = 6290.0  # MI355X_MICROARCH.md: measured achievable HBM read bandwidth
+# The lookup's measured latency floor per workload: the same launch with neither the window
+# loads nor the output stores (coords load, taps, barriers, graph launch), i.e. what no change of
+# memory traffic can remove (tools/kbench_lookup.hip "abl QB32 noload nostore",
+# profiles/r05t_kbench_lookup_ablations.txt, median us).
+LOOKUP_NOLOAD_NOSTORE_US = {"dsec": 4.19, "mvsec": 11.49, "train": 6.86, "hires1280": 8.54}
 
 
 def parse():
@@ -115,6 +128,8 @@ def parse():
                          "(pair k+1's broadcast during pair k; eager)")
     ap.add_argument("--no-sharded-leg", action="store_true",
                     help="N > 1 dsec: skip the row-sharded 1280x960 leg reported beside the replica value")
+    ap.add_argument("--no-workloads", action="store_true",
+                    help="N = 1 dsec: skip the train / mvsec / hires1280 entries of `workloads`")
     return ap.parse_args()
 
 
@@ -404,6 +419,31 @@ def build_roofline(algo, fl, bb, t_ms, traffic_b):
             "note": BUILD_NOTE[algo]}
 
 
+def lookup_ceiling(wl_name, lb, look_ms, traffic_b):
+    """What bounds the lookup short of 8 TB/s, stated as ceilings on `frac`:
+    latency_floor — the launch without window loads or output stores (measured, see
+    LOOKUP_NOLOAD_NOSTORE_US): algorithmic bytes / that time is the best the kernel's fixed
+    chain allows; line_granularity — the window gather moves whole 128-B lines, so the counted
+    HBM traffic per launch (PMC) exceeds the algorithmic bytes: at the achievable 6.29 TB/s the
+    algorithmic rate is at most (algorithmic / counted) x 6.29 TB/s.  `binding` is the lower."""
+    out = {}
+    fl = LOOKUP_NOLOAD_NOSTORE_US.get(wl_name)
+    if fl:
+        gbs = lb / (fl * 1e-6) / 1e9
+        out["latency_floor"] = {"noload_nostore_us": fl, "frac": round(gbs / PEAK_HBM_GBS, 4),
+                                "source": "profiles/r05t_kbench_lookup_ablations.txt"}
+    if traffic_b:
+        r = min(1.0, lb / traffic_b)
+        out["line_granularity"] = {"algorithmic_over_counted": round(r, 4),
+                                   "frac": round(r * ACHIEVABLE_HBM_GBS / PEAK_HBM_GBS, 4)}
+    if out:
+        name, c = min(out.items(), key=lambda kv: kv[1]["frac"])
+        frac = lb / (look_ms * 1e-3) / 1e9 / PEAK_HBM_GBS
+        out["binding"] = name
+        out["frac_of_ceiling"] = round(frac / c["frac"], 4)
+    return out
+
+
 _JSON_OUT = None  # where the one JSON line goes (the process's stdout, see main)
 
 
@@ -481,11 +521,26 @@ def main():
         run_e2e(args, world, rank, dev)
     else:
         res = run_corr(args, args.workload, args.sharded, world, rank, dev)
+        if world == 1 and not args.sharded and args.workload == "dsec" and not args.no_workloads:
+            # BASELINE configs 3, 4 and 5 measured in the same (driver) run, beside `value`
+            res["workloads"] = {}
+            for wl in EXTRA_WORKLOADS:
+                torch.cuda.empty_cache()
+                t_w = time.perf_counter()
+                try:
+                    ent = run_corr(args, wl, False, world, rank, dev, role="workload")
+                    for k in ("metric", "unit", "n_gpus", "higher_is_better", "vs_baseline", "data", "dtype",
+                              "scaling", "build_arith", "kernel_timing", "warmup"):
+                        ent.pop(k, None)
+                except Exception as exc:  # noqa: BLE001 — the DSEC line stands; say why the entry is missing
+                    ent = {"error": f"{type(exc).__name__}: {exc}"}
+                ent["wall_s"] = round(time.perf_counter() - t_w, 2)
+                res["workloads"][wl] = ent
         if world > 1 and not args.sharded and args.workload == "dsec" and not args.no_sharded_leg:
             # the north_star's scaling case beside the replica value: ONE 1280x960 pair row-sharded
             # over the N ranks (chunked RCCL broadcast of fmap2, graph-captured), strong scaling
             try:
-                leg = run_corr(args, "hires1280", True, world, rank, dev, primary=False)
+                leg = run_corr(args, "hires1280", True, world, rank, dev, role="leg")
             except Exception as exc:  # noqa: BLE001 — the replica line above stands; say why the leg is missing
                 leg = {"error": f"{type(exc).__name__}: {exc}"}
             if rank == 0:
@@ -496,9 +551,12 @@ def main():
         dist.destroy_process_group()
 
 
-def run_corr(args, wl_name, sharded, world, rank, dev, primary=True):
-    """One CorrBlock workload: returns the result dict on rank 0 (None elsewhere).  primary=False
-    (the sharded leg of an N > 1 run): no alternative builds, no CPU baseline."""
+def run_corr(args, wl_name, sharded, world, rank, dev, role="primary"):
+    """One CorrBlock workload: returns the result dict on rank 0 (None elsewhere).  role "leg"
+    (the sharded leg of an N > 1 run): no alternative builds, no CPU baseline; "workload" (an
+    entry of the DSEC line's `workloads`): no alternative builds, CPU baselines on half the
+    sample budget."""
+    primary = role == "primary"
     from eraft_amd import CorrBlock, _lib
     from eraft_amd.corr import _alloc_grad_pyramid, _alloc_pyramid
 
@@ -805,7 +863,8 @@ def run_corr(args, wl_name, sharded, world, rank, dev, primary=True):
                                 "achieved": round(look_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                 "frac": round(look_gbs / PEAK_HBM_GBS, 4),
                                 "traffic": traffic(wl_name, "lookup_kernel"),
-                                "avg_us": round(look_ms * 1e3, 3), "bytes_per_launch": lb},
+                                "avg_us": round(look_ms * 1e3, 3), "bytes_per_launch": lb,
+                                "ceiling": lookup_ceiling(wl_name, lb, look_ms, traffic(wl_name, "lookup_kernel"))},
             "kernel_timing": "HIP events around 10 back-to-back launches of one kernel in one HIP graph on "
                              "the launch stream, median of 5: the gaps between dependent launches of DIFFERENT "
                              "kernels are not in avg_us (the build's pack -> MFMA boundary is in "
@@ -860,11 +919,12 @@ def run_corr(args, wl_name, sharded, world, rank, dev, primary=True):
                 "backend": os.environ.get("ERAFT_AMD_DIST_BACKEND", "nccl")}
         if capture_error is not None:
             res["capture_error"] = capture_error
-        if primary and world == 1 and not args.no_cpu_baseline and wl_name not in CPU_SKIP:
-            cb = cpu_baseline(wl, args.cpu_seconds, train)
+        if role != "leg" and world == 1 and not args.no_cpu_baseline and wl_name not in CPU_SKIP:
+            budget = args.cpu_seconds * (1.0 if primary else 0.5)
+            cb = cpu_baseline(wl, budget, train)
             res["cpu_baseline"] = cb
             res["speedup_vs_cpu"] = round(value / cb["value"], 1)
-            res["cpu_baseline_1thread"] = cpu_baseline(wl, args.cpu_seconds * 0.75, train, threads=1)
+            res["cpu_baseline_1thread"] = cpu_baseline(wl, budget * 0.75, train, threads=1)
         return res
     return None
 

@@ -163,15 +163,18 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
 }
 
 // Sum split-K slabs in split order, scale, write C[b][m][n] (ldc = Nn, batch stride sC).
+// fix.K > 0: outputs that come out NaN are recomputed in fp32 (NanFix, corr_common.h).
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restrict__ ws,
                                                             float *__restrict__ C, int splits,
                                                             size_t per_split, float alpha,
-                                                            int exact_mul, float s) {
+                                                            int exact_mul, float s, NanFix fix) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < per_split;
          i += (size_t)gridDim.x * blockDim.x) {
         float acc = ws[i];
         for (int k = 1; k < splits; ++k) acc = acc + ws[(size_t)k * per_split + i];
-        C[i] = exact_mul ? acc * alpha : acc / s;
+        acc = exact_mul ? acc * alpha : acc / s;
+        if (fix.K && __builtin_expect(acc != acc, 0)) acc = nanfix_flat(fix, i);
+        C[i] = acc;
     }
 }
 
@@ -180,7 +183,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float *__restr
 __global__ __launch_bounds__(256) void splitk_reduce_vec4_kernel(const float4 *__restrict__ ws,
                                                                  float4 *__restrict__ C, int splits,
                                                                  size_t per4, float alpha, int exact_mul,
-                                                                 float s) {
+                                                                 float s, NanFix fix) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < per4;
          i += (size_t)gridDim.x * blockDim.x) {
         float4 acc = ws[i];
@@ -192,6 +195,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_vec4_kernel(const float4 *_
             acc.x = acc.x * alpha, acc.y = acc.y * alpha, acc.z = acc.z * alpha, acc.w = acc.w * alpha;
         else
             acc.x = acc.x / s, acc.y = acc.y / s, acc.z = acc.z / s, acc.w = acc.w / s;
+        if (fix.K && __builtin_expect(acc.x != acc.x || acc.y != acc.y || acc.z != acc.z || acc.w != acc.w, 0)) {
+            if (acc.x != acc.x) acc.x = nanfix_flat(fix, 4 * i);
+            if (acc.y != acc.y) acc.y = nanfix_flat(fix, 4 * i + 1);
+            if (acc.z != acc.z) acc.z = nanfix_flat(fix, 4 * i + 2);
+            if (acc.w != acc.w) acc.w = nanfix_flat(fix, 4 * i + 3);
+        }
         C[i] = acc;
     }
 }
@@ -245,7 +254,7 @@ hipError_t run_gemm(bool b_kcontig, const float *A, const float *Bm, float *C, i
     const size_t per = (size_t)batch * M * Nn;
     const int grid = (int)std::min<size_t>((per + 255) / 256, 8192);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, stream, ws, C, p.splits, per,
-                       p.alpha, exact ? 1 : 0, s);
+                       p.alpha, exact ? 1 : 0, s, NanFix{});
     return hipGetLastError();
 }
 
@@ -253,17 +262,19 @@ hipError_t run_gemm(bool b_kcontig, const float *A, const float *Bm, float *C, i
 
 // Ordered split-K sum + 1/sqrt(D) for corr_bwd_split.hip's slabs ([split][per] floats).
 // vec4 = false: the scalar reduce (tools/kbench_gemm.hip A/B).
-hipError_t launch_splitk_reduce(const float *ws, float *C, int splits, size_t per, float sD, hipStream_t s, bool vec4) {
+hipError_t launch_splitk_reduce(const float *ws, float *C, int splits, size_t per, float sD, hipStream_t s, bool vec4,
+                                const NanFix *fix) {
+    const NanFix f = fix ? *fix : NanFix{};
     if (per % 4 == 0 && ((uintptr_t)ws & 15) == 0 && ((uintptr_t)C & 15) == 0 && vec4) {
         const size_t per4 = per / 4;
         const int grid = (int)std::min<size_t>((per4 + 255) / 256, 8192);
         hipLaunchKernelGGL(splitk_reduce_vec4_kernel, dim3(grid), dim3(256), 0, s, (const float4 *)ws, (float4 *)C,
-                           splits, per4, 1.0f / sD, is_pow2(sD) ? 1 : 0, sD);
+                           splits, per4, 1.0f / sD, is_pow2(sD) ? 1 : 0, sD, f);
         return hipGetLastError();
     }
     const int grid = (int)std::min<size_t>((per + 255) / 256, 8192);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, ws, C, splits, per, 1.0f / sD,
-                       is_pow2(sD) ? 1 : 0, sD);
+                       is_pow2(sD) ? 1 : 0, sD, f);
     return hipGetLastError();
 }
 

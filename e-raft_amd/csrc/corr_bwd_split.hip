@@ -334,8 +334,10 @@ __device__ __forceinline__ void split2(float x0, float x1, int s, bool guard, ha
 // (same binade, or |x| <= 2^-126 ... ), and so is the last difference, so x = hi + mid + lo bit for
 // bit — the same pieces as split3 wherever hi does not overflow; past M, hi = the bf16 maximum
 // and the residual carries the rest (split3 truncates there instead).  An infinite element
-// splits as (the clamped hi, inf, NaN), so every output it reaches is NaN where an fp32 GEMM
-// gives +-inf (documented with corr_build_bwd_ex; one accumulator cannot tell them apart).
+// splits as (the clamped hi, inf, NaN), so every output it reaches comes out of the MFMAs as NaN
+// (one accumulator cannot tell inf * 0 from a real NaN); the reduce / direct epilogue then
+// recompute exactly those outputs as the fp32 reference does (NanFix, corr_common.h), which
+// restores fp32's +-inf.
 __device__ __forceinline__ void split3_bwd(float a, float b, unsigned &hi, unsigned &mid, unsigned &lo) {
     constexpr float M = 3.3961775e38f;  // 0x7F7F7FFF
     float ha, hb, ma, mb, da, db;
@@ -395,6 +397,7 @@ struct FGemmParams {
     size_t tail_per4;
     int tail_splits, tail_exact, tail_wgs, gemm_wgs;
     float tail_alpha, tail_s;
+    NanFix fix, tail_fix;  // BF: NaN outputs recomputed in fp32 (direct epilogue; the tail reduce's GEMM)
 };
 
 // The tail reduce's share of workgroup t of p.tail_wgs (bit-identical to the separate reduce).
@@ -411,6 +414,12 @@ __device__ __forceinline__ void gemm_tail_reduce(const FGemmParams &p, int t) {
             acc.w = acc.w * p.tail_alpha;
         else
             acc.x = acc.x / p.tail_s, acc.y = acc.y / p.tail_s, acc.z = acc.z / p.tail_s, acc.w = acc.w / p.tail_s;
+        if (p.tail_fix.K && __builtin_expect(acc.x != acc.x || acc.y != acc.y || acc.z != acc.z || acc.w != acc.w, 0)) {
+            if (acc.x != acc.x) acc.x = nanfix_flat(p.tail_fix, 4 * i);
+            if (acc.y != acc.y) acc.y = nanfix_flat(p.tail_fix, 4 * i + 1);
+            if (acc.z != acc.z) acc.z = nanfix_flat(p.tail_fix, 4 * i + 2);
+            if (acc.w != acc.w) acc.w = nanfix_flat(p.tail_fix, 4 * i + 3);
+        }
         p.tail_C[i] = acc;
     }
 }
@@ -936,6 +945,8 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
                 const int i = i0 + il;
                 float x = BF ? acc[m][n][g] : ldexpf(acc[m][n][g], lex[il] + ej);
                 if (p.direct) x = x * p.alpha;
+                if (BF && p.direct && __builtin_expect(x != x, 0) && i < p.NI && j < p.NJ)
+                    x = nanfix_dot(p.fix, b, i, j);
                 if (i < p.NI && j < p.NJ) {
                     if (p.nt) __builtin_nontemporal_store(x, &C[(size_t)i * p.NJ + j]);
                     else C[(size_t)i * p.NJ + j] = x;
@@ -1048,6 +1059,7 @@ struct PendingReduce {
     int splits = 0;
     size_t per = 0;
     float sD = 1.f;
+    NanFix fix;
 };
 
 // CU count of the current device, looked up once per device (a process may drive parts with
@@ -1092,6 +1104,11 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     auto al16 = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
     p.vec = al16(A) && al16(Bm) && a_sb % 4 == 0 && a_sr % 4 == 0 && b_sb % 4 == 0 &&
             (BCOL ? b_sk % 4 == 0 : b_sr % 4 == 0);
+    if (bf) {  // the bf16x6 non-finite rule: NaN outputs recomputed as fp32 computes them
+        p.fix.A = A, p.fix.Bm = Bm, p.fix.a_sb = a_sb, p.fix.a_sr = a_sr;
+        p.fix.b_sb = b_sb, p.fix.b_sr = b_sr, p.fix.b_sk = b_sk;
+        p.fix.NI = NI, p.fix.NJ = NJ, p.fix.K = K, p.fix.s = sD;
+    }
     const bool dma = t.dma && p.vec && K % kBK == 0 && (!BCOL || NJ % 4 == 0);
     // 256-row tiles when there are more than 128 rows (D = 256): every staged element feeds twice
     // the MFMAs, a third less split work per MFMA (train: dF1 73 -> 67, dF2 75 -> 67 us)
@@ -1113,7 +1130,8 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
         const long slots = (long)device_cus() * per_cu;
         if (tail && tail->ws && grid + 16 > slots) {
             // no idle slots in the first round: the sum runs as its own launch, before this GEMM
-            hipError_t e3 = launch_splitk_reduce(tail->ws, tail->C, tail->splits, tail->per, tail->sD, s, true);
+            hipError_t e3 = launch_splitk_reduce(tail->ws, tail->C, tail->splits, tail->per, tail->sD, s, true,
+                                                 &tail->fix);
             if (e3 != hipSuccess) return e3;
         } else if (tail && tail->ws) {
             tail_wgs = slots - grid;
@@ -1125,6 +1143,7 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
             q.tail_alpha = 1.0f / tail->sD;
             q.tail_s = tail->sD;
             q.tail_wgs = (int)tail_wgs;
+            q.tail_fix = tail->fix;
         }
         static std::atomic<unsigned long long> done{0};
         hipError_t e2 = ensure_lds_limit((const void *)split_gemm_f32_kernel<BCOL, D, WI, P, BF>,
@@ -1149,9 +1168,10 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     const size_t per = (size_t)B * NI * NJ;
     if (defer && t.reduce_vec4 && per % 4 == 0 && al16(slab) && al16(C)) {
         defer->ws = slab, defer->C = C, defer->splits = p.splits, defer->per = per, defer->sD = sD;
+        defer->fix = p.fix;
         return hipSuccess;
     }
-    return launch_splitk_reduce(slab, C, p.splits, per, sD, s, t.reduce_vec4);
+    return launch_splitk_reduce(slab, C, p.splits, per, sD, s, t.reduce_vec4, &p.fix);
 }
 
 // rowmax_done: F2's and F1's row maxima are already in w.mxA / w.mxA2 (computed by the fold

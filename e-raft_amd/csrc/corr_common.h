@@ -50,6 +50,35 @@ __host__ __device__ inline unsigned map_row4(int y, int t, int TC) { return map_
 // opposite infinities reach it as NaN), so an infinite leading sum is the result.
 __device__ inline float split_sum(float hi, float lo) { return __builtin_isinf(hi) ? hi : hi + lo; }
 
+// The bf16x6 backward GEMMs' non-finite rule.  C[b][i][j] = sum_k A[b][i][k] Bm[b][j][k] / s runs
+// on exact three-piece bf16 splits into ONE accumulator, so an infinite operand element meets
+// zero pieces of the other operand (inf * 0 = NaN) and every output it reaches comes out NaN
+// where the reference's fp32 matmul gives +-inf (autograd of model/corr.py:58-60).  The split-K
+// reduce (and the direct epilogue) therefore recompute exactly the outputs that came out NaN as
+// the reference does — dmatmul = dC / sqrt(D) elementwise, then a plain fp32 dot product — so
+// NaN stays NaN where fp32 has one (a NaN operand, inf * 0, opposite infinities) and the rest
+// become fp32's +-inf.  Finite inputs never reach it (no NaN), so their bits are unchanged.
+// K = 0: off (the fp32-operand and f16x3 GEMMs).
+struct NanFix {
+    const float *A = nullptr, *Bm = nullptr;
+    long a_sb = 0, a_sr = 0, b_sb = 0, b_sr = 0, b_sk = 0;
+    int NI = 0, NJ = 0, K = 0;
+    float s = 1.f;  // sqrt(D): the reference divides dC by it before the matmul
+};
+__device__ __noinline__ inline float nanfix_dot(const NanFix &f, int b, int i, int j) {
+    const float *a = f.A + (size_t)b * f.a_sb + (size_t)i * f.a_sr;
+    const float *m = f.Bm + (size_t)b * f.b_sb + (size_t)j * f.b_sr;
+    float acc = 0.f;
+    for (int k = 0; k < f.K; ++k) acc = fmaf(a[k], m[(size_t)k * f.b_sk] / f.s, acc);
+    return acc;
+}
+// The same for flat output index e of C [B][NI][NJ].
+__device__ __noinline__ inline float nanfix_flat(const NanFix &f, size_t e) {
+    const size_t per = (size_t)f.NI * f.NJ;
+    const size_t r = e % per;
+    return nanfix_dot(f, (int)(e / per), (int)(r / f.NJ), (int)(r % f.NJ));
+}
+
 // Set the thread-local error and return `code`.
 int fail(int code, const char *fmt, ...);
 // Map a HIP status to CORR_OK / CORR_EHIP (recording the message).
@@ -104,8 +133,9 @@ hipError_t launch_build_bf16_region(const float *f1, int NQ, const float *f2_row
                                     int H, int W, int levels, const LevelPtrs &pyr, void *ws, bool pack_q,
                                     hipStream_t s);
 // Ordered split-K sum + 1/sqrt(D) of [splits][per] partial slabs into C (corr_bwd.hip).
+// fix: the bf16x6 GEMMs' NaN recompute (NanFix), or null.
 hipError_t launch_splitk_reduce(const float *ws, float *C, int splits, size_t per, float sD, hipStream_t s,
-                                bool vec4 = true);
+                                bool vec4 = true, const NanFix *fix = nullptr);
 size_t build_bwd_split_workspace(int B, int D, int NQ, int H, int W);
 hipError_t launch_build_bwd_split(const float *grad_c, const float *f1, int NQ, const float *f2, int B, int D, int H,
                                   int W, float *df1, float *df2, void *ws, hipStream_t s, bool bf);

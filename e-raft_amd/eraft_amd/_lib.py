@@ -174,6 +174,32 @@ def _ptrs(ts, name):
     return arr
 
 
+TILE_W = 4  # cells per tile row (include/corr_mi355x.h): tiles of 4 rows x TILE_W cells
+
+
+def map_floats(Hl: int, Wl: int) -> int:
+    """Floats of one query's tiled level map (include/corr_mi355x.h, corr_map_floats)."""
+    return ((Hl + 3) // 4) * ((Wl + TILE_W - 1) // TILE_W) * 4 * TILE_W
+
+
+def _check_levels(levels, BN: int, H: int, W: int, name: str, tiled: bool = True, exact: bool = False):
+    """Every level tensor must hold the BN maps the library will read or write: BN * map_floats
+    of the level for the tiled value pyramid, BN * H_l * W_l for the row-major ones (gradient
+    pyramids, the reference-layout export).  The C-ABI takes bare pointers, so a short buffer
+    (e.g. a caller still allocating the ABI-104 row-major [B*N, 1, H_l, W_l] value levels, which
+    are smaller than the tiled maps whenever H_l or W_l is not a multiple of 4) would be an
+    out-of-bounds device access: refuse it here."""
+    if not 1 <= len(levels) <= MAX_LEVELS:
+        raise ValueError(f"{name}: {len(levels)} levels (1..{MAX_LEVELS} supported)")
+    for l, t in enumerate(levels):
+        h, w = H >> l, W >> l
+        need = BN * (map_floats(h, w) if tiled else h * w)
+        n = t.numel()
+        if n < need or (exact and n != need):
+            what = f"{BN} maps of {'map_floats' if tiled else 'H_l*W_l'}({h}, {w})"
+            raise ValueError(f"{name}[{l}] has {n} floats, needs {'exactly ' if exact else ''}{need} ({what})")
+
+
 def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
@@ -190,9 +216,13 @@ def pyramid_export(levels, H, W, out=None):
     """corr_pyramid_export: the tiled levels ([BN, map_floats]) -> the reference's layout, a list
     of [BN, 1, H_l, W_l] tensors (allocated unless `out` is given)."""
     BN = levels[0].shape[0]
+    _check_levels(levels, BN, H, W, "pyr")
     if out is None:
         out = [torch.empty((BN, 1, H >> l, W >> l), dtype=torch.float32, device=levels[0].device)
                for l in range(len(levels))]
+    elif len(out) != len(levels):
+        raise ValueError(f"out has {len(out)} levels, the pyramid {len(levels)}")
+    _check_levels(out, BN, H, W, "out", tiled=False, exact=True)
     with torch.cuda.device(levels[0].device):
         _check(load().corr_pyramid_export(_ptrs(levels, "pyr"), BN, H, W, len(levels), _ptrs(out, "out"),
                                           _stream(levels[0])))
@@ -204,9 +234,12 @@ def pyramid_import(src, levels, H, W):
     the tiled `levels` (padding cells zeroed)."""
     BN = levels[0].shape[0]
     src = [t.contiguous() for t in src]
+    if len(src) != len(levels):
+        raise ValueError(f"src has {len(src)} levels, the pyramid {len(levels)}")
     for l, t in enumerate(src):
         if t.numel() != BN * (H >> l) * (W >> l):
             raise ValueError(f"level {l} has {t.numel()} values, expected {BN}x{H >> l}x{W >> l}")
+    _check_levels(levels, BN, H, W, "pyr")
     with torch.cuda.device(levels[0].device):
         _check(load().corr_pyramid_import(_ptrs(src, "src"), BN, H, W, len(levels), _ptrs(levels, "pyr"),
                                           _stream(levels[0])))
@@ -232,6 +265,7 @@ def build(fmap1, fmap2, levels, algo=None, workspace=None):
     algo = default_algo() if algo is None else algo
     B, D, H, W = fmap2.shape
     a, b, pp = _dev(fmap1, "fmap1"), _dev(fmap2, "fmap2"), _ptrs(levels, "pyr")
+    _check_levels(levels, B * _nq(fmap1), H, W, "pyr")
     if workspace is None:
         workspace = build_workspace(fmap1, fmap2, algo & 0xff)
     wp = 0 if workspace is None else workspace.data_ptr()
@@ -251,6 +285,7 @@ def build_region(fmap1, fmap2_rows, y0, y1, H, levels, workspace, pack_queries, 
     if rows != y1 - y0:
         raise ValueError(f"fmap2_rows has {rows} rows for the region [{y0}, {y1})")
     a, b, pp = _dev(fmap1, "fmap1"), _dev(fmap2_rows, "fmap2_rows"), _ptrs(levels, "pyr")
+    _check_levels(levels, B * _nq(fmap1), H, W, "pyr")
     with torch.cuda.device(fmap1.device):
         _check(load().corr_build_region(algo, a, _nq(fmap1), b, y0, y1, B, D, H, W, len(levels), pp,
                                         workspace.data_ptr(), workspace.numel() * workspace.element_size(),
@@ -264,6 +299,10 @@ def lookup(levels, coords, radius, out, H=None, W=None):
     H = coords.shape[2] if H is None else H
     W = coords.shape[3] if W is None else W
     pp, c, o = _ptrs(levels, "pyr"), _dev(coords, "coords"), _dev(out, "out")
+    _check_levels(levels, B * _nq(coords), H, W, "pyr")
+    K = (2 * radius + 1) ** 2
+    if out.numel() != B * len(levels) * K * _nq(coords):
+        raise ValueError(f"out has {out.numel()} floats, the lookup writes {B}x{len(levels) * K}x{_nq(coords)}")
     with torch.cuda.device(coords.device):
         _check(load().corr_lookup_rows(pp, c, B, _nq(coords), H, W, len(levels), radius, o,
                                        _stream(coords)))
@@ -274,6 +313,7 @@ def lookup_bwd(coords, grad_out, radius, grad_levels, H=None, W=None):
     H = coords.shape[2] if H is None else H
     W = coords.shape[3] if W is None else W
     c, g, gp = _dev(coords, "coords"), _dev(grad_out, "grad_out"), _ptrs(grad_levels, "grad_pyr")
+    _check_levels(grad_levels, B * _nq(coords), H, W, "grad_pyr", tiled=False)
     with torch.cuda.device(coords.device):
         _check(load().corr_lookup_bwd_rows(c, g, B, _nq(coords), H, W, len(grad_levels), radius, gp,
                                            _stream(coords)))
@@ -282,6 +322,7 @@ def lookup_bwd(coords, grad_out, radius, grad_levels, H=None, W=None):
 def pool_bwd(grad_levels, H, W):
     BN = grad_levels[0].shape[0]
     gp = _ptrs(grad_levels, "grad_pyr")
+    _check_levels(grad_levels, BN, H, W, "grad_pyr", tiled=False)
     with torch.cuda.device(grad_levels[0].device):
         _check(load().corr_pool_bwd(gp, BN, H, W, len(grad_levels), _stream(grad_levels[0])))
 
@@ -296,6 +337,8 @@ def build_bwd(grad_c, fmap1, fmap2, algo=None):
         _dev(t, nm)
     lib = load()
     NQ = _nq(fmap1)
+    if grad_c.numel() != B * NQ * H * W:
+        raise ValueError(f"grad_c has {grad_c.numel()} values, expected {B * NQ}x{H * W}")
     ws_bytes = lib.corr_build_bwd_ex_workspace(algo, B, D, NQ, H, W)
     if ws_bytes == ctypes.c_size_t(-1).value:
         raise CorrError(CORR_EUNSUPPORTED, f"unknown backward algorithm {algo}")
@@ -317,6 +360,7 @@ def lookup_bwd_multi(coords_list, grad_list, radius, grad_levels, H=None, W=None
     H = c0.shape[2] if H is None else H
     W = c0.shape[3] if W is None else W
     cp, gp = _ptrs(coords_list, "coords"), _ptrs(grad_list, "grad_out")
+    _check_levels(grad_levels, B * _nq(c0), H, W, "grad_pyr", tiled=False)
     with torch.cuda.device(c0.device):
         _check(load().corr_lookup_bwd_multi(cp, gp, len(coords_list), B, _nq(c0), H, W, len(grad_levels), radius,
                                             _ptrs(grad_levels, "grad_pyr"), _stream(c0)))
@@ -325,6 +369,7 @@ def lookup_bwd_multi(coords_list, grad_list, radius, grad_levels, H=None, W=None
 def pool_fold(grad_levels, B, H, W):
     """corr_pool_fold: the pool-backward chain folded into grad_levels[0] in one pass."""
     NQ = grad_levels[0].shape[0] // B
+    _check_levels(grad_levels, B * NQ, H, W, "grad_pyr", tiled=False)
     with torch.cuda.device(grad_levels[0].device):
         _check(load().corr_pool_fold(_ptrs(grad_levels, "grad_pyr"), B, NQ, H, W, len(grad_levels),
                                      _stream(grad_levels[0])))
@@ -352,6 +397,7 @@ def backward(coords_list, grad_list, radius, grad_levels, fmap1, fmap2, algo=Non
         algo |= BACKWARD_EXACT_FOLD
     if ws_bytes == ctypes.c_size_t(-1).value:
         raise CorrError(CORR_EUNSUPPORTED, f"unknown backward algorithm {algo}")
+    _check_levels(grad_levels, B * NQ, H, W, "grad_pyr", tiled=False)
     df1 = torch.empty_like(fmap1)
     df2 = torch.empty_like(fmap2)
     ws = torch.empty(max(1, (ws_bytes + 3) // 4), dtype=torch.float32, device=fmap1.device)
@@ -461,6 +507,7 @@ def lookup_conv(levels, coords, radius, packed, bias, out, relu=True):
     """corr_lookup_conv: fused lookup + 1x1 conv (+ReLU) -> out [B, 256, H, W]."""
     B, _, H, W = coords.shape
     pp, c = _ptrs(levels, "pyr"), _dev(coords, "coords")
+    _check_levels(levels, B * H * W, H, W, "pyr")
     pw, bs, o = _dev(packed, "packed_weight"), _dev(bias, "bias"), _dev(out, "out")
     with torch.cuda.device(coords.device):
         _check(load().corr_lookup_conv(pp, c, B, H, W, len(levels), radius, pw, bs, int(bool(relu)), o,
@@ -475,6 +522,7 @@ def lookup_conv_bwd(levels, coords, radius, packed, out, relu, grad_out, grad_we
     B, _, H, W = coords.shape
     lib = load()
     pp, c = _ptrs(levels, "pyr"), _dev(coords, "coords")
+    _check_levels(levels, B * H * W, H, W, "pyr")
     g = _dev(grad_out, "grad_out")
     o = _dev(out, "out") if relu else None
     opt = lambda t, name: None if t is None else _dev(t, name)

@@ -34,13 +34,36 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_library(force: bool = False, verbose: bool = False) -> str:
-    """Build the shared library if any source is newer than it.  Returns its path."""
+OBJ_DIR = os.path.join(OUT_DIR, "obj")
+
+
+def _compile(src: str, force: bool, verbose: bool) -> str:
+    """One translation unit -> _build/obj/<name>.o, rebuilt when it or a shared header is newer."""
+    obj = os.path.join(OBJ_DIR, os.path.splitext(src)[0] + ".o")
+    deps = [os.path.join(SRC, src)] + [os.path.join(SRC, h) for h in HEADERS] + [__file__]
+    if not force and os.path.exists(obj) and all(os.path.getmtime(d) <= os.path.getmtime(obj) for d in deps):
+        return obj
+    flags = [f for f in FLAGS if f != "-shared"]
+    cmd = [HIPCC, *flags, "-c", "-o", obj + ".tmp", os.path.join(SRC, src)]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(obj + ".tmp", obj)
+    return obj
+
+
+def build_library(force: bool = False, verbose: bool = False, jobs: int | None = None) -> str:
+    """Build the shared library if any source is newer than it (translation units compiled in
+    parallel, only the stale ones).  Returns its path."""
     if not force and not _stale():
         return SO_PATH
-    os.makedirs(OUT_DIR, exist_ok=True)
+    from concurrent.futures import ThreadPoolExecutor
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    jobs = jobs or min(len(SOURCES), int(os.environ.get("MAX_JOBS") or 0) or os.cpu_count() or 4, 16)
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force, verbose), SOURCES))
     tmp = SO_PATH + ".tmp"
-    cmd = [HIPCC, *FLAGS, "-o", tmp, *[os.path.join(SRC, s) for s in SOURCES]]
+    cmd = [HIPCC, "--offload-arch=gfx950", "-fPIC", "-shared", "-o", tmp, *objs]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -33,12 +33,8 @@ def level_shapes(H: int, W: int, num_levels: int):
     return [(H >> l, W >> l) for l in range(num_levels)]
 
 
-TILE_W = 4  # cells per tile row (include/corr_mi355x.h): tiles of 4 rows x TILE_W cells
-
-
-def map_floats(Hl: int, Wl: int) -> int:
-    """Floats of one query's tiled level map (include/corr_mi355x.h)."""
-    return ((Hl + 3) // 4) * ((Wl + TILE_W - 1) // TILE_W) * 4 * TILE_W
+TILE_W = _lib.TILE_W  # cells per tile row (include/corr_mi355x.h): tiles of 4 rows x TILE_W cells
+map_floats = _lib.map_floats  # floats of one query's tiled level map
 
 
 def _alloc_pyramid(B: int, H: int, W: int, num_levels: int, like: torch.Tensor, zero=False, NQ=None):
@@ -249,6 +245,9 @@ class _LookupConvFn(torch.autograd.Function):
         _lib.lookup_conv(levels, coords, radius, _weight_pack(weight), bias.detach().contiguous().float(), out, relu)
         ctx.save_for_backward(coords, weight, out)
         ctx.relu, ctx.radius, ctx.state = relu, radius, state
+        # the levels this output was made from (an assignment to corr_pyramid installs new ones),
+        # and whether the build is upstream (a constant pyramid's token carries no gradient)
+        ctx.levels, ctx.trains = levels, ctx.needs_input_grad[1]
         return out
 
     @staticmethod
@@ -259,17 +258,42 @@ class _LookupConvFn(torch.autograd.Function):
         if g.data_ptr() % 16:  # the kernel's 16-B loads need an aligned base (a view with an odd offset)
             g = g.clone()
         B, O, H, W = g.shape
-        C = len(st.levels) * (2 * ctx.radius + 1) ** 2
+        C = len(ctx.levels) * (2 * ctx.radius + 1) ** 2
         dev = coords.device
         dW = torch.empty((O, C), dtype=torch.float32, device=dev) if ctx.needs_input_grad[2] else None
         dbias = torch.empty((O,), dtype=torch.float32, device=dev) if ctx.needs_input_grad[3] else None
-        dlk = torch.empty((B, C, H, W), dtype=torch.float32, device=dev) if st.trains else None
-        _lib.lookup_conv_bwd(st.levels, coords, ctx.radius, _weight_pack(weight), out, ctx.relu, g, dW, dbias, dlk)
+        dlk = torch.empty((B, C, H, W), dtype=torch.float32, device=dev) if ctx.trains else None
+        _lib.lookup_conv_bwd(ctx.levels, coords, ctx.radius, _weight_pack(weight), out, ctx.relu, g, dW, dbias, dlk)
         if dlk is not None:  # the lookup's upstream gradient, for the build's backward
             _LookupFn.stash_backward(st, coords, dlk, ctx.radius)
         if dW is not None:
             dW = dW.view_as(weight).to(weight.dtype)
         return None, None, dW, dbias, None, None, None
+
+
+class _CorrFn(torch.autograd.Function):
+    """CorrBlock.corr under autograd.  The reference's static corr (corr.py:52-60) is a torch
+    matmul scaled by 1/sqrt(D), so gradients reach both feature maps; here the forward is the
+    one-level build exported to [B, H, W, 1, H, W] and the backward the library's GEMMs on dC
+    (corr_build_bwd_ex: dF1 = F2 dC^T / sqrt(D), dF2 = F1 dC / sqrt(D))."""
+
+    @staticmethod
+    def forward(ctx, fmap1, fmap2):
+        B, _, H, W = fmap1.shape
+        lvl = _alloc_pyramid(B, H, W, 1, fmap1)
+        _lib.build(fmap1, fmap2, lvl)
+        ctx.save_for_backward(fmap1, fmap2)
+        ctx.set_materialize_grads(False)
+        return _lib.pyramid_export(lvl, H, W)[0].view(B, H, W, 1, H, W)
+
+    @staticmethod
+    def backward(ctx, grad):
+        if grad is None:
+            return None, None
+        fmap1, fmap2 = ctx.saved_tensors
+        B, _, H, W = fmap1.shape
+        df1, df2 = _lib.build_bwd(grad.contiguous().view(B * H * W, H * W), fmap1, fmap2)
+        return (df1 if ctx.needs_input_grad[0] else None, df2 if ctx.needs_input_grad[1] else None)
 
 
 class CorrBlock:
@@ -286,7 +310,9 @@ class CorrBlock:
         _, _, H, W = fmap1.shape
         self._state = _State(H, W, radius)
         self._token = None
-        self._view = None  # corr_pyramid's exported levels, made on first access
+        self._view = None  # corr_pyramid's exported levels, made on first access ...
+        self._view_grad = False  # ... with (True) or without autograd
+        self._assigned = False  # corr_pyramid was assigned: later lookups carry no gradient
         if torch.is_grad_enabled() and (fmap1.requires_grad or fmap2.requires_grad):
             self._token = _BuildFn.apply(fmap1, fmap2, num_levels, self._state)
             self._state.trains = True
@@ -302,21 +328,38 @@ class CorrBlock:
         view is materialised (corr_pyramid_export) on first access; with the build in the autograd
         graph, gradients that reach it flow to both fmaps as in the reference.  Assigning a list
         of such tensors installs them (corr_pyramid_import) for the following lookups."""
-        if self._view is None:
-            st = self._state
-            if self._token is not None and torch.is_grad_enabled():
+        st = self._state
+        grad = self._token is not None and not self._assigned and torch.is_grad_enabled()
+        if self._view is None or (grad and not self._view_grad):
+            # (re-)export: a view first made under no_grad (or by inspection only) must not stand
+            # in for the differentiable one a later grad-enabled read needs
+            if grad:
                 self._view = list(_PyramidViewFn.apply(self._token, st))
             else:
                 self._view = _lib.pyramid_export(st.levels, st.H, st.W)
+            self._view_grad = grad
         return self._view
 
     @corr_pyramid.setter
     def corr_pyramid(self, levels):
+        """Install a pyramid for the following lookups (corr_pyramid_import).  As in the
+        reference, those lookups then read the assigned tensors, not the build: they send no
+        gradient to fmap1 / fmap2.  Gradients INTO assigned tensors that require grad are not
+        supported (the tiled copy is not in their graph): that raises instead of losing them."""
         st = self._state
         if len(levels) != len(st.levels):
             raise ValueError(f"corr_pyramid needs {len(st.levels)} levels (got {len(levels)})")
-        _lib.pyramid_import([l.detach() for l in levels], st.levels, st.H, st.W)
+        if torch.is_grad_enabled() and any(getattr(l, "requires_grad", False) for l in levels):
+            raise NotImplementedError("assigning corr_pyramid levels that require grad: gradients cannot "
+                                      "reach them through the tiled copy; assign detached levels")
+        B = st.levels[0].shape[0] // (st.H * st.W)
+        # a fresh buffer: a lookup_conv backward still pending reads the levels it was made from
+        fresh = _alloc_pyramid(B, st.H, st.W, len(st.levels), st.levels[0])
+        _lib.pyramid_import([l.detach() for l in levels], fresh, st.H, st.W)
+        st.levels = fresh
+        self._assigned = True
         self._view = None
+        self._view_grad = False
 
     def _check_coords(self, coords):
         if coords.dim() != 4 or coords.shape[1] != 2:
@@ -330,7 +373,7 @@ class CorrBlock:
         B, _, H, W = coords.shape
         # the reference accepts any strides (permute at corr.py:31); fp32 as in eraft.py:128
         coords = coords.detach().contiguous()
-        if self._token is not None and torch.is_grad_enabled():
+        if self._token is not None and not self._assigned and torch.is_grad_enabled():
             return _LookupFn.apply(coords, self._token, self.radius, self._state)
         K = (2 * self.radius + 1) ** 2
         out = torch.empty((B, self.num_levels * K, H, W), dtype=torch.float32, device=coords.device)
@@ -350,8 +393,9 @@ class CorrBlock:
             raise ValueError(f"lookup_conv needs weight [256, {C}, 1, 1] and bias [256] "
                              f"(got {tuple(weight.shape)}, {tuple(bias.shape)})")
         coords = coords.detach().contiguous()
-        if torch.is_grad_enabled() and (self._token is not None or weight.requires_grad or bias.requires_grad):
-            token = self._token
+        live = self._token is not None and not self._assigned
+        if torch.is_grad_enabled() and (live or weight.requires_grad or bias.requires_grad):
+            token = self._token if live else None
             if token is None:  # the pyramid is constant; gradients reach only the weight and bias
                 token = coords.new_empty(())
             return _LookupConvFn.apply(coords, token, weight, bias, relu, self.radius, self._state)
@@ -363,9 +407,13 @@ class CorrBlock:
 
     @staticmethod
     def corr(fmap1, fmap2):
-        """model/corr.py:52-60: all-pairs volume [B, H, W, 1, H, W] scaled by 1/sqrt(D)."""
+        """model/corr.py:52-60: all-pairs volume [B, H, W, 1, H, W] scaled by 1/sqrt(D);
+        differentiable w.r.t. both feature maps as the reference's matmul is (_CorrFn)."""
         _validate_fmaps(fmap1, fmap2, 1)
+        f1, f2 = fmap1.contiguous(), fmap2.contiguous()
+        if torch.is_grad_enabled() and (f1.requires_grad or f2.requires_grad):
+            return _CorrFn.apply(f1, f2)
         B, _, H, W = fmap1.shape
         lvl = _alloc_pyramid(B, H, W, 1, fmap1)
-        _lib.build(fmap1.detach().contiguous(), fmap2.detach().contiguous(), lvl)
+        _lib.build(f1.detach(), f2.detach(), lvl)
         return _lib.pyramid_export(lvl, H, W)[0].view(B, H, W, 1, H, W)

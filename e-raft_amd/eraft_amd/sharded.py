@@ -55,6 +55,11 @@ class HipRows:
 
     # target-row regions of one build (the chunked broadcast): allocate, then build region by region
     @staticmethod
+    def export(levels, H, W):
+        """The slab's tiled levels -> the reference layout [B*NQ, 1, H_l, W_l]."""
+        return _lib.pyramid_export(levels, H, W)
+
+    @staticmethod
     def region_supported(num_levels):
         return _lib.default_algo() == _lib.BUILD_BF16X6 and num_levels <= 4
 
@@ -138,13 +143,36 @@ def _broadcast_build_chunked(backend, f1_rows, fmap2, num_levels, bounds, src, g
 _CHUNKS_AGREED = {}
 
 
+def _group_key(group):
+    """A cache key for a process group that survives the group object: its backend and the
+    global ranks it spans (id() of a destroyed group can be reused by a new one)."""
+    ranks = tuple(dist.get_process_group_ranks(group)) if group is not None else tuple(range(dist.get_world_size()))
+    return (dist.get_backend(group), ranks)
+
+
+def agree_chunks(H, num_levels, chunks=0, group=None, device=None, region=True):
+    """The chunk count RowShardedCorrBlock(..., chunks=chunks) will use for H rows, agreed over
+    the group (a blocking all-reduce + host read).  The agreement runs the first time a
+    (group, H, levels, chunks) key is seen; call this once, eagerly, before capturing a
+    RowShardedCorrBlock construction into a HIP graph, since a capture cannot hold the host
+    read (bench.py's eager warm-up pair does the same)."""
+    local = chunks if chunks else (4 if region and H >= 32 else 1)
+    if not region:
+        local = 1
+    if dist.get_world_size(group) == 1:
+        return local
+    return _agreed_chunks(group, (H, num_levels, chunks), local, device)
+
+
 def _agreed_chunks(group, key, local, device):
     """The broadcast's chunk count, agreed over the group once per (group, key): the MIN of the
     ranks' own choices.  Each rank's choice depends on its environment (ERAFT_AMD_BUILD decides
     whether the region build exists), and ranks that disagreed would issue different numbers of
     broadcasts and hang.  key holds only values every rank shares (H, levels, the requested
-    count), so every rank hits or misses the cache together."""
-    k = (id(group), key)
+    count), so every rank hits or misses the cache together.  The first call for a key runs a
+    blocking all-reduce and a host read: it must not happen inside a graph capture (see
+    agree_chunks)."""
+    k = (_group_key(group), key)
     if k not in _CHUNKS_AGREED:
         t = torch.tensor([local], dtype=torch.int64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
@@ -364,14 +392,25 @@ class RowShardedCorrBlock:
             self._st = st
             src1 = fmap1 if st.full1 else f1.contiguous()
             self._token = _ShardBuildFn.apply(src1, fmap2, num_levels, st)
-            self.corr_pyramid = st.levels if self.h1 > self.h0 else None
+            self._levels = st.levels if self.h1 > self.h0 else None
             return
         if chunked:
             lv = _broadcast_build_chunked(backend, f1.contiguous(), fmap2, num_levels, bounds, src, group, self.rank)
-            self.corr_pyramid = lv if self.h1 > self.h0 else None
+            self._levels = lv if self.h1 > self.h0 else None
         else:
-            self.corr_pyramid = (backend.build(f1.contiguous(), fmap2, num_levels)
-                                 if self.h1 > self.h0 else None)
+            self._levels = (backend.build(f1.contiguous(), fmap2, num_levels)
+                            if self.h1 > self.h0 else None)
+
+    @property
+    def corr_pyramid(self):
+        """This rank's slab of the pyramid as the reference holds it (corr.py:16,24,27,36): a list
+        of [B*rows*W, 1, H_l, W_l] tensors (None on a rank without rows), exported from the
+        backend's internal levels on access as CorrBlock.corr_pyramid does (HipRows keeps them
+        tiled, include/corr_mi355x.h).  A read-only export: it carries no gradient."""
+        if self._levels is None:
+            return None
+        export = getattr(self.backend, "export", None)
+        return export(self._levels, self.H, self.W) if export is not None else self._levels
 
     @property
     def rows(self):
@@ -382,13 +421,13 @@ class RowShardedCorrBlock:
             coords = coords[:, :, self.h0:self.h1]
         coords = coords.contiguous()
         K = (2 * self.radius + 1) ** 2
-        if self.corr_pyramid is None:
+        if self._levels is None:
             out = coords.new_empty((self.B, self.num_levels * K, 0, self.W))
             # keep the rank in the autograd graph so its backward joins the all-reduce
             return out + self._token if self._token is not None and torch.is_grad_enabled() else out
         if self._token is not None and torch.is_grad_enabled():
             return _ShardLookupFn.apply(coords.detach(), self._token, self.radius, self._st)
-        return self.backend.lookup(self.corr_pyramid, coords, self.radius, self.H, self.W)
+        return self.backend.lookup(self._levels, coords, self.radius, self.H, self.W)
 
     def gather(self, out_rows):
         """All-gather the ranks' output rows into the full [B, L*K, H, W] tensor."""

@@ -226,9 +226,11 @@ int corr_build_bwd_rows(const float *grad_c, const float *fmap1_rows, int NQ, co
  * (6 roundings per 16 k, an fp32 fmaf chain 16): every element within (3 + 6 ceil(K/16) + splits)
  * u sum|ab| (an fp32 dot product: K u sum|ab|), worst and mean row error below the fp32 GEMMs',
  * checked against fp64 — but with one accumulator not every single row (unlike the build's).
- * Non-finite inputs: an infinite element of F1, F2 or dC splits as (clamped hi, inf, NaN), so
- * every output it reaches is NaN where an fp32 GEMM gives +-inf (NaN inputs give NaN as there;
- * finite inputs are unaffected; tests/test_gpu_parity.py::test_build_bwd_bf16x6_inf_gives_nan).
+ * Non-finite inputs give the fp32 reference's results: an output the split makes NaN (an
+ * infinite element meets zero pieces: inf * 0) is recomputed by the split-K reduce as the
+ * reference computes it (dC / sqrt(D), then an fp32 dot product), so it becomes +-inf where
+ * fp32 has +-inf and stays NaN where fp32 has NaN; finite inputs are unaffected
+ * (tests/test_gpu_parity.py::test_build_bwd_bf16x6_inf_matches_fp32).
  * CORR_BUILD_F16X3 packs F1, F2 (per feature row d) and dC (per query
  * row for dfmap1, per target column for dfmap2) as 2^e (hi + lo) f16 pairs and runs three f16
  * MFMAs per product (~2^-22 relative: narrower than fp32).  Split-K partial sums are reduced in

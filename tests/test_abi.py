@@ -213,3 +213,22 @@ def test_tiled_map_size_and_layout_validation(lib):
     assert rc == -1 and "BN" in lib.corr_last_error().decode()
     rc = lib.corr_pyramid_import(ok, 4800, 4, 80, 4, ok, None)
     assert rc == -1 and "too small" in lib.corr_last_error().decode()
+
+
+def test_python_level_size_check():
+    """the ctypes front-end refuses level buffers smaller than the maps the library
+    will touch (the C-ABI takes bare pointers): tiled value levels need BN * map_floats per
+    level, row-major gradient / export levels BN * H_l * W_l (exactly, for the export's out)."""
+    import torch
+    from eraft_amd import _lib
+    BN, H, W = 6, 30, 40
+    tiled = [torch.empty(BN * _lib.map_floats(H >> l, W >> l)) for l in range(3)]
+    _lib._check_levels(tiled, BN, H, W, "pyr")
+    rowmajor = [torch.empty(BN, 1, H >> l, W >> l) for l in range(3)]  # ABI-104 value levels: too small
+    with pytest.raises(ValueError, match=r"pyr\[0\] has 7200 floats, needs 7680"):
+        _lib._check_levels(rowmajor, BN, H, W, "pyr")
+    _lib._check_levels(rowmajor, BN, H, W, "out", tiled=False, exact=True)
+    with pytest.raises(ValueError, match="exactly"):
+        _lib._check_levels(tiled, BN, H, W, "out", tiled=False, exact=True)
+    with pytest.raises(ValueError, match="levels"):
+        _lib._check_levels(rowmajor * 3, BN, H, W, "pyr", tiled=False)

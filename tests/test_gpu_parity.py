@@ -171,6 +171,115 @@ def test_corr_staticmethod_shape_and_values():
     assert norm_rel(vol.reshape(B * H * W, 1, H, W).cpu().numpy(), g["pyr0"]) < REL_TOL
 
 
+def _ref_autograd(f1n, f2n, L, r, coords, grads, pyr_grads=None, vol_grad=None):
+    """fp64 torch-CPU autograd of the reference composition (oracle/torch_ops.py restates
+    model/corr.py:13-60 op by op): lookups with upstream gradients `grads`, plus optional loss
+    terms on the pyramid levels (corr_pyramid) and on the static corr volume."""
+    from oracle import torch_ops
+    a = torch.from_numpy(f1n).double().requires_grad_(True)
+    b = torch.from_numpy(f2n).double().requires_grad_(True)
+    loss = 0.0
+    if L:
+        lv = torch_ops.cpu_build(a, b, L)
+        for c, g in zip(coords, grads):
+            loss = loss + (torch_ops.cpu_lookup(lv, torch.from_numpy(c).double(), r) * torch.from_numpy(g).double()).sum()
+        for l, g in (pyr_grads or {}).items():
+            loss = loss + (lv[l] * torch.from_numpy(g).double()).sum()
+    if vol_grad is not None:
+        B, D, H, W = f1n.shape
+        vol = torch.matmul(a.reshape(B, D, H * W).transpose(1, 2), b.reshape(B, D, H * W)) / np.sqrt(D)
+        loss = loss + (vol.reshape(vol_grad.shape) * torch.from_numpy(vol_grad).double()).sum()
+    loss.backward()
+    return a.grad.numpy(), b.grad.numpy()
+
+
+@pytest.mark.parametrize("which", ["both", "fmap1", "fmap2"])
+def test_corr_staticmethod_is_differentiable(which):
+    """CorrBlock.corr (model/corr.py:52-60, a torch matmul) passes gradients to the
+    feature maps it requires them for, within the north_star's 1e-4 of fp64 autograd."""
+    B, D, H, W = 2, 48, 12, 16
+    f1n, f2n = prng.gauss(91, (B, D, H, W)), prng.gauss(92, (B, D, H, W))
+    G = prng.gauss(93, (B, H, W, 1, H, W))
+    t1 = torch.from_numpy(f1n).to(DEV).requires_grad_(which in ("both", "fmap1"))
+    t2 = torch.from_numpy(f2n).to(DEV).requires_grad_(which in ("both", "fmap2"))
+    vol = _cb().corr(t1, t2)
+    assert vol.requires_grad and tuple(vol.shape) == (B, H, W, 1, H, W)
+    (vol * torch.from_numpy(G).to(DEV)).sum().backward()
+    r1, r2 = _ref_autograd(f1n, f2n, 0, 0, [], [], vol_grad=G)
+    for t, ref in ((t1, r1), (t2, r2)):
+        if t.requires_grad:
+            assert norm_rel(t.grad.cpu().numpy(), ref) < REL_TOL
+        else:
+            assert t.grad is None
+    with torch.no_grad():  # and no graph under no_grad
+        assert not _cb().corr(t1, t2).requires_grad
+
+
+@pytest.mark.parametrize("lookups", [False, True])
+def test_corr_pyramid_gradients_match_reference(lookups):
+    """gradients that reach the exported corr_pyramid view (alone, and mixed with
+    lookups) match fp64 autograd of the reference composition (matmul / sqrt(D), avg_pool2d,
+    grid_sample) within 1e-4 — not only the per-lookup path."""
+    B, D, H, W, L, r = 1, 32, 16, 20, 3, 3
+    f1n, f2n = prng.gauss(94, (B, D, H, W)), prng.gauss(95, (B, D, H, W))
+    N = H * W
+    pg = {0: prng.gauss(96, (B * N, 1, H, W)), 2: prng.gauss(97, (B * N, 1, H >> 2, W >> 2))}
+    K = (2 * r + 1) ** 2
+    cs = [prng.lookup_coords(98 + t, B, H, W, 2.0) for t in range(2)] if lookups else []
+    gs = [prng.gauss(100 + t, (B, L * K, H, W)) for t in range(2)] if lookups else []
+    t1 = torch.from_numpy(f1n).to(DEV).requires_grad_(True)
+    t2 = torch.from_numpy(f2n).to(DEV).requires_grad_(True)
+    cb = _cb()(t1, t2, L, r)
+    loss = sum((cb.corr_pyramid[l] * torch.from_numpy(g).to(DEV)).sum() for l, g in pg.items())
+    for c, g in zip(cs, gs):
+        loss = loss + (cb(torch.from_numpy(c).to(DEV)) * torch.from_numpy(g).to(DEV)).sum()
+    loss.backward()
+    r1, r2 = _ref_autograd(f1n, f2n, L, r, cs, gs, pyr_grads=pg)
+    assert norm_rel(t1.grad.cpu().numpy(), r1) < REL_TOL
+    assert norm_rel(t2.grad.cpu().numpy(), r2) < REL_TOL
+
+
+def test_corr_pyramid_view_follows_grad_mode():
+    """a corr_pyramid first read under no_grad is re-exported for a later
+    grad-enabled read (which then carries gradients); an assigned pyramid makes later lookups
+    constant, as in the reference, and assigning levels that require grad raises."""
+    B, D, H, W, L, r = 1, 16, 12, 16, 2, 2
+    t1 = torch.from_numpy(prng.gauss(111, (B, D, H, W))).to(DEV).requires_grad_(True)
+    t2 = torch.from_numpy(prng.gauss(112, (B, D, H, W))).to(DEV).requires_grad_(True)
+    cb = _cb()(t1, t2, L, r)
+    with torch.no_grad():
+        v0 = cb.corr_pyramid
+    assert not v0[0].requires_grad
+    v1 = cb.corr_pyramid
+    assert v1[0].requires_grad and bit_equal(v1[0].detach().cpu().numpy(), v0[0].cpu().numpy())
+    v1[0].sum().backward()
+    assert t1.grad is not None and t2.grad is not None
+    c = torch.from_numpy(prng.lookup_coords(113, B, H, W, 1.0)).to(DEV)
+    before = cb(c).detach()
+    cb.corr_pyramid = [2 * v.detach() for v in v1]
+    after = cb(c)
+    assert not after.requires_grad  # reads the assigned (constant) tensors
+    assert bit_equal(after.cpu().numpy(), (2 * before).cpu().numpy())
+    with pytest.raises(NotImplementedError):
+        cb.corr_pyramid = [v.detach().requires_grad_(True) for v in v1]
+
+
+def test_short_level_buffers_are_refused():
+    """a caller handing the library reference-layout (ABI-104) [B*N, 1, H_l, W_l]
+    value levels — smaller than the tiled maps when H_l or W_l is not a multiple of 4 — gets a
+    ValueError before any device access."""
+    from eraft_amd import _lib
+    B, D, H, W, L, r = 1, 16, 30, 40, 2, 2
+    f1 = torch.from_numpy(prng.gauss(121, (B, D, H, W))).to(DEV)
+    short = [torch.empty(B * H * W, 1, H >> l, W >> l, device=DEV) for l in range(L)]  # 30 x 40: level 1 15 x 20
+    with pytest.raises(ValueError, match="map_floats"):
+        _lib.build(f1, f1, short)
+    c = torch.from_numpy(prng.lookup_coords(122, B, H, W, 1.0)).to(DEV)
+    out = torch.empty(B, L * (2 * r + 1) ** 2, H, W, device=DEV)
+    with pytest.raises(ValueError, match="map_floats"):
+        _lib.lookup(short, c, r, out)
+
+
 @pytest.mark.parametrize("name", golden_names("g_bwd"))
 def test_backward_matches_reference(name):
     g = load(name)
@@ -461,29 +570,35 @@ def test_build_bwd_bf16x6_not_narrower_than_fp32(case):
         assert rb.max() <= r32.max() and rb.mean() <= r32.mean()
 
 
-def test_build_bwd_bf16x6_inf_gives_nan():
-    """The documented non-finite behaviour of the bf16x6 backward GEMMs (include/corr_mi355x.h,
-    corr_build_bwd_ex): an infinite dC element makes exactly the outputs it reaches NaN (dF1
-    column of its query row, dF2 column of its target), where fp32 gives +-inf; every other output
-    is finite and matches the fp32-operand GEMMs within 1e-6 of the scale."""
+@pytest.mark.parametrize("D,H,W", [(16, 8, 12), (32, 8, 12), (64, 32, 48)])
+def test_build_bwd_bf16x6_inf_matches_fp32(D, H, W):
+    """Non-finite inputs of the bf16x6 backward GEMMs give the fp32 reference's results
+    (include/corr_mi355x.h, corr_build_bwd_ex): the split makes every output an infinite element
+    reaches NaN (inf * 0 pieces), and the reduce / direct epilogue recompute exactly those as the
+    reference does, so +-inf land where the fp32-operand GEMMs put them and NaN (inf * 0 in the
+    fp32 sum, a NaN element) stays NaN.  Shapes: D 16 (one split, sqrt(D) a power of two: the
+    direct epilogue), D 32 (one split, the reduce kernel / dF2's tail), D 64 at 32x48 (split-K).
+    Every finite output matches the fp32-operand GEMMs within 1e-6 of the scale."""
     from eraft_amd import _lib
-    B, D, H, W = 1, 32, 8, 12
+    B = 1
     N = H * W
     f1, f2 = prng.gauss(181, (B, D, H, W)), prng.gauss(182, (B, D, H, W))
     gc = prng.gauss(183, (B * N, N))
-    gc[5, 17] = np.inf
+    gc[5, 17] = np.inf     # +inf in dC: dF1 column 5, dF2 column 17
+    gc[9, 3] = -np.inf     # -inf
+    f2[0, 2].flat[17] = 0  # F2[2][17] = 0 meets dC[5][17] = inf: fp32 gives NaN at dF1[2][5]
+    gc[20, 40] = np.nan    # a NaN element: NaN outputs as in fp32
+    f1[0, 3].flat[30] = np.inf  # an infinite feature: dF2 row 3
     tg, t1, t2 = (torch.from_numpy(x).to(DEV) for x in (gc, f1, f2))
     d1, d2 = (g.cpu().numpy().reshape(B, D, N) for g in _lib.build_bwd(tg, t1, t2, _lib.BUILD_BF16X6))
     e1, e2 = (g.cpu().numpy().reshape(B, D, N) for g in _lib.build_bwd(tg, t1, t2, _lib.BUILD_FP32))
-    nan1 = np.zeros_like(d1, bool)
-    nan1[0, :, 5] = True
-    nan2 = np.zeros_like(d2, bool)
-    nan2[0, :, 17] = True
-    assert np.array_equal(np.isnan(d1), nan1) and np.array_equal(np.isnan(d2), nan2)
-    assert np.isinf(e1[nan1]).all() and np.isinf(e2[nan2]).all()  # fp32: +-inf there
     for a, b in ((d1, e1), (d2, e2)):
+        assert np.isnan(b).any() and np.isposinf(b).any() and np.isneginf(b).any()
+        assert np.array_equal(np.isnan(a), np.isnan(b))
+        assert np.array_equal(np.isposinf(a), np.isposinf(b)) and np.array_equal(np.isneginf(a), np.isneginf(b))
         ok = np.isfinite(b)
         assert np.abs(a[ok] - b[ok]).max() <= 1e-6 * np.abs(b[ok]).max()
+    assert np.isnan(d1[0, 2, 5])  # inf * 0 in the fp32 sum
 
 
 def _bf16_to_f32(u16):
@@ -600,7 +715,7 @@ def test_bf16x6_infinite_features_match_fp32(algo_name):
         assert inf.any() and np.array_equal(np.isinf(a), inf) and np.array_equal(a[inf], b[inf])
         fin = np.isfinite(b)
         scale = np.where(fin, np.abs(b), 0).max(axis=1, keepdims=True)
-        assert (np.abs(np.where(fin, a - b, 0)) <= 1e-5 * scale + 1e-30).all()
+        assert (np.abs(np.where(fin, a, 0) - np.where(fin, b, 0)) <= 1e-5 * scale + 1e-30).all()
 
 
 def test_lookup_nan_and_inf_coords():
