@@ -100,41 +100,57 @@ struct PackArgs {
     int D, S, W, CB, y0, y1, z0;
 };
 
+// R: records per wave, all R records' loads issued before any split or store (more bytes in
+// flight per wave); the workgroup's 4 waves take 4 consecutive records at each r, so a k row is
+// still read as one 256-B run per workgroup.
+template <int R = 1>
 __global__ __launch_bounds__(256) void bf16_pack_kernel(PackArgs a) {
     const int z = blockIdx.z + a.z0, b = blockIdx.y;
     const int nblk = a.nblk[z];
-    const int rec = blockIdx.x * 4 + (threadIdx.x >> 6);  // record = s * nblk + blk
-    if (rec >= a.S * nblk) return;
-    const int s = rec / nblk, blk = rec - s * nblk;
     const int lane = threadIdx.x & 63, ci = lane & 15, grp = lane >> 4;
-    int n, iblk;  // source pixel in the slab, block in the packed image
-    bool valid;
-    if (z == 0) {
-        n = blk * 16 + ci;
-        valid = n < a.np[0];
-        iblk = blk;
-    } else {
-        // target block = a 4x4 tile of the map (tile row ty, column tx; 4 CB tiles per row), pixel
-        // ci at (ci / 4, ci % 4): the MFMA's output rows then hold whole tile rows of the pyramid
-        const int TCp = 4 * a.CB, ty = blk / TCp, tx = blk - ty * TCp;
-        const int ly = 4 * ty + (ci >> 2), x = 4 * tx + (ci & 3);
-        valid = a.y0 + ly < a.y1 && x < a.W;
-        n = ly * a.W + x;
-        iblk = (a.y0 >> 2) * TCp + blk;
+    const int NP = a.np[z];
+    float v[R][8];
+    bool live[R];
+    size_t dst[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int rec = (blockIdx.x * R + r) * 4 + (threadIdx.x >> 6);  // record = s * nblk + blk
+        live[r] = rec < a.S * nblk;
+        const int s = live[r] ? rec / nblk : 0, blk = live[r] ? rec - s * nblk : 0;
+        int n, iblk;  // source pixel in the slab, block in the packed image
+        bool valid;
+        if (z == 0) {
+            n = blk * 16 + ci;
+            valid = n < a.np[0];
+            iblk = blk;
+        } else {
+            // target block = a 4x4 tile of the map (tile row ty, column tx; 4 CB tiles per row), pixel
+            // ci at (ci / 4, ci % 4): the MFMA's output rows then hold whole tile rows of the pyramid
+            const int TCp = 4 * a.CB, ty = blk / TCp, tx = blk - ty * TCp;
+            const int ly = 4 * ty + (ci >> 2), x = 4 * tx + (ci & 3);
+            valid = a.y0 + ly < a.y1 && x < a.W;
+            n = ly * a.W + x;
+            iblk = (a.y0 >> 2) * TCp + blk;
+        }
+        valid = valid && live[r];
+        const int k0 = s * kStepK + 8 * grp;
+        const float *src = a.f[z] + (size_t)b * a.D * NP + (valid ? n : 0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[r][j] = (valid && k0 + j < a.D) ? src[(size_t)(k0 + j) * NP] : 0.f;
+        dst[r] = (((size_t)b * a.S + s) * a.img[z] + iblk) * kRecU + lane;
     }
-    const int NP = a.np[z], k0 = s * kStepK + 8 * grp;
-    const float *src = a.f[z] + (size_t)b * a.D * NP + (valid ? n : 0);
-    float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (valid && k0 + j < a.D) ? src[(size_t)(k0 + j) * NP] : 0.f;
-    unsigned hh[4], mm[4], ll[4];
+    for (int r = 0; r < R; ++r) {
+        if (!live[r]) continue;
+        unsigned hh[4], mm[4], ll[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) split3(v[2 * j], v[2 * j + 1], hh[j], mm[j], ll[j]);
-    const u32x4_t h{hh[0], hh[1], hh[2], hh[3]}, m{mm[0], mm[1], mm[2], mm[3]}, l{ll[0], ll[1], ll[2], ll[3]};
-    u32x4_t *out = a.pk[z] + (((size_t)b * a.S + s) * a.img[z] + iblk) * kRecU + lane;
-    out[0] = h;
-    out[64] = m;
-    out[128] = l;
+        for (int j = 0; j < 4; ++j) split3(v[r][2 * j], v[r][2 * j + 1], hh[j], mm[j], ll[j]);
+        const u32x4_t h{hh[0], hh[1], hh[2], hh[3]}, m{mm[0], mm[1], mm[2], mm[3]}, l{ll[0], ll[1], ll[2], ll[3]};
+        u32x4_t *out = a.pk[z] + dst[r];
+        out[0] = h;
+        out[64] = m;
+        out[128] = l;
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -149,6 +165,7 @@ struct Args {
     int exact;         // 1/sqrt(D) is a power of two (x * 1/s == x / s); else x * RN(1/s), within ~1 ulp
     float inv_s, s;
     int order;  // tile order: 0, 1 = patch_tile's; 2 = XCD blocks (xcd_block_tile)
+    int gq;     // orders 0 / 1: query groups per L2 tile group (patch_tile)
     int nqh, npq;  // order 2: query-group and patch splits of a batch item into XCD blocks
 };
 
@@ -497,7 +514,7 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
 template <int SS, bool ACC2 = true, int VF = 0, bool FAST = false>
 __global__ __launch_bounds__(256, 2) void corr_build_bf16_kernel(Args p) {
     const int t = xcd_swizzle(blockIdx.x, gridDim.x);
-    Tile tl = p.order == 2 ? xcd_block_tile(p, t) : patch_tile(t, p.npatch, p.NQG, p.CB, p.order);
+    Tile tl = p.order == 2 ? xcd_block_tile(p, t) : patch_tile(t, p.npatch, p.NQG, p.CB, p.order, p.gq);
     tl.py += p.py0;
     // two whole code paths (no value flows out of either): a half patch runs half the MFMAs
     if (!(VF & 4) && SS > 0 && tl.py * kPatchRows + kPatchRows / 2 >= p.H)
@@ -543,8 +560,11 @@ size_t workspace_bytes(int B, int D, int NQ, int H, int W) {
 
 // Packs the queries (pack_q) and the target rows [y0, y1) (f2 = that slab, [B][D][y1 - y0][W];
 // y0 a multiple of 8, y1 a multiple of 8 or H): the patch rows [y0 / 8, ceil(y1 / 8)).
+// rpw: records per wave (bf16_pack_kernel's R); 0 = by size: 4 once there are >= 8192 records
+// (train B8 15.4 -> 14.0 us, MVSEC B16 29.9 -> 27.7 us), else 1 (DSEC's 4,800 records: 6.3 us
+// with one, 8.5 with four — a single round of workgroups, profiles/r06g_kbench_pack_rpw.txt).
 hipError_t launch_pack(const float *f1, int NQ, const float *f2, int B, int D, int H, int W, void *ws,
-                       hipStream_t s, int y0 = 0, int y1 = -1, bool pack_q = true) {
+                       hipStream_t s, int y0 = 0, int y1 = -1, bool pack_q = true, int rpw = 0) {
     if (y1 < 0) y1 = H;
     const Geom g = geom(D, NQ, H, W);
     const Ws w = workspace_of(ws, B, g);
@@ -558,7 +578,14 @@ hipError_t launch_pack(const float *f1, int NQ, const float *f2, int B, int D, i
     a.D = D, a.S = g.S, a.W = W, a.CB = g.CB, a.y0 = y0, a.y1 = y1;
     a.z0 = pack_q ? 0 : 1;
     const int recs = g.S * std::max(pack_q ? a.nblk[0] : 0, a.nblk[1]);
-    hipLaunchKernelGGL(bf16_pack_kernel, dim3((unsigned)((recs + 3) / 4), B, pack_q ? 2 : 1), dim3(256), 0, s, a);
+    if (rpw == 0) rpw = (long)recs * B * (pack_q ? 2 : 1) >= 8192 ? 4 : 1;
+    const dim3 blk(256);
+    if (rpw == 4)
+        hipLaunchKernelGGL(bf16_pack_kernel<4>, dim3((unsigned)((recs + 15) / 16), B, pack_q ? 2 : 1), blk, 0, s, a);
+    else if (rpw == 2)
+        hipLaunchKernelGGL(bf16_pack_kernel<2>, dim3((unsigned)((recs + 7) / 8), B, pack_q ? 2 : 1), blk, 0, s, a);
+    else
+        hipLaunchKernelGGL(bf16_pack_kernel<1>, dim3((unsigned)((recs + 3) / 4), B, pack_q ? 2 : 1), blk, 0, s, a);
     return hipGetLastError();
 }
 
@@ -568,7 +595,7 @@ hipError_t launch_pack(const float *f1, int NQ, const float *f2, int B, int D, i
 // y0, y1: the target region (as launch_pack), whose pyramid rows [y0 >> l, ceil(y1 / 2^l)) of
 // every level it writes.
 hipError_t launch_mfma(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
-                       hipStream_t s, int variant = 0, int order = 1, int y0 = 0, int y1 = -1) {
+                       hipStream_t s, int variant = 0, int order = 1, int y0 = 0, int y1 = -1, int gq = kGroupQ) {
     if (y1 < 0) y1 = H;
     const Geom g = geom(D, NQ, H, W);
     const Ws w = workspace_of(ws, B, g);
@@ -586,6 +613,7 @@ hipError_t launch_mfma(int NQ, int B, int D, int H, int W, int levels, const Lev
     // XCD blocks: split each batch item into 8 / B blocks (2 x 4 for one item), so the 8 XCDs
     // get disjoint operand sets; B >= 8: one or more whole batch items per XCD
     p.order = order;
+    p.gq = std::max(1, gq);
     const int per = B >= 8 ? 1 : 8 / B;
     p.nqh = per >= 2 && g.NQG >= 2 ? 2 : 1;
     p.npq = std::max(1, std::min(per / p.nqh, p.npatch));

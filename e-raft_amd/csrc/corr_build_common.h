@@ -62,23 +62,24 @@ struct Tile {
 // one XCD has in flight cover ~8 patches x 8 query groups).  order 1: a patch row's patches
 // consecutive for one query group (the 64-B row segments of horizontally adjacent patches share
 // 128-B lines and are written close in time on one XCD).
-__device__ __forceinline__ Tile patch_tile(int t, int npatch, int NQG, int CB, int order) {
+// gq: query groups per L2 tile group (kGroupQ unless a caller passes its own).
+__device__ __forceinline__ Tile patch_tile(int t, int npatch, int NQG, int CB, int order, int gq = kGroupQ) {
     Tile o;
     const int per_b = npatch * NQG;
     o.b = t / per_b;
     const int r = t - o.b * per_b;
-    const int g = r / (kGroupQ * npatch);
-    const int gm = min(kGroupQ, NQG - g * kGroupQ);
-    const int r2 = r - g * kGroupQ * npatch;
+    const int g = r / (gq * npatch);
+    const int gm = min(gq, NQG - g * gq);
+    const int r2 = r - g * gq * npatch;
     if (order == 1) {
         o.py = r2 / (gm * CB);
         const int r3 = r2 - o.py * gm * CB;
-        o.qg = g * kGroupQ + r3 / CB;
+        o.qg = g * gq + r3 / CB;
         o.cb = r3 - (r3 / CB) * CB;
         return o;
     }
     const int patch = r2 / gm;
-    o.qg = g * kGroupQ + (r2 - patch * gm);
+    o.qg = g * gq + (r2 - patch * gm);
     o.py = patch / CB;
     o.cb = patch - o.py * CB;
     return o;

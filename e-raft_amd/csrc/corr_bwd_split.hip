@@ -335,9 +335,9 @@ __device__ __forceinline__ void split2(float x0, float x1, int s, bool guard, ha
 // bit — the same pieces as split3 wherever hi does not overflow; past M, hi = the bf16 maximum
 // and the residual carries the rest (split3 truncates there instead).  An infinite element
 // splits as (the clamped hi, inf, NaN), so every output it reaches comes out of the MFMAs as NaN
-// (one accumulator cannot tell inf * 0 from a real NaN); the reduce / direct epilogue then
-// recompute exactly those outputs as the fp32 reference does (NanFix, corr_common.h), which
-// restores fp32's +-inf.
+// (one accumulator cannot tell inf * 0 from a real NaN); the split-K reduce then recomputes
+// exactly those outputs as the fp32 reference does (NanFix, corr_common.h), which restores
+// fp32's +-inf.
 __device__ __forceinline__ void split3_bwd(float a, float b, unsigned &hi, unsigned &mid, unsigned &lo) {
     constexpr float M = 3.3961775e38f;  // 0x7F7F7FFF
     float ha, hb, ma, mb, da, db;
@@ -397,7 +397,7 @@ struct FGemmParams {
     size_t tail_per4;
     int tail_splits, tail_exact, tail_wgs, gemm_wgs;
     float tail_alpha, tail_s;
-    NanFix fix, tail_fix;  // BF: NaN outputs recomputed in fp32 (direct epilogue; the tail reduce's GEMM)
+    NanFix fix, tail_fix;  // BF: NaN outputs recomputed in fp32 (the tail reduce's GEMM: tail_fix)
 };
 
 // The tail reduce's share of workgroup t of p.tail_wgs (bit-identical to the separate reduce).
@@ -945,8 +945,6 @@ __global__ __launch_bounds__(64 * WI * kWJ, 2) void split_gemm_f32_kernel(FGemmP
                 const int i = i0 + il;
                 float x = BF ? acc[m][n][g] : ldexpf(acc[m][n][g], lex[il] + ej);
                 if (p.direct) x = x * p.alpha;
-                if (BF && p.direct && __builtin_expect(x != x, 0) && i < p.NI && j < p.NJ)
-                    x = nanfix_dot(p.fix, b, i, j);
                 if (i < p.NI && j < p.NJ) {
                     if (p.nt) __builtin_nontemporal_store(x, &C[(size_t)i * p.NJ + j]);
                     else C[(size_t)i * p.NJ + j] = x;
@@ -1098,7 +1096,8 @@ hipError_t gemm_f32(const float *A, long a_sb, long a_sr, const float *Bm, long 
     p.splits = (p.nkc + p.kc_per - 1) / p.kc_per;
     const bool exact = is_pow2(sD);
     p.alpha = 1.0f / sD;
-    p.direct = p.splits == 1 && exact;
+    // bf16x6: always the slab path, so that the reduce applies the non-finite rule (NanFix)
+    p.direct = p.splits == 1 && exact && !bf;
     p.C = p.direct ? C : slab;
     p.nt = t.nt ? 1 : 0;
     auto al16 = [](const void *q) { return ((uintptr_t)q & 15) == 0; };

@@ -65,15 +65,19 @@ struct NanFix {
     int NI = 0, NJ = 0, K = 0;
     float s = 1.f;  // sqrt(D): the reference divides dC by it before the matmul
 };
-__device__ __noinline__ inline float nanfix_dot(const NanFix &f, int b, int i, int j) {
+// (inlined: a call would give every kernel that holds it a call stack — 336 B of scratch and
+// +24 % on the backward GEMMs, +120 % on the reduce when the fixup was a __noinline__ function)
+__device__ __forceinline__ float nanfix_dot(const NanFix &f, int b, int i, int j) {
     const float *a = f.A + (size_t)b * f.a_sb + (size_t)i * f.a_sr;
     const float *m = f.Bm + (size_t)b * f.b_sb + (size_t)j * f.b_sr;
     float acc = 0.f;
     for (int k = 0; k < f.K; ++k) acc = fmaf(a[k], m[(size_t)k * f.b_sk] / f.s, acc);
     return acc;
 }
-// The same for flat output index e of C [B][NI][NJ].
-__device__ __noinline__ inline float nanfix_flat(const NanFix &f, size_t e) {
+// The same for flat output index e of C [B][NI][NJ].  Only the split-K reduces call these (the
+// separate reduce kernel and a GEMM's appended tail-reduce workgroups); the bf16x6 GEMMs always
+// take the slab path, so no GEMM epilogue carries the fixup.
+__device__ __forceinline__ float nanfix_flat(const NanFix &f, size_t e) {
     const size_t per = (size_t)f.NI * f.NJ;
     const size_t r = e % per;
     return nanfix_dot(f, (int)(e / per), (int)(r / f.NJ), (int)(r % f.NJ));

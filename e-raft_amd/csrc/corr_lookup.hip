@@ -1293,13 +1293,21 @@ struct LaneTable {
 // PROBE (measurement builds only, tools/kbench_bwd.hip; the library uses 0): bit 0 = no lookup
 // loop, bit 1 = no fold (no dC / maxima), bit 2 = no LDS zero-init (wrong results, timing only),
 // bit 3 = plain (L2-cached) dC stores instead of the non-temporal ones, bit 4 = wait for the
-// lookup's LDS writes at the end of each lookup (round 5's s_waitcnt).
+// lookup's LDS writes at the end of each lookup (round 5's s_waitcnt).  (Moving the closed form's
+// y-tap broadcasts, or its previous-column gradients, from DPP to ds_bpermute — LDS pipe
+// instead of VALU — was measured and dropped: T = 12 79 -> 88 / 83 us,
+// profiles/r06f_kbench_bwd_lean.txt.)
 // SEP: regular windows by the separable closed form (corr_backward's default); false replays
 // grid_sampler_2d_backward's per-tap products bit for bit (CORR_BACKWARD_EXACT_FOLD).
 // (Several query groups per workgroup — 8 or 16 queries, so that the groups' waves would share
 // L1 fills of the upstream-gradient lines — were measured and dropped: L2 requests unchanged,
 // T = 12 92 -> 101 / 164 us, profiles/r05zi_kbench_bwd_groups_dropped.txt.)
-template <int S, int PROBE = 0, bool SEP = false>
+// LEAN: the fold phase for the common case — 4 levels, no maxima (the bf16x6 backward),
+// W % 4 == 0 and 16-B aligned dC — with the level values shared across a thread's 4 cells read
+// once and no maxima arithmetic (the generic fold recomputed the coarse chain per cell and took
+// |max| of every value: ~45 % of the fold phase's VALU).  The same per-cell sums in the same
+// order (bit-identical).
+template <int S, int PROBE = 0, bool SEP = false, bool LEAN = false>
 __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLookups lk, FusedOut o) {
     using ST = FusedStage<S>;
     constexpr int R = (S - 1) / 2, K = S * S, C = S + 1, WIN = ST::WIN;
@@ -1327,6 +1335,10 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     const float rdx = recip_rn((float)(Wl - 1)), rdy = recip_rn((float)(Hl - 1));
     float *st = fsm + o.aux + lc * ST::SIZE;  // this wave's staging
     const int mbase = o.moff[lc] + q * o.qstr[lc];
+    // fsm's LDS byte address (0 unless the kernel gains static LDS) and an LDS float at an
+    // absolute byte address
+    const int lds_base = (int)(uintptr_t)(__attribute__((address_space(3))) float *)fsm;
+    auto lds_at = [](unsigned a) { return (__attribute__((address_space(3))) float *)(uintptr_t)a; };
     const int dump = o.aux + lc * ST::SIZE + ST::DUMP + lane;
     auto tx = [&](int c, int t) -> float & { return st[ST::TX + (c * S + t) * BQ + q]; };
     auto ty = [&](int c, int t) -> float & { return st[ST::TY + (c * S + t) * BQ + q]; };
@@ -1346,10 +1358,11 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
     constexpr uint32_t kOob = 0x80000000u;
     const uint32_t coff = loader ? (uint32_t)n * 4u : kOob;
     constexpr bool kQuadLoads = SLOTS == 16 && BQ == 4;
-    const int lq = kQuadLoads ? (lane & 3) : q, lx = kQuadLoads ? (lane >> 2) : cx;
+    const int lq = kQuadLoads ? ((lane & 3) ^ ((lane >> 5) << 1)) : q, lx = kQuadLoads ? (lane >> 2) : cx;
     const bool gloader = act && lx < S && n0 + lq < NQ;
     const uint32_t goff = gloader ? (uint32_t)(((lc * K + lx * S) * NQ + n0 + lq) * 4) : kOob;
-    const int gsrc = kQuadLoads ? 4 * (4 * cx + q) : 0;  // ds_bpermute byte address of this lane's loader
+    // ds_bpermute byte address of this lane's loader (lane 4 cx + (q ^ 2 [cx >= 8]))
+    const int gsrc = kQuadLoads ? 4 * (4 * cx + (q ^ ((cx >> 3) << 1))) : 0;
     float pcx, pcy, pv[S];
     const LaneTable table(lane);
     auto prefetch = [&](int t) {
@@ -1364,6 +1377,22 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
 #pragma unroll
         for (int u = 0; u < S; ++u)
             pv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, goff, u * NQ * 4, 0));
+    };
+    // PROBE & 32 (A/B): L2 warm-up of lookup t + 3's upstream-gradient lines by the first workgroup
+    // of each 32-query line group — one dword per row (lane = row), consumed one lookup later
+    float warm[2] = {0.f, 0.f}, warm_prev[2] = {0.f, 0.f};
+    const bool warmer = (PROBE & 32) != 0 && act && (n0 & 31) == 0;
+    auto warmup = [&](int t) {
+        const float *coords, *grad_out;
+        table.get(t, coords, grad_out);
+        const auto rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(grad_out + (size_t)b * L * K * NQ), 0,
+                                                          L * K * NQ * 4, 0x00020000);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int row = lane + 64 * h;
+            const uint32_t off = row < K ? (uint32_t)(((lc * K + row) * NQ + n0) * 4) : kOob;
+            warm[h] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, off, 0, 0));
+        }
     };
     if (act) prefetch(0);  // issued before the LDS zeroing, so its latency hides behind it
     if (!(PROBE & 4))
@@ -1380,6 +1409,10 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         for (int u = 0; u < S; ++u)
             v[u] = kQuadLoads ? __int_as_float(__builtin_amdgcn_ds_bpermute(gsrc, __float_as_int(pv[u]))) : pv[u];
         prefetch(min(t + 1, lk.T - 1));
+        if constexpr ((PROBE & 32) != 0) {
+            warm_prev[0] = warm[0], warm_prev[1] = warm[1];
+            if (warmer && t + 3 < lk.T) warmup(t + 3);
+        }
         const Axis a = tap_axis(cxv, inv_scale, cxl, R, Wl, rdx);
         const Axis c = tap_axis(cyv, inv_scale, cxl, R, Hl, rdy);
         // ---- 2. the (query, level) group's form, decided per group ----
@@ -1435,20 +1468,21 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         // add and one v_med3.
         auto add_column = [&]<int NC>(const float (&sv)[NC]) {
             const bool mine = colok && cx < NC;
-            const int cb = mine ? 4 * (mbase + X) : kLdsOob;
+            // absolute LDS byte addresses (fsm's own offset folded into cb once: the accesses
+            // then take the clamped address as is, no add per cell)
+            const int cb = lds_base + (mine ? 4 * (mbase + X) : kLdsOob);
             const int s4 = 4 * Wl;
             const int gtop = cb - s4, gbot = cb + Hl * s4;
             // rows past [-NC, H_l] clamp like those bounds (and keep s4 * ay in range)
             int ra = cb + s4 * (mine ? min(max(ay, -NC), Hl) : 0);
-            char *const lds = reinterpret_cast<char *>(fsm);
             float old[NC];
             unsigned at[NC];
 #pragma unroll
             for (int cy = 0; cy < NC; ++cy, ra += s4) at[cy] = (unsigned)med3_i32(ra, gtop, gbot);
 #pragma unroll
-            for (int cy = 0; cy < NC; ++cy) old[cy] = *reinterpret_cast<float *>(lds + at[cy]);  // all reads, then all writes
+            for (int cy = 0; cy < NC; ++cy) old[cy] = *lds_at(at[cy]);  // all reads, then all writes
 #pragma unroll
-            for (int cy = 0; cy < NC; ++cy) *reinterpret_cast<float *>(lds + at[cy]) = old[cy] + sv[cy];
+            for (int cy = 0; cy < NC; ++cy) *lds_at(at[cy]) = old[cy] + sv[cy];
         };
         if (!irregular) {
             // closed form.  Absent terms (window edges) carry zero weights and gradients: adding
@@ -1654,11 +1688,52 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         // needed: the map writes drain while the next lookup's taps are computed)
         if constexpr ((PROBE & 16) != 0) wave_lds_sync();
         else asm volatile("" ::: "memory");
+        if constexpr ((PROBE & 32) != 0) asm volatile("" ::"v"(warm_prev[0]), "v"(warm_prev[1]));
     }
     __syncthreads();
 
     if constexpr ((PROBE & 2) != 0) return;
     // ---- 3. fold into level 0, write dC with its row / column maxima ----
+    if constexpr (LEAN) {
+        // 4 consecutive level-0 cells of one row per thread (x % 4 == 0): they share one level-2
+        // and one level-3 cell and two level-1 cells, so the coarse chain is folded once per
+        // shared cell — g2 = c2 + c3 / 4, g1 = c1 + g2 / 4, g0 = c0 + g1 / 4, each "+ coarse *
+        // 0.25" only where the finer cell lies in the coarser level's pooled region (corr_pool_bwd)
+        const int W1 = W >> 1, W2 = W >> 2, W3 = W >> 3;
+        const int PH0 = 2 * (H >> 1), PH1 = 2 * (H >> 2), PH2 = 2 * (H >> 3);  // pooled rows of levels 0..2
+        const int PW1 = 2 * (W1 >> 1), PW2 = 2 * (W2 >> 1);                      // pooled columns of levels 1, 2
+        const f32x4 *F4 = reinterpret_cast<const f32x4 *>(fsm);
+        const f32x2 *F2 = reinterpret_cast<const f32x2 *>(fsm);
+        for (int u = tid; u < N / 4; u += NT) {
+            const int m = 4 * u, y = m / W, x = m - y * W;
+            const int y1 = y >> 1, y2 = y >> 2, y3 = y >> 3, x1 = x >> 1, x2 = x >> 2, x3 = x >> 3;
+            // pooled-region flags: level-0 rows (columns always: W even), level-1 cells x1, x1 + 1,
+            // the level-2 cell
+            const bool p0 = y < PH0;
+            const bool p1a = y1 < PH1 && x1 < PW1, p1b = y1 < PH1 && x1 + 1 < PW1;
+            const bool p2 = y2 < PH2 && x2 < PW2;
+            const int o0 = (o.moff[0] + y * W + x) >> 2, o1 = (o.moff[1] + y1 * W1 + x1) >> 1;
+            const int o2 = o.moff[2] + y2 * W2 + x2, o3 = o.moff[3] + y3 * W3 + x3;
+#pragma unroll
+            for (int k = 0; k < WQ; ++k) {
+                if (n0 + k >= NQ) continue;
+                const f32x4 c0 = F4[o0 + ((k * o.qstr[0]) >> 2)];
+                const f32x2 c1 = F2[o1 + ((k * o.qstr[1]) >> 1)];
+                const float c2 = fsm[o2 + k * o.qstr[2]], c3 = fsm[o3 + k * o.qstr[3]];
+                const float g2 = p2 ? c2 + c3 * 0.25f : c2;
+                const float g1a = p1a ? c1.x + g2 * 0.25f : c1.x, g1b = p1b ? c1.y + g2 * 0.25f : c1.y;
+                f32x4 r;
+                r.x = p0 ? c0.x + g1a * 0.25f : c0.x;
+                r.y = p0 ? c0.y + g1a * 0.25f : c0.y;
+                r.z = p0 ? c0.z + g1b * 0.25f : c0.z;
+                r.w = p0 ? c0.w + g1b * 0.25f : c0.w;
+                f32x4 *dst = reinterpret_cast<f32x4 *>(o.dc + ((size_t)b * NQ + n0 + k) * N + m);
+                if constexpr ((PROBE & 8) != 0) *dst = r;
+                else __builtin_nontemporal_store(r, dst);
+            }
+        }
+        return;
+    }
     float rq[WQ];
 #pragma unroll
     for (int k = 0; k < WQ; ++k) rq[k] = 0.f;
@@ -2026,8 +2101,13 @@ hipError_t launch_fused_s(const BwdLookups &lk, FusedOut o, hipStream_t s) {
     if (e != hipSuccess) return e;
     const int limit = std::min(160 * 1024, dev_max);
     if (bytes > (size_t)limit) return hipErrorNotSupported;
-    static std::atomic<unsigned long long> done{0};
-    e = ensure_lds_limit((const void *)lookup_bwd_fold_kernel<S, 0, SEP>, limit, done);
+    // the lean fold (no maxima, 4 levels, 16-B rows of dC): the bf16x6 backward at radius 4
+    const bool lean = S == 9 && !o.rmax && !o.cmax && !o.cpart && o.L == kFusedLv && o.W % 4 == 0 &&
+                      ((uintptr_t)o.dc & 15) == 0;
+    const void *fn = lean ? (const void *)lookup_bwd_fold_kernel<S, 0, SEP, S == 9>
+                          : (const void *)lookup_bwd_fold_kernel<S, 0, SEP>;
+    static std::atomic<unsigned long long> done[2];
+    e = ensure_lds_limit(fn, limit, done[lean]);
     if (e != hipSuccess) return e;
     constexpr int WQ = FusedStage<S>::BQ, WAVES = kFusedLv;
     const int nqb = (o.NQ + WQ - 1) / WQ;
@@ -2040,8 +2120,12 @@ hipError_t launch_fused_s(const BwdLookups &lk, FusedOut o, hipStream_t s) {
         o.rm_rows_per_wave = (int)std::max(1L, (rows + cap * WAVES - 1) / (cap * WAVES));
         extra = (int)((rows + (long)o.rm_rows_per_wave * WAVES - 1) / ((long)o.rm_rows_per_wave * WAVES));
     }
-    hipLaunchKernelGGL((lookup_bwd_fold_kernel<S, 0, SEP>), dim3((unsigned)(o.nfold + extra)), dim3(64 * WAVES), bytes,
-                       s, lk, o);
+    if (lean)
+        hipLaunchKernelGGL((lookup_bwd_fold_kernel<S, 0, SEP, S == 9>), dim3((unsigned)(o.nfold + extra)),
+                           dim3(64 * WAVES), bytes, s, lk, o);
+    else
+        hipLaunchKernelGGL((lookup_bwd_fold_kernel<S, 0, SEP>), dim3((unsigned)(o.nfold + extra)), dim3(64 * WAVES),
+                           bytes, s, lk, o);
     return hipGetLastError();
 }
 }  // namespace

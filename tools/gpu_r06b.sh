@@ -1,0 +1,21 @@
+#!/bin/bash
+# Fold A/B (HEAD kernel vs working tree, interleaved) + an LDS / VALU PMC pass of each.
+#   bash tools/gpu_r06b.sh <tag>
+set -o pipefail
+TAG=${1:-r06b}
+export TMPDIR=/tmp
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+V="SEP full T=12, no maxima (bf16x6)"
+for r in 1 2; do
+  for b in kbench_bwd_old kbench_bwd; do
+    echo "== $b round $r" >> $OUT/ab.txt
+    timeout -k 10 120 ./tools/_build/$b 10 >> $OUT/ab.txt 2>&1 || { echo "$b failed"; exit 3; }
+  done
+done
+echo ab done
+P="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES"
+for b in kbench_bwd_old kbench_bwd; do
+  timeout -s KILL 90 rocprofv3 --pmc $P -d $OUT/pmc_$b -o run --output-format csv -- ./tools/_build/$b 3 "$V" > $OUT/pmc_$b.log 2>&1 || { echo "pmc $b failed"; exit 4; }
+done
+echo pmc done

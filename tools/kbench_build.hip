@@ -132,6 +132,10 @@ int main(int argc, char **argv) {
         vs.push_back({"bf16x6 pack only", [&](float *o) {
                           return launch_build_bf16(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), wsbf, 0, 1);
                       }, false});
+        for (int rpw : {1, 2, 4})
+            vs.push_back({"bf16x6 pack only rpw" + std::to_string(rpw), [&, rpw](float *) {
+                              return bf16b::launch_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, wsbf, 0, 0, -1, true, rpw);
+                          }, false});
         vs.push_back({"bf16x6 mfma only", [&](float *o) {
                           return launch_build_bf16(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), wsbf, 0, 2);
                       }, false});
@@ -150,6 +154,13 @@ int main(int argc, char **argv) {
         vs.push_back({"bf16x6 mfma order2 (XCD blocks)", [&](float *o) {
                           return bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), wsbf, 0, 0, 2);
                       }, false});
+        for (int od : {0, 1})
+            for (int gq : {4, 8, 16, 32}) {
+                if (od == 1 && gq == 8) continue;  // the library's default ("bf16x6 mfma only")
+                vs.push_back({"bf16x6 mfma order" + std::to_string(od) + " gq" + std::to_string(gq), [&, od, gq](float *o) {
+                                  return bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), wsbf, 0, 0, od, 0, -1, gq);
+                              }, false});
+            }
         vs.push_back({"bf16x6 mfma NOSTORE", [&](float *o) {
                           return launch_build_bf16(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 0, lp_of(o), wsbf, 0, 2);
                       }, false});
@@ -232,11 +243,13 @@ int main(int argc, char **argv) {
             same("1-tile no half path", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 2); });
             same("1-tile nopipe", [&](float *o) { return launch_split_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), ws, 0, true, 1); });
             if (sh.D == 256) {
-                for (int vv : {2, 3, 5, 9}) {  // bf16x6 variants vs the default bf16x6 kernel (9: tile order 2)
+                for (int vv : {2, 3, 5, 9, 10, 11}) {  // bf16x6 variants vs the default bf16x6 kernel (9: tile order 2; 10: order 0 gq 16; 11: order 1 gq 32)
                     CK(launch_build_bf16(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, 4, lp_of(ref), wsbf, 0, 0));
                     CK(hipMemset(out, 0xff, tot * 4));
-                    CK(vv == 9 ? bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), wsbf, 0, 0, 2)
-                               : bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), wsbf, 0, vv));
+                    CK(vv == 9    ? bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), wsbf, 0, 0, 2)
+                       : vv == 10 ? bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), wsbf, 0, 0, 0, 0, -1, 16)
+                       : vv == 11 ? bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), wsbf, 0, 0, 1, 0, -1, 32)
+                                  : bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(out), wsbf, 0, vv));
                     std::vector<unsigned> ha(tot), hb(tot);
                     CK(hipMemcpy(ha.data(), out, tot * 4, hipMemcpyDeviceToHost));
                     CK(hipMemcpy(hb.data(), ref, tot * 4, hipMemcpyDeviceToHost));
@@ -246,6 +259,21 @@ int main(int argc, char **argv) {
                 }
             }
 
+        }
+        {  // bf16x6 pack with 2 / 4 records per wave: byte-identical workspaces
+            void *w2;
+            CK(hipMalloc(&w2, wsbfb));
+            for (int rpw : {2, 4}) {
+                CK(hipMemset(wsbf, 0, wsbfb));
+                CK(hipMemset(w2, 0, wsbfb));
+                CK(bf16b::launch_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, wsbf, 0, 0, -1, true, 1));
+                CK(bf16b::launch_pack(f1, NQ, f2, sh.B, sh.D, sh.H, sh.W, w2, 0, 0, -1, true, rpw));
+                std::vector<unsigned char> ha(wsbfb), hb(wsbfb);
+                CK(hipMemcpy(ha.data(), wsbf, wsbfb, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(hb.data(), w2, wsbfb, hipMemcpyDeviceToHost));
+                printf("%-10s bf16x6 pack rpw%d vs default: %s\n", sh.name, rpw, ha == hb ? "byte-identical" : "DIFFER");
+            }
+            CK(hipFree(w2));
         }
         {  // pack variants: byte-identical workspaces
             void *ws2;

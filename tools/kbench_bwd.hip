@@ -108,6 +108,11 @@ int main(int argc, char **argv) {
     vs.push_back({"full T=12", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12); }, {}});
     vs.push_back({"full T=12, no maxima (bf16x6)", [&] { launch(lookup_bwd_fold_kernel<S, 0>, 12, false, 0, &onm); }, {}});
     vs.push_back({"SEP full T=12, no maxima (bf16x6)", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, bytes_sep, &osnm); }, {}});
+    vs.push_back({"SEP LEAN full T=12, no maxima (bf16x6)", [&] { launch(lookup_bwd_fold_kernel<S, 0, true, true>, 12, false, bytes_sep, &osnm); }, {}});
+    vs.push_back({"SEP LEAN T=12, cold", [&] { launch(lookup_bwd_fold_kernel<S, 0, true, true>, 12, false, bytes_sep, &osnm); }, {}});
+    vs.push_back({"SEP LEAN T=12 L2 warm-up", [&] { launch(lookup_bwd_fold_kernel<S, 32, true, true>, 12, false, bytes_sep, &osnm); }, {}});
+    vs.push_back({"SEP LEAN T=12 L2 warm-up, cold", [&] { launch(lookup_bwd_fold_kernel<S, 32, true, true>, 12, false, bytes_sep, &osnm); }, {}});
+    vs.push_back({"LEAN fold only (no zero)", [&] { launch(lookup_bwd_fold_kernel<S, 5, true, true>, 12, false, bytes_sep, &osnm); }, {}});
     vs.push_back({"SEP full T=12", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, bytes_sep, &os); }, {}});
     vs.push_back({"SEP full T=12, LDS padded to 3 WG/CU", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, 52 * 1024, &os); }, {}});
     // "cold": the upstream gradients evicted from the MALL before each launch (a 512 MB memset in
@@ -171,6 +176,21 @@ int main(int argc, char **argv) {
             CK(hipEventElapsedTime(&ms, e0, e1));
             v.us.push_back(ms * 1e3f / PER);
         }
+    {  // the generic fold phase and the LEAN one: dC bit-identical
+        std::vector<unsigned> ref((size_t)B * N * N), got((size_t)B * N * N);
+        launch(lookup_bwd_fold_kernel<S, 0, true, true>, 12, false, bytes_sep, &osnm);
+        CK(hipMemcpy(ref.data(), dc, ref.size() * 4, hipMemcpyDeviceToHost));
+        auto cmp = [&](const char *nm, std::function<void()> run) {
+            CK(hipMemset(dc, 0xff, ref.size() * 4));
+            run();
+            CK(hipMemcpy(got.data(), dc, got.size() * 4, hipMemcpyDeviceToHost));
+            size_t bad = 0;
+            for (size_t i = 0; i < ref.size(); ++i) bad += ref[i] != got[i];
+            printf("check %-28s vs LEAN: %s (%zu mismatches)\n", nm, bad ? "DIFFER" : "bit-identical", bad);
+        };
+        cmp("L2 warm-up", [&] { launch(lookup_bwd_fold_kernel<S, 32, true, true>, 12, false, bytes_sep, &osnm); });
+        cmp("generic fold (SEP, no maxima)", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, bytes_sep, &osnm); });
+    }
     for (auto &v : vs) {
         std::sort(v.us.begin(), v.us.end());
         printf("%-42s median %8.2f us  min %8.2f us\n", v.name.c_str(), v.us[v.us.size() / 2], v.us[0]);
