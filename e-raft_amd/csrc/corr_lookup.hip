@@ -1296,7 +1296,9 @@ struct LaneTable {
 // lookup's LDS writes at the end of each lookup (round 5's s_waitcnt).  (Moving the closed form's
 // y-tap broadcasts, or its previous-column gradients, from DPP to ds_bpermute — LDS pipe
 // instead of VALU — was measured and dropped: T = 12 79 -> 88 / 83 us,
-// profiles/r06f_kbench_bwd_lean.txt.)
+// profiles/r06f_kbench_bwd_lean.txt; so was an L2 warm-up of lookup t + 3's gradient lines, one
+// dword per row by the first workgroup of each 32-query line group: 145 -> 144 us with the
+// gradients evicted before the launch, 79 -> 114 us warm, profiles/r06i_kbench_bwd_l2warm.txt.)
 // SEP: regular windows by the separable closed form (corr_backward's default); false replays
 // grid_sampler_2d_backward's per-tap products bit for bit (CORR_BACKWARD_EXACT_FOLD).
 // (Several query groups per workgroup — 8 or 16 queries, so that the groups' waves would share
@@ -1378,22 +1380,6 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         for (int u = 0; u < S; ++u)
             pv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, goff, u * NQ * 4, 0));
     };
-    // PROBE & 32 (A/B): L2 warm-up of lookup t + 3's upstream-gradient lines by the first workgroup
-    // of each 32-query line group — one dword per row (lane = row), consumed one lookup later
-    float warm[2] = {0.f, 0.f}, warm_prev[2] = {0.f, 0.f};
-    const bool warmer = (PROBE & 32) != 0 && act && (n0 & 31) == 0;
-    auto warmup = [&](int t) {
-        const float *coords, *grad_out;
-        table.get(t, coords, grad_out);
-        const auto rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(grad_out + (size_t)b * L * K * NQ), 0,
-                                                          L * K * NQ * 4, 0x00020000);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int row = lane + 64 * h;
-            const uint32_t off = row < K ? (uint32_t)(((lc * K + row) * NQ + n0) * 4) : kOob;
-            warm[h] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, off, 0, 0));
-        }
-    };
     if (act) prefetch(0);  // issued before the LDS zeroing, so its latency hides behind it
     if (!(PROBE & 4))
         // every map of the workgroup, 16 B per store (o.aux is a multiple of 4 floats)
@@ -1409,10 +1395,6 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         for (int u = 0; u < S; ++u)
             v[u] = kQuadLoads ? __int_as_float(__builtin_amdgcn_ds_bpermute(gsrc, __float_as_int(pv[u]))) : pv[u];
         prefetch(min(t + 1, lk.T - 1));
-        if constexpr ((PROBE & 32) != 0) {
-            warm_prev[0] = warm[0], warm_prev[1] = warm[1];
-            if (warmer && t + 3 < lk.T) warmup(t + 3);
-        }
         const Axis a = tap_axis(cxv, inv_scale, cxl, R, Wl, rdx);
         const Axis c = tap_axis(cyv, inv_scale, cxl, R, Hl, rdy);
         // ---- 2. the (query, level) group's form, decided per group ----
@@ -1688,7 +1670,6 @@ __global__ __launch_bounds__(64 * kFusedLv) void lookup_bwd_fold_kernel(BwdLooku
         // needed: the map writes drain while the next lookup's taps are computed)
         if constexpr ((PROBE & 16) != 0) wave_lds_sync();
         else asm volatile("" ::: "memory");
-        if constexpr ((PROBE & 32) != 0) asm volatile("" ::"v"(warm_prev[0]), "v"(warm_prev[1]));
     }
     __syncthreads();
 

@@ -110,8 +110,6 @@ int main(int argc, char **argv) {
     vs.push_back({"SEP full T=12, no maxima (bf16x6)", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, bytes_sep, &osnm); }, {}});
     vs.push_back({"SEP LEAN full T=12, no maxima (bf16x6)", [&] { launch(lookup_bwd_fold_kernel<S, 0, true, true>, 12, false, bytes_sep, &osnm); }, {}});
     vs.push_back({"SEP LEAN T=12, cold", [&] { launch(lookup_bwd_fold_kernel<S, 0, true, true>, 12, false, bytes_sep, &osnm); }, {}});
-    vs.push_back({"SEP LEAN T=12 L2 warm-up", [&] { launch(lookup_bwd_fold_kernel<S, 32, true, true>, 12, false, bytes_sep, &osnm); }, {}});
-    vs.push_back({"SEP LEAN T=12 L2 warm-up, cold", [&] { launch(lookup_bwd_fold_kernel<S, 32, true, true>, 12, false, bytes_sep, &osnm); }, {}});
     vs.push_back({"LEAN fold only (no zero)", [&] { launch(lookup_bwd_fold_kernel<S, 5, true, true>, 12, false, bytes_sep, &osnm); }, {}});
     vs.push_back({"SEP full T=12", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, bytes_sep, &os); }, {}});
     vs.push_back({"SEP full T=12, LDS padded to 3 WG/CU", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, 52 * 1024, &os); }, {}});
@@ -188,7 +186,6 @@ int main(int argc, char **argv) {
             for (size_t i = 0; i < ref.size(); ++i) bad += ref[i] != got[i];
             printf("check %-28s vs LEAN: %s (%zu mismatches)\n", nm, bad ? "DIFFER" : "bit-identical", bad);
         };
-        cmp("L2 warm-up", [&] { launch(lookup_bwd_fold_kernel<S, 32, true, true>, 12, false, bytes_sep, &osnm); });
         cmp("generic fold (SEP, no maxima)", [&] { launch(lookup_bwd_fold_kernel<S, 0, true>, 12, false, bytes_sep, &osnm); });
     }
     for (auto &v : vs) {
