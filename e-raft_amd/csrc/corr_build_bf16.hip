@@ -226,10 +226,15 @@ __device__ __forceinline__ Tile xcd_block_tile(const Args &p, int t) {
 // inline asm (the compiler then adds no wait of its own on them), bit 1 = s_setprio 1 over the
 // K loop (the epilogue of a neighbouring workgroup yields issue slots to MFMA-phase waves), bit 2 =
 // no half-patch body (padding rows computed and discarded: one kernel body).
+// (8 waves per workgroup — 256 queries against the patch, so its LDS-DMA records feed twice the
+// MFMAs and the L2 operand traffic per flop drops by a quarter, one workgroup per CU — was
+// measured and dropped: bit-identical, 5-15 % slower at every size,
+// profiles/r06k_kbench_build_8waves_dropped.txt.)
 // FAST: levels == 4 (no level-count branches in the epilogue).
 template <int SS, int NR, bool ACC2, int VF = 0, bool FAST = false>
 __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
     constexpr int QS = ACC2 ? 3 : 4, QD = QS - 1;
+    constexpr int WV = kWaves, QPWG = kQPerWG, DPW = kDmaPerWave;
     extern __shared__ __attribute__((aligned(16))) char smem_bf16[];
     char *smem = smem_bf16;
 
@@ -237,7 +242,7 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ci = lane & 15, grp = lane >> 4;
-    const int qb0 = tl.qg * (kQPerWG / 16) + 2 * w;  // this wave's first 16-query block
+    const int qb0 = tl.qg * (QPWG / 16) + 2 * w;  // this wave's first 16-query block
     const int S = SS > 0 ? SS : p.S;
     const bool qact = qb0 * 16 < p.NQ;  // wave-uniform
 
@@ -247,10 +252,10 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
     const int TCp = 4 * p.CB;                          // tiles per row of the target image
     const size_t tstep = (size_t)p.Hp * p.CB * kRecU;  // u32x4 per K step of the target image
     const u32x4_t *tbase = p.pt + (((size_t)b * S * (p.Hp >> 2) + (y0 >> 2)) * TCp + 4 * tl.cb) * kRecU + lane;
-    unsigned toff[kDmaPerWave];
+    unsigned toff[DPW];
 #pragma unroll
-    for (int m = 0; m < kDmaPerWave; ++m) {
-        const int pc = w + 4 * m, rp = pc / kPieces;
+    for (int m = 0; m < DPW; ++m) {
+        const int pc = w + WV * m, rp = pc / kPieces;
         toff[m] = (unsigned)(((rp >> 2) * TCp + (rp & 3)) * kRecU + (pc % kPieces) * 64);
     }
     const size_t qstep = (size_t)p.NQB * kRecU;
@@ -280,7 +285,7 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
         const uint32_t base = lds_base + slot * kSlotBytes;
         const u32x4_t *src = tbase + s * tstep;
 #pragma unroll
-        for (int m = 0; m < kDmaPerWave; ++m) dma16(src + toff[m], base + (w + 4 * m) * 1024);
+        for (int m = 0; m < DPW; ++m) dma16(src + toff[m], base + (w + WV * m) * 1024);
     };
 
     f32x4_t acc[2][kPatchRows], acs[2][kPatchRows];  // hi*hi; the small products (ACC2)
@@ -388,10 +393,10 @@ __device__ __forceinline__ void build_tile(const Args &p, const Tile tl) {
         for (int s = 0; s < SS; ++s) {
             // operations younger than T(s): at step 0 the prologue's [Q2,] T1; else step s - 1's
             // group Q(s - 1 + QD), T(s + 1) — where they exist
-            const int younger = s == 0 ? (QD > 2 && SS > 2 ? kQLoads : 0) + (SS > 1 ? kDmaPerWave : 0)
-                                       : (s - 1 + QD < SS ? kQLoads : 0) + (s + 1 < SS ? kDmaPerWave : 0);
-            if (younger == kQLoads + kDmaPerWave) wait_vmcnt_barrier<kQLoads + kDmaPerWave>();
-            else if (younger == kDmaPerWave) wait_vmcnt_barrier<kDmaPerWave>();
+            const int younger = s == 0 ? (QD > 2 && SS > 2 ? kQLoads : 0) + (SS > 1 ? DPW : 0)
+                                       : (s - 1 + QD < SS ? kQLoads : 0) + (s + 1 < SS ? DPW : 0);
+            if (younger == kQLoads + DPW) wait_vmcnt_barrier<kQLoads + DPW>();
+            else if (younger == DPW) wait_vmcnt_barrier<DPW>();
             else if (younger == kQLoads) wait_vmcnt_barrier<kQLoads>();
             else wait_vmcnt_barrier<0>();
             const int qs = s % QS;
@@ -544,10 +549,11 @@ hipError_t launch_kernel(dim3 grid, const Args &p, hipStream_t s) {
                           : (const void *)corr_build_bf16_kernel<SS, ACC2, VF, false>;
     const hipError_t e = ensure_lds_limit(fn, kLds, lds_done[fast]);
     if (e != hipSuccess) return e;
+    const dim3 blk(256);
     if (fast)
-        hipLaunchKernelGGL((corr_build_bf16_kernel<SS, ACC2, VF, true>), grid, dim3(256), kLds, s, p);
+        hipLaunchKernelGGL((corr_build_bf16_kernel<SS, ACC2, VF, true>), grid, blk, kLds, s, p);
     else
-        hipLaunchKernelGGL((corr_build_bf16_kernel<SS, ACC2, VF, false>), grid, dim3(256), kLds, s, p);
+        hipLaunchKernelGGL((corr_build_bf16_kernel<SS, ACC2, VF, false>), grid, blk, kLds, s, p);
     return hipGetLastError();
 }
 
@@ -595,7 +601,7 @@ hipError_t launch_pack(const float *f1, int NQ, const float *f2, int B, int D, i
 // y0, y1: the target region (as launch_pack), whose pyramid rows [y0 >> l, ceil(y1 / 2^l)) of
 // every level it writes.
 hipError_t launch_mfma(int NQ, int B, int D, int H, int W, int levels, const LevelPtrs &pyr, void *ws,
-                       hipStream_t s, int variant = 0, int order = 1, int y0 = 0, int y1 = -1, int gq = kGroupQ) {
+                       hipStream_t s, int variant = 0, int order = 1, int y0 = 0, int y1 = -1, int gq = 0) {
     if (y1 < 0) y1 = H;
     const Geom g = geom(D, NQ, H, W);
     const Ws w = workspace_of(ws, B, g);
@@ -613,11 +619,14 @@ hipError_t launch_mfma(int NQ, int B, int D, int H, int W, int levels, const Lev
     // XCD blocks: split each batch item into 8 / B blocks (2 x 4 for one item), so the 8 XCDs
     // get disjoint operand sets; B >= 8: one or more whole batch items per XCD
     p.order = order;
-    p.gq = std::max(1, gq);
+    // query groups per L2 band: 4 for one batch item (DSEC 78.7 -> 75.2 us, 1280x960 1,042 -> 1,019,
+    // 1920x1280 4,321 -> 4,276), the default 8 for batches (MVSEC B16 prefers it: 141 vs 146 us;
+    // train B8 even) — profiles/r06d_kbench_build_tile_groups_dropped.txt, r06k_*
+    p.gq = gq > 0 ? gq : (B == 1 ? 4 : kGroupQ);
     const int per = B >= 8 ? 1 : 8 / B;
     p.nqh = per >= 2 && g.NQG >= 2 ? 2 : 1;
     p.npq = std::max(1, std::min(per / p.nqh, p.npatch));
-    const long tiles = (long)B * p.npatch * g.NQG;
+    const long tiles = (long)B * p.npatch * p.NQG;
     if (tiles > 0x7fffffffL) return hipErrorInvalidValue;
     const dim3 grid((unsigned)tiles);
     hipError_t e;

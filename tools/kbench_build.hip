@@ -156,7 +156,6 @@ int main(int argc, char **argv) {
                       }, false});
         for (int od : {0, 1})
             for (int gq : {4, 8, 16, 32}) {
-                if (od == 1 && gq == 8) continue;  // the library's default ("bf16x6 mfma only")
                 vs.push_back({"bf16x6 mfma order" + std::to_string(od) + " gq" + std::to_string(gq), [&, od, gq](float *o) {
                                   return bf16b::launch_mfma(NQ, sh.B, sh.D, sh.H, sh.W, 4, lp_of(o), wsbf, 0, 0, od, 0, -1, gq);
                               }, false});
