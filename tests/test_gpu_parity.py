@@ -811,6 +811,9 @@ def test_lookup_bwd_multi_and_fold_bitexact(T, B, H, W, L, r):
 @pytest.mark.parametrize("algo", ["bf16x6", "f16x3", "fp32"])
 @pytest.mark.parametrize("B,D,H,W,L,r,T", [(2, 32, 18, 24, 4, 4, 5), (1, 20, 17, 23, 3, 3, 2), (1, 16, 17, 23, 4, 4, 3),
                                            (8, 64, 36, 48, 4, 4, 12),
+                                           # the lean fold's edges: odd H (last level-0 row unpooled), W / 4 odd
+                                           # (last level-2 column unpooled), W / 8 = 2
+                                           (2, 16, 17, 20, 4, 4, 4),
                                            (1, 16, 12, 16, 4, 4, 33), (1, 16, 60, 80, 4, 4, 3),
                                            (1, 16, 64, 96, 5, 2, 2), (1, 8, 120, 160, 4, 4, 2)])
 def test_corr_backward_matches_staged_path(algo, B, D, H, W, L, r, T, exact):
