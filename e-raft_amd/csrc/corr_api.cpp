@@ -87,7 +87,7 @@ using namespace corr;
 
 extern "C" {
 
-int corr_version(void) { return 201; }
+int corr_version(void) { return 202; }
 
 const char *corr_last_error(void) { return g_err; }
 

@@ -32,7 +32,7 @@ EXPORTS = ("corr_version", "corr_last_error", "corr_build", "corr_lookup", "corr
            "corr_backward", "corr_convex_upsample_bwd_workspace", "corr_convex_upsample_bwd", "corr_build_region",
            "corr_lookup_conv_bwd_workspace", "corr_lookup_conv_bwd", "corr_map_floats", "corr_pyramid_export",
            "corr_pyramid_import")
-ABI_VERSION = 201  # include/corr_mi355x.h: the tiled value pyramid; separable fold by default
+ABI_VERSION = 202  # include/corr_mi355x.h: tiled value pyramid, separable fold, fp32 non-finite rule (bf16x6 bwd)
 
 # Build algorithms (include/corr_mi355x.h).  BF16X6 is the default: every fp32 feature split
 # exactly into three bf16 pieces, the six largest piece products on the bf16 MFMA, fp32

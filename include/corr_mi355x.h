@@ -60,7 +60,10 @@ extern "C" {
  *        16-B aligned levels, corr_map_floats per map); corr_map_floats, corr_pyramid_export,
  *        corr_pyramid_import.  Gradient pyramids keep the reference layout.
  *   201: corr_backward's fused fold takes the separable closed form by default (dC within ~1e-7
- *        of the staged path, not bitwise); CORR_BACKWARD_EXACT_FOLD restores the bit-exact replay. */
+ *        of the staged path, not bitwise); CORR_BACKWARD_EXACT_FOLD restores the bit-exact replay.
+ *   202: the CORR_BUILD_BF16X6 backward GEMMs (corr_build_bwd_ex, corr_backward) give the fp32
+ *        reference's results for non-finite inputs (+-inf where fp32 has +-inf; NaN only where it
+ *        has NaN) instead of NaN for every output an infinity reaches. */
 int corr_version(void);
 
 /* Thread-local description of the last error on this thread ("" if none). */

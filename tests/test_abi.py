@@ -35,7 +35,7 @@ def test_every_declared_symbol_is_exported(lib):
 
 
 def test_version_and_workspace(lib):
-    assert lib.corr_version() == 201
+    assert lib.corr_version() == 202
     # DSEC: 256 x 4800 slabs; at least one slab, deterministic plan
     ws = lib.corr_build_bwd_workspace(1, 256, 60, 80)
     assert ws >= 256 * 4800 * 4 and ws % (256 * 4800 * 4) == 0
