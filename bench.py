@@ -96,9 +96,9 @@ WORKLOADS = {
 CPU_SKIP = {"hires1280", "hires1920"}  # a CPU pair takes tens of seconds and >10 GB
 TRAIN_WORKLOADS = {"train"}
 # The default (DSEC) line also measures these BASELINE configs, one `workloads` entry each
-# (config 4 train, config 3 MVSEC B16, config 5's 1280x960 size), so the driver's own run times
-# them; --no-workloads skips them.
-EXTRA_WORKLOADS = ("train", "mvsec", "hires1280")
+# (config 4 train, config 3 MVSEC B16, config 5's 1280x960 size, config 2 the full E-RAFT forward),
+# so the driver's own run times them; --no-workloads skips them.
+EXTRA_WORKLOADS = ("train", "mvsec", "hires1280", "e2e")
 ACHIEVABLE_HBM_GBS = 6290.0  # MI355X_MICROARCH.md: measured achievable HBM read bandwidth
 # The lookup's measured latency floor per workload: the same launch with neither the window
 # loads nor the output stores (coords load, taps, barriers, graph launch), i.e. what no change of
@@ -246,11 +246,12 @@ def cpu_baseline(workload, budget_s, train=False, threads=None):
                       f"{cpu}"}
 
 
-def run_e2e(args, world, rank, dev):
+def run_e2e(args, world, rank, dev, role="primary"):
     """BASELINE config 2: full E-RAFT forward (encoders on MIOpen, the HIP CorrBlock, 12 GRU
     iterations, convex upsampling) on 15-bin voxel pairs at 480x640, warm start (flow_init at
     1/8 resolution), random-init weights.  One step = one frame pair, replayed from one HIP
-    graph (--eager: launched op by op)."""
+    graph (--eager: launched op by op).  role "workload": return the result (an entry of the
+    DSEC line's `workloads`, CPU baseline on half the budget) instead of printing it."""
     from eraft_amd.model import ERAFT
     torch.manual_seed(0)
     bins, H, W, iters = 15, 480, 640, 12
@@ -314,8 +315,11 @@ def run_e2e(args, world, rank, dev):
                    "parallelism": f"replicas x{world}"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_e2e(model, im1, im2, finit, iters, args.cpu_seconds)
+        budget = args.cpu_seconds * (0.5 if role == "workload" else 1.0)
+        res["cpu_baseline"] = cpu_e2e(model, im1, im2, finit, iters, budget)
         res["speedup_vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
+    if role == "workload":
+        return res
     if rank == 0:
         emit(res)
 
@@ -522,15 +526,17 @@ def main():
     else:
         res = run_corr(args, args.workload, args.sharded, world, rank, dev)
         if world == 1 and not args.sharded and args.workload == "dsec" and not args.no_workloads:
-            # BASELINE configs 3, 4 and 5 measured in the same (driver) run, beside `value`
+            # BASELINE configs 2, 3, 4 and 5 measured in the same (driver) run, beside `value`
             res["workloads"] = {}
             for wl in EXTRA_WORKLOADS:
                 torch.cuda.empty_cache()
                 t_w = time.perf_counter()
                 try:
-                    ent = run_corr(args, wl, False, world, rank, dev, role="workload")
-                    for k in ("metric", "unit", "n_gpus", "higher_is_better", "vs_baseline", "data", "dtype",
-                              "scaling", "build_arith", "kernel_timing", "warmup"):
+                    ent = (run_e2e(args, world, rank, dev, role="workload") if wl == "e2e" else
+                           run_corr(args, wl, False, world, rank, dev, role="workload"))
+                    same = ("metric", "unit", "higher_is_better") if wl != "e2e" else ()
+                    for k in same + ("n_gpus", "vs_baseline", "data", "dtype",
+                                     "scaling", "build_arith", "kernel_timing", "warmup"):
                         ent.pop(k, None)
                 except Exception as exc:  # noqa: BLE001 — the DSEC line stands; say why the entry is missing
                     ent = {"error": f"{type(exc).__name__}: {exc}"}
