@@ -21,7 +21,8 @@ Rank 0 at N=1 also times the reference op sequence on the host CPU (oracle/torch
 a bounded sample: ``cpu_baseline``.  At N=1 the DSEC line also carries ``workloads``: the same
 measurement (value, ms_per_step, roofline, roofline_lookup; train: backward_kernels; train and
 mvsec: cpu_baseline) for BASELINE config 4 (train, B8 36x48 forward + backward), config 3
-(mvsec, B16 36x44) and config 5's 1280x960 size (hires1280), each in the same process.
+(mvsec, B16 36x44), config 5's 1280x960 and 1920x1280 sizes on one GPU (hires1280, hires1920)
+and config 2 (e2e: the full E-RAFT forward, with its CPU baseline), each in the same process.
 """
 from __future__ import annotations
 
@@ -96,9 +97,10 @@ WORKLOADS = {
 CPU_SKIP = {"hires1280", "hires1920"}  # a CPU pair takes tens of seconds and >10 GB
 TRAIN_WORKLOADS = {"train"}
 # The default (DSEC) line also measures these BASELINE configs, one `workloads` entry each
-# (config 4 train, config 3 MVSEC B16, config 5's 1280x960 size, config 2 the full E-RAFT forward),
+# (config 4 train, config 3 MVSEC B16, config 5's 1280x960 and 1920x1280 sizes on one GPU, config 2
+# the full E-RAFT forward),
 # so the driver's own run times them; --no-workloads skips them.
-EXTRA_WORKLOADS = ("train", "mvsec", "hires1280", "e2e")
+EXTRA_WORKLOADS = ("train", "mvsec", "hires1280", "hires1920", "e2e")
 ACHIEVABLE_HBM_GBS = 6290.0  # MI355X_MICROARCH.md: measured achievable HBM read bandwidth
 # The lookup's measured latency floor per workload: the same launch with neither the window
 # loads nor the output stores (coords load, taps, barriers, graph launch), i.e. what no change of
@@ -129,7 +131,7 @@ def parse():
     ap.add_argument("--no-sharded-leg", action="store_true",
                     help="N > 1 dsec: skip the row-sharded 1280x960 leg reported beside the replica value")
     ap.add_argument("--no-workloads", action="store_true",
-                    help="N = 1 dsec: skip the train / mvsec / hires1280 entries of `workloads`")
+                    help="N = 1 dsec: skip the train / mvsec / hires1280 / hires1920 / e2e entries of `workloads`")
     return ap.parse_args()
 
 
