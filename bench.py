@@ -105,8 +105,9 @@ ACHIEVABLE_HBM_GBS = 6290.0  # MI355X_MICROARCH.md: measured achievable HBM read
 # The lookup's measured latency floor per workload: the same launch with neither the window
 # loads nor the output stores (coords load, taps, barriers, graph launch), i.e. what no change of
 # memory traffic can remove (tools/kbench_lookup.hip "abl QB32 noload nostore",
-# profiles/r05t_kbench_lookup_ablations.txt, median us).
-LOOKUP_NOLOAD_NOSTORE_US = {"dsec": 4.19, "mvsec": 11.49, "train": 6.86, "hires1280": 8.54}
+# profiles/r05t_kbench_lookup_ablations.txt; 1920x1280: profiles/r06za_kbench_lookup_1920.txt; median us).
+LOOKUP_NOLOAD_NOSTORE_US = {"dsec": 4.19, "mvsec": 11.49, "train": 6.86, "hires1280": 8.54, "hires1920": 14.78}
+LOOKUP_FLOOR_SOURCE = {"hires1920": "profiles/r06za_kbench_lookup_1920.txt"}
 
 
 def parse():
@@ -437,7 +438,7 @@ def lookup_ceiling(wl_name, lb, look_ms, traffic_b):
     if fl:
         gbs = lb / (fl * 1e-6) / 1e9
         out["latency_floor"] = {"noload_nostore_us": fl, "frac": round(gbs / PEAK_HBM_GBS, 4),
-                                "source": "profiles/r05t_kbench_lookup_ablations.txt"}
+                                "source": LOOKUP_FLOOR_SOURCE.get(wl_name, "profiles/r05t_kbench_lookup_ablations.txt")}
     if traffic_b:
         r = min(1.0, lb / traffic_b)
         out["line_granularity"] = {"algorithmic_over_counted": round(r, 4),

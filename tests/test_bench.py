@@ -64,7 +64,9 @@ def test_lookup_ceiling_binds_the_lower_bound():
     frac = lb / 0.0055e-3 / 1e9 / bench.PEAK_HBM_GBS
     assert c["frac_of_ceiling"] == pytest.approx(frac / min(floor, gran), abs=1e-3)
     # no floor measured and no PMC pass: no ceiling claimed
-    assert bench.lookup_ceiling("hires1920", lb, 0.03, None) == {}
+    assert bench.lookup_ceiling("mvsec_crop", lb, 0.03, None) == {}
+    # every workload the default line measures has a measured floor
+    assert all(w in bench.LOOKUP_NOLOAD_NOSTORE_US for w in bench.EXTRA_WORKLOADS if w != "e2e")
 
 
 def test_traffic_reads_the_newest_committed_pmc_pass():

@@ -85,7 +85,7 @@ int main(int argc, char **argv) {
     constexpr int PER = 12;  // one frame pair's worth of lookups per sample
     std::vector<Shape> shapes = {{"dsec", 1, 60, 80}, {"mvsec-pad", 16, 36, 44}, {"train", 8, 36, 48},
                                  {"1280x960", 1, 120, 160}, {"mvsec-crop", 16, 32, 32}, {"train-b4", 4, 36, 48},
-                                 {"train-b12", 12, 36, 48}};
+                                 {"train-b12", 12, 36, 48}, {"1920x1280", 1, 160, 240}};
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
